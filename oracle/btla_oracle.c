@@ -1,0 +1,730 @@
+/*
+ * btla_oracle.c -- scalar C restatement of the reference's WOQ packing / dequant / GEMV algorithms.
+ * TEST INFRASTRUCTURE ONLY (see btla_oracle.h).  Each function cites the reference file:line it follows,
+ * relative to /root/reference.
+ */
+#include "btla_oracle.h"
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ------------------------------------------------------------------ scalar helpers */
+typedef union {
+  float f;
+  uint32_t u;
+} f32u;
+
+/* bestla_utils.h:146-153 bf16::fromfloat: tmp.u += 0x7fff + lsb (no NaN special-case) */
+uint16_t orc_f32_to_bf16(float v) {
+  f32u t;
+  t.f = v;
+  uint32_t lsb = (t.u >> 16) & 1u;
+  t.u += 0x7fffu + lsb;
+  return (uint16_t)(t.u >> 16);
+}
+
+float orc_bf16_to_f32(uint16_t x) {
+  f32u t;
+  t.u = ((uint32_t)x) << 16;
+  return t.f;
+}
+
+/* bestla_utils.h:184-196 fp16::operator=(float) */
+uint16_t orc_f32_to_fp16_bestla(float val) {
+  f32u t;
+  t.f = val;
+  const uint32_t b = t.u + 0x00001000u;
+  const uint32_t e = (b & 0x7F800000u) >> 23;
+  const uint32_t m = b & 0x007FFFFFu;
+  return (uint16_t)((b & 0x80000000u) >> 16 | (e > 112) * ((((e - 112) << 10) & 0x7C00u) | m >> 13) |
+                    ((e < 113) & (e > 101)) * ((((0x007FF000u + m) >> (125 - e)) + 1) >> 1) | (e > 143) * 0x7FFFu);
+}
+
+/* IEEE-754 binary16 round-to-nearest-even (vcvtps2ph with RNE on AVX512-FP16/F16C hosts) */
+uint16_t orc_f32_to_fp16_rne(float v) {
+  f32u t;
+  t.f = v;
+  uint32_t x = t.u;
+  uint32_t sign = (x >> 16) & 0x8000u;
+  uint32_t ax = x & 0x7FFFFFFFu;
+  if (ax > 0x7F800000u) return (uint16_t)(sign | 0x7E00u | ((ax >> 13) & 0x3FFu)); /* NaN */
+  if (ax >= 0x477FF000u) return (uint16_t)(sign | 0x7C00u);                         /* overflow -> inf */
+  if (ax < 0x38800000u) {                                                            /* subnormal / zero */
+    if (ax < 0x33000000u) return (uint16_t)sign;
+    uint32_t e = ax >> 23;
+    uint32_t mant = (ax & 0x7FFFFFu) | 0x800000u;
+    uint32_t shift = 126 - e; /* 14..24 */
+    uint32_t q = mant >> shift;
+    uint32_t rem = mant & ((1u << shift) - 1);
+    uint32_t half = 1u << (shift - 1);
+    if (rem > half || (rem == half && (q & 1u))) q++;
+    return (uint16_t)(sign | q);
+  }
+  uint32_t e = (ax >> 23) - 112;
+  uint32_t mant = ax & 0x7FFFFFu;
+  uint32_t q = (e << 10) | (mant >> 13);
+  uint32_t rem = mant & 0x1FFFu;
+  if (rem > 0x1000u || (rem == 0x1000u && (q & 1u))) q++;
+  return (uint16_t)(sign | q);
+}
+
+/* bestla_utils.h:197-206 explicit operator float */
+float orc_fp16_to_f32(uint16_t x) {
+  const uint32_t e = (x & 0x7C00u) >> 10;
+  const uint32_t m = (uint32_t)(x & 0x03FFu) << 13;
+  f32u mv;
+  mv.f = (float)m;
+  const uint32_t v = mv.u >> 23;
+  f32u r;
+  r.u = ((uint32_t)(x & 0x8000u)) << 16 | (e != 0) * ((e + 112) << 23 | m) |
+        ((e == 0) & (m != 0)) * ((v - 37) << 23 | ((m << (150 - v)) & 0x007FE000u));
+  return r.f;
+}
+
+/* std::max / std::min semantics (first argument wins unless strictly ordered) */
+static inline float smax(float a, float b) { return (a < b) ? b : a; }
+static inline float smin(float a, float b) { return (b < a) ? b : a; }
+
+/* float -> int32 as x86 cvttss2si: NaN / out-of-range -> INT32_MIN */
+static inline int32_t f2i_x86(float x) {
+  if (isnan(x) || x >= 2147483648.0f || x < -2147483648.0f) return INT32_MIN;
+  return (int32_t)x;
+}
+static inline int32_t iadd_wrap(int32_t a, int32_t b) { return (int32_t)((uint32_t)a + (uint32_t)b); }
+
+/* bestla_utils.h:507-512 cast<float,int8_t>: roundf then clamp to [-128,127] */
+static inline int8_t cast_f32_s8(float v) {
+  v = roundf(v);
+  v = smin(v, 127.f);
+  v = smax(v, -128.f);
+  return (int8_t)f2i_x86(v);
+}
+/* bestla_utils.h:522-525 cast<float,int>: int(roundf) */
+static inline int32_t cast_f32_int(float v) { return f2i_x86(roundf(v)); }
+
+/* ------------------------------------------------------------------ quantizer */
+/* kernel_ref.h:1608-1719.  dispatch_calc always takes the sNauto_* lambdas for integer types. */
+void orc_quantize_rowblock(const float* srcptr, int8_t* dstptr, int row, int col, int ld_src, int ld_dst,
+                           float* scales, int8_t* zero_points, int blocksize, int bits) {
+  const int raw_blocksize = blocksize;
+  const int FullValue = 1 << (bits - 1);
+  const int SymValue = FullValue - 1;
+#define CLIPV(s) ((s) < -FullValue ? -FullValue : ((s) > SymValue ? SymValue : (s)))
+  for (int i = 0; i < col; i++) {
+    int align_row_loop = row / blocksize * blocksize;
+    int j = 0;
+    while (j < row) {
+      int bs = (j < align_row_loop) ? blocksize : row - align_row_loop;
+      if (zero_points == NULL) {
+        /* sNauto_calc_store_scale_and_quantv_sym, kernel_ref.h:1650-1671 */
+        float maxval = 1.17549435e-38f; /* std::numeric_limits<float>::min() */
+        float minval = 3.40282347e+38f;
+        float absmax = 0.f;
+        for (int ij = 0; ij < bs; ij++) {
+          float x = srcptr[(size_t)(j + ij) * ld_src + i];
+          maxval = smax(maxval, x);
+          minval = smin(minval, x);
+          absmax = smax(absmax, fabsf(x));
+        }
+        float NVal = (float)SymValue + 0.5f;
+        float sum = maxval + minval;
+        if (fabsf(sum) >= absmax / (float)FullValue) {
+          NVal = sum > 0.f ? (float)(-FullValue) : (float)FullValue;
+        }
+        float scale = absmax / NVal;
+        float rscale = 1.f / scale;
+        scales[(size_t)(j / raw_blocksize) * ld_dst + i] = scale;
+        for (int ij = 0; ij < bs; ij++) {
+          int v = cast_f32_s8(srcptr[(size_t)(j + ij) * ld_src + i] * rscale);
+          dstptr[(size_t)(j + ij) * ld_dst + i] = (int8_t)CLIPV(v);
+        }
+      } else {
+        /* sNauto_calc_store_scale_and_quantv_asym, kernel_ref.h:1673-1693 */
+        float maxval = 0.f, minval = 0.f;
+        for (int ij = 0; ij < bs; ij++) {
+          float x = srcptr[(size_t)(j + ij) * ld_src + i];
+          maxval = smax(maxval, x);
+          minval = smin(minval, x);
+        }
+        float scale = (maxval - minval) / (float)((1 << bits) - 1);
+        float rscale = 1.f / scale;
+        scales[(size_t)(j / raw_blocksize) * ld_dst + i] = scale;
+        int32_t bzp = iadd_wrap(cast_f32_int((0 - minval) * rscale), -FullValue);
+        bzp = CLIPV(bzp);
+        zero_points[(size_t)(j / raw_blocksize) * ld_dst + i] = (int8_t)bzp;
+        for (int ij = 0; ij < bs; ij++) {
+          int32_t t = iadd_wrap(cast_f32_int(srcptr[(size_t)(j + ij) * ld_src + i] * rscale), bzp);
+          t = CLIPV(t);
+          dstptr[(size_t)(j + ij) * ld_dst + i] = (int8_t)t;
+        }
+      }
+      j += bs;
+    }
+  }
+#undef CLIPV
+}
+
+/* ------------------------------------------------------------------ interleave / compress */
+/* kernel_ref.h:39-59 */
+void orc_padding_interleave(const int8_t* src, int8_t* dst, int row, int col, int rowpad, int colpad, int src_step,
+                            int dst_step, int ntile, int rowpack) {
+  for (int i = 0; i < rowpad; i += rowpack)
+    for (int j = 0; j < colpad; j += ntile)
+      for (int jj = 0; jj < ntile; jj++)
+        for (int ii = 0; ii < rowpack; ii++)
+          dst[(size_t)i * ntile + (size_t)j * dst_step + jj * rowpack + ii] =
+              ((i + ii) < row && (j + jj) < col) ? src[(size_t)(i + ii) * src_step + (j + jj)] : 0;
+}
+
+/* kernel_ref.h:62-80 */
+void orc_revert_padding_interleave(const int8_t* src, int8_t* dst, int row, int col, int rowpad, int colpad,
+                                   int src_step, int dst_step, int ntile, int rowpack) {
+  for (int i = 0; i < rowpad; i += rowpack)
+    for (int j = 0; j < colpad; j += ntile)
+      for (int jj = 0; jj < ntile; jj++)
+        if ((j + jj) < col)
+          for (int ii = 0; ii < rowpack; ii++)
+            if ((i + ii) < row)
+              dst[(size_t)(i + ii) * dst_step + (j + jj)] =
+                  src[(size_t)i * ntile + (size_t)j * src_step + jj * rowpack + ii];
+}
+
+/* kernel_ref.h:155-165: int4x2 {x: low nibble, y: high nibble} = value + 8 */
+void orc_compress_s4(const int8_t* src, uint8_t* dst, size_t n) {
+  for (size_t i = 0; i < n; i += 2)
+    dst[i / 2] = (uint8_t)(((uint8_t)(src[i] + 8) & 0xF) | (((uint8_t)(src[i + 1] + 8) & 0xF) << 4));
+}
+/* kernel_ref.h:330-341: bit2x4 {a,b,c,d} LSB..MSB = value + 2 */
+void orc_compress_s2(const int8_t* src, uint8_t* dst, size_t n) {
+  for (size_t i = 0; i < n; i += 4) {
+    uint8_t v = 0;
+    for (int t = 0; t < 4; t++) v |= (uint8_t)(((uint8_t)(src[i + t] + 2) & 0x3) << (2 * t));
+    dst[i / 4] = v;
+  }
+}
+/* kernel_ref.h:471-479 */
+void orc_decompress_s4(const uint8_t* src, int8_t* dst, size_t n) {
+  for (size_t i = 0; i < n; i += 2) {
+    dst[i] = (int8_t)((src[i / 2] & 0xF) - 8);
+    dst[i + 1] = (int8_t)((src[i / 2] >> 4) - 8);
+  }
+}
+/* kernel_ref.h:499-509 */
+void orc_decompress_s2(const uint8_t* src, int8_t* dst, size_t n) {
+  for (size_t i = 0; i < n; i += 4)
+    for (int t = 0; t < 4; t++) dst[i + t] = (int8_t)(((src[i / 4] >> (2 * t)) & 3) - 2);
+}
+
+/* ------------------------------------------------------------------ core ids */
+/* BTLA_ISA (bestla.h:23-36): AVX2=2, AVX_VNNI=3, AVX512F=4, AVX512BW=5, AVX512_VNNI=6, AMX_BF16=9, AMX_INT8=10,
+   AMX_FP16=11.  CompType (bestla_gemm.h:22-50): FP32=0x000, BF16_FP32=0x011, FP16_FP32=0x022,
+   INT8_US_FP32=0x034.  make_core_id: NTILE | PACKROW<<8 | COMP<<16 | ISA<<32 (bestla_gemm.h:91). */
+static uint64_t mkid(int nt, int pr, int comp, int isa) {
+  return (uint64_t)nt | ((uint64_t)pr << 8) | ((uint64_t)comp << 16) | ((uint64_t)isa << 32);
+}
+uint64_t orc_core_id(const char* name) {
+  if (!strcmp(name, "avx2")) return mkid(24, 1, 0x000, 2);
+  if (!strcmp(name, "avx512f")) return mkid(48, 1, 0x000, 4);
+  if (!strcmp(name, "amx_bf16")) return mkid(48, 2, 0x011, 9);
+  if (!strcmp(name, "amx_fp16")) return mkid(48, 2, 0x022, 11);
+  if (!strcmp(name, "avx512_vnni_kblock")) return mkid(48, 4, 0x034, 6);
+  if (!strcmp(name, "avx512bw_kblock")) return mkid(48, 4, 0x034, 5);
+  if (!strcmp(name, "avx_vnni_kblock")) return mkid(24, 4, 0x034, 3);
+  if (!strcmp(name, "avx2_vnni_kblock")) return mkid(24, 4, 0x034, 2);
+  if (!strcmp(name, "amx_int8_kblock")) return mkid(48, 4, 0x034, 10);
+  return 0;
+}
+int orc_core_ntile(uint64_t id) { return (int)(id & 0xff); }
+int orc_core_packrow(uint64_t id) { return (int)((id >> 8) & 0xff); }
+int orc_core_is_int(uint64_t id) {
+  int b = (int)((id >> 16) & 0xf0) >> 4; /* CompTypeHelper::get_B, bestla_gemm.h:66-79 */
+  return b == 3 || b == 4;
+}
+int orc_core_ktile(uint64_t id) {
+  int isa = (int)((id >> 32) & 0xff);
+  int pr = orc_core_packrow(id);
+  if (pr == 1) return 1;                /* Avx2N8P1 / Avx512fN16P1: KTILE 1 */
+  if (isa == 9 || isa == 11) return 32; /* Amxbf16N16P2 / Amxfp16N16P2 */
+  if (isa == 10) return 64;             /* Amxint8N16P4 */
+  return 4;                             /* VNNI / BW KBlock cores */
+}
+
+uint64_t orc_select_core(int comp_type, uint32_t qtype, int bs, int asym, int profile) {
+  int amx = profile == 0, vnni = profile <= 1, a512 = profile <= 2;
+  int is_int = ((qtype >> 8) & 0xff) == 1;
+  switch (comp_type) {
+    case 4: /* NE_COMP_INT8 */
+      if (is_int && !(qtype == ORC_S8 && asym)) {
+        if (amx && bs % 64 == 0) return orc_core_id("amx_int8_kblock");
+        if (vnni && bs % 4 == 0) return orc_core_id("avx512_vnni_kblock");
+        if (a512 && bs % 4 == 0) return orc_core_id("avx512bw_kblock");
+        if (bs % 4 == 0) return orc_core_id("avx2_vnni_kblock");
+      }
+      /* fallthrough */
+    case 2: /* NE_COMP_BF16 */
+      if (amx && bs % 32 == 0) return orc_core_id("amx_bf16");
+      /* fallthrough */
+    case 3: /* NE_COMP_F16: AMX-FP16 absent on every profile here */
+    case 1:
+    case 0:
+      if (a512) return orc_core_id("avx512f");
+      return orc_core_id("avx2");
+    default:
+      return 0;
+  }
+}
+
+/* ------------------------------------------------------------------ blob layout */
+static int dtype_bits(uint32_t t) { return (int)(t & 0xff); }
+static size_t dtype_bytes(uint32_t t) { return (size_t)((t & 0xff) / 8); }
+static size_t updiv(size_t a, size_t b) { return (a + b - 1) / b; }
+static size_t padto(size_t a, size_t b) { return updiv(a, b) * b; }
+
+typedef struct {
+  int npad, kpad, n, k, bs, dq_bs;
+  uint32_t prologue, dtype, scat, zpt, redt;
+  uint64_t coreid;
+  int cstep;
+  size_t csize, msize;
+  int asym, has_red, has_shf;
+  size_t q_size, s_size, z_size, r_size, shf_size;
+  /* offsets from blob base */
+  size_t q_off, s_off, z_off, r_off, shf_off;
+} blob_t;
+
+/* StorageWeightKBlockNInteger::resize (bestla_storage.h:725-753) + createStorage (bestla_prologue_b.h:120-127) */
+static void blob_describe(blob_t* b, int n, int k, int blocksize, uint32_t qtype, uint32_t stype, int asym,
+                          uint64_t coreid, int shuffle) {
+  memset(b, 0, sizeof(*b));
+  int ktile = orc_core_ktile(coreid), ntile = orc_core_ntile(coreid);
+  b->kpad = (int)padto((size_t)k, (size_t)ktile);
+  b->npad = (int)padto((size_t)n, (size_t)ntile);
+  b->n = n;
+  b->k = k;
+  b->bs = blocksize <= 0 ? b->kpad : blocksize;
+  b->prologue = 1; /* BTLA_PROLOGUEB_IDS::WeightKBlockNInteger (bestla.h:91-102) */
+  b->coreid = coreid;
+  b->dtype = qtype;
+  b->scat = stype;
+  b->zpt = ORC_S8;
+  b->redt = ORC_BF16; /* reduce dtype fixed to BF16 by the callers, bestla_gemm.cpp:229,308,408 */
+  b->q_size = updiv((size_t)b->npad * b->kpad * dtype_bits(qtype), 8);
+  int nk = (int)updiv((size_t)b->kpad, (size_t)b->bs);
+  b->cstep = b->npad;
+  b->csize = (size_t)nk * b->npad;
+  b->asym = asym;
+  b->has_red = orc_core_is_int(coreid);
+  b->has_shf = shuffle;
+  b->s_size = b->csize * dtype_bytes(stype);
+  b->z_size = asym ? b->csize * 1 : 0;
+  b->r_size = b->has_red ? b->csize * 2 : 0;
+  b->shf_size = shuffle ? (size_t)k * 4 : 0;
+  /* update_size (bestla_storage.h:812-816): header 48 + aligned/optional buffer sizes, padto 64 */
+  size_t sz = 48;
+  sz += 16 + b->q_size + 64;
+  sz += 24 + (16 + b->s_size + 64);
+  sz += 1 + (asym ? 16 + b->z_size + 64 : 0);
+  sz += 1 + (b->has_red ? 16 + b->r_size + 64 : 0);
+  sz += 1; /* DQ correction buffer: absent */
+  sz += 1 + (shuffle ? 16 + b->shf_size + 64 : 0);
+  b->msize = padto(sz, 64);
+}
+
+static inline void w64(int8_t** p, uint64_t v) {
+  memcpy(*p, &v, 8);
+  *p += 8;
+}
+static inline void w32(int8_t** p, uint32_t v) {
+  memcpy(*p, &v, 4);
+  *p += 4;
+}
+static inline void w8(int8_t** p, uint8_t v) {
+  **p = (int8_t)v;
+  *p += 1;
+}
+/* ObjectAlignedBuffer<64>::serializeToBuffer (bestla_storage.h:77-88): size, offset to next 64-B boundary */
+static size_t aligned_buf(int8_t** p, int8_t* base, size_t size) {
+  w64(p, size);
+  uintptr_t tmp = (uintptr_t)(*p + 8);
+  uint64_t off = ((tmp + 63) / 64 * 64) - tmp;
+  w64(p, off);
+  *p += off;
+  size_t at = (size_t)(*p - base);
+  *p += size;
+  return at;
+}
+
+/* assign() (bestla_storage.h:818-823): writes the header and every buffer descriptor, returns data offsets */
+static void blob_write_header(blob_t* b, int8_t* base) {
+  int8_t* p = base;
+  w64(&p, b->msize);
+  w32(&p, b->prologue);
+  w64(&p, b->coreid);
+  w32(&p, (uint32_t)b->npad);
+  w32(&p, (uint32_t)b->kpad);
+  w32(&p, (uint32_t)b->n);
+  w32(&p, (uint32_t)b->k);
+  w32(&p, b->dtype);
+  w32(&p, (uint32_t)b->bs);
+  w32(&p, (uint32_t)b->dq_bs);
+  b->q_off = aligned_buf(&p, base, b->q_size);
+  w32(&p, b->scat);
+  w32(&p, b->zpt);
+  w32(&p, b->redt);
+  w32(&p, (uint32_t)b->cstep);
+  w64(&p, b->csize);
+  b->s_off = aligned_buf(&p, base, b->s_size);
+  w8(&p, (uint8_t)(b->asym != 0));
+  if (b->asym) b->z_off = aligned_buf(&p, base, b->z_size);
+  w8(&p, (uint8_t)(b->has_red != 0));
+  if (b->has_red) b->r_off = aligned_buf(&p, base, b->r_size);
+  w8(&p, 0); /* mDQCorrectionBuf */
+  w8(&p, (uint8_t)(b->has_shf != 0));
+  if (b->has_shf) b->shf_off = aligned_buf(&p, base, b->shf_size);
+}
+
+static inline uint64_t r64(const int8_t** p) {
+  uint64_t v;
+  memcpy(&v, *p, 8);
+  *p += 8;
+  return v;
+}
+static inline uint32_t r32(const int8_t** p) {
+  uint32_t v;
+  memcpy(&v, *p, 4);
+  *p += 4;
+  return v;
+}
+static inline uint8_t r8(const int8_t** p) {
+  uint8_t v = (uint8_t)**p;
+  *p += 1;
+  return v;
+}
+static size_t read_buf(const int8_t** p, const int8_t* base, size_t* size) {
+  *size = r64(p);
+  uint64_t off = r64(p);
+  *p += off;
+  size_t at = (size_t)(*p - base);
+  *p += *size;
+  return at;
+}
+
+/* deserialize() (bestla_storage.h:831-836) */
+static int blob_parse(blob_t* b, const void* buf) {
+  memset(b, 0, sizeof(*b));
+  const int8_t* base = (const int8_t*)buf;
+  const int8_t* p = base;
+  b->msize = r64(&p);
+  b->prologue = r32(&p);
+  if (b->prologue != 1) return -1; /* only WeightKBlockNInteger */
+  b->coreid = r64(&p);
+  b->npad = (int)r32(&p);
+  b->kpad = (int)r32(&p);
+  b->n = (int)r32(&p);
+  b->k = (int)r32(&p);
+  b->dtype = r32(&p);
+  b->bs = (int)r32(&p);
+  b->dq_bs = (int)r32(&p);
+  b->q_off = read_buf(&p, base, &b->q_size);
+  b->scat = r32(&p);
+  b->zpt = r32(&p);
+  b->redt = r32(&p);
+  b->cstep = (int)r32(&p);
+  b->csize = r64(&p);
+  b->s_off = read_buf(&p, base, &b->s_size);
+  b->asym = r8(&p);
+  if (b->asym) b->z_off = read_buf(&p, base, &b->z_size);
+  b->has_red = r8(&p);
+  if (b->has_red) b->r_off = read_buf(&p, base, &b->r_size);
+  if (r8(&p)) return -2; /* double quant unsupported */
+  b->has_shf = r8(&p);
+  if (b->has_shf) b->shf_off = read_buf(&p, base, &b->shf_size);
+  return 0;
+}
+
+size_t orc_blob_size(int n, int k, int blocksize, uint32_t qtype, uint32_t stype, int asym, uint64_t core_id,
+                     int shuffle) {
+  blob_t b;
+  blob_describe(&b, n, k, blocksize, qtype, stype, asym, core_id, shuffle);
+  return b.msize;
+}
+
+int orc_blob_info(const void* buf, int64_t* o) {
+  blob_t b;
+  int r = blob_parse(&b, buf);
+  if (r) return r;
+  int64_t v[27] = {(int64_t)b.msize, b.prologue, (int64_t)b.coreid, b.npad, b.kpad, b.n, b.k, b.dtype, b.bs,
+                   b.scat, b.zpt, b.redt, b.cstep, (int64_t)b.csize, b.asym, b.has_red, b.has_shf,
+                   (int64_t)b.q_off, (int64_t)b.q_size, (int64_t)b.s_off, (int64_t)b.s_size, (int64_t)b.z_off,
+                   (int64_t)b.z_size, (int64_t)b.r_off, (int64_t)b.r_size, (int64_t)b.shf_off,
+                   (int64_t)b.shf_size};
+  memcpy(o, v, sizeof(v));
+  return 0;
+}
+
+/* store one scale value in the blob's scale dtype (setQuantCorrection, bestla_prologue_b.h:244-271):
+   BF16 via bf16(float) RNE; F16 via the host's vcvtps2ph (IEEE RNE) on AVX512-FP16 hosts */
+static void put_scale(uint8_t* sp, size_t idx, uint32_t scat, float v) {
+  if (scat == ORC_F32) {
+    memcpy(sp + idx * 4, &v, 4);
+  } else if (scat == ORC_BF16) {
+    uint16_t h = orc_f32_to_bf16(v);
+    memcpy(sp + idx * 2, &h, 2);
+  } else {
+    uint16_t h = orc_f32_to_fp16_rne(v);
+    memcpy(sp + idx * 2, &h, 2);
+  }
+}
+static float get_scale(const uint8_t* sp, size_t idx, uint32_t scat) {
+  if (scat == ORC_F32) {
+    float v;
+    memcpy(&v, sp + idx * 4, 4);
+    return v;
+  }
+  uint16_t h;
+  memcpy(&h, sp + idx * 2, 2);
+  return scat == ORC_BF16 ? orc_bf16_to_f32(h) : orc_fp16_to_f32(h);
+}
+
+/* dequantized W[k][n] (ld = ldw) from a parsed blob: getWeight + RevertPaddingInterleave (bestla_prologue_b.h:211-242) */
+static void blob_dequant(const blob_t* b, const int8_t* base, float* W, int ldw, int8_t* Qout, float* Sout,
+                         int8_t* Zout) {
+  int nt = orc_core_ntile(b->coreid), pr = orc_core_packrow(b->coreid);
+  size_t nel = (size_t)b->npad * b->kpad;
+  int8_t* flat = (int8_t*)malloc(nel);
+  const uint8_t* q = (const uint8_t*)(base + b->q_off);
+  int bits = dtype_bits(b->dtype);
+  if (bits == 4)
+    orc_decompress_s4(q, flat, nel);
+  else if (bits == 2)
+    orc_decompress_s2(q, flat, nel);
+  else
+    memcpy(flat, q, nel);
+  int8_t* qkn = (int8_t*)malloc((size_t)b->k * b->n);
+  orc_revert_padding_interleave(flat, qkn, b->k, b->n, b->kpad, b->npad, b->kpad, b->n, nt, pr);
+  const uint8_t* sp = (const uint8_t*)(base + b->s_off);
+  const int8_t* zp = b->asym ? base + b->z_off : NULL;
+  for (int kk = 0; kk < b->k; kk++) {
+    int g = kk / b->bs;
+    for (int nn = 0; nn < b->n; nn++) {
+      size_t ci = (size_t)g * b->cstep + nn;
+      int z = zp ? zp[ci] : 0;
+      float s = get_scale(sp, ci, b->scat);
+      int8_t qv = qkn[(size_t)kk * b->n + nn];
+      if (W) W[(size_t)kk * ldw + nn] = (float)(qv - z) * s; /* kernel_ref.h:1035 */
+      if (Qout) Qout[(size_t)kk * b->n + nn] = qv;
+    }
+  }
+  int nblk = (int)updiv((size_t)b->k, (size_t)b->bs);
+  for (int g = 0; g < nblk; g++)
+    for (int nn = 0; nn < b->n; nn++) {
+      size_t ci = (size_t)g * b->cstep + nn;
+      if (Sout) Sout[(size_t)g * b->n + nn] = get_scale(sp, ci, b->scat);
+      if (Zout) Zout[(size_t)g * b->n + nn] = zp ? zp[ci] : 0;
+    }
+  free(flat);
+  free(qkn);
+}
+
+/* packQWeight (bestla_prologue_b.h:378-398): setQuantCorrection -> reorderWeight -> compressWeight -> reduceWeight */
+static int blob_pack_q_impl(blob_t* b, int8_t* base, const int8_t* Q, int ldb, const float* S, const int8_t* Z) {
+  int nt = orc_core_ntile(b->coreid), pr = orc_core_packrow(b->coreid);
+  int n = b->n, k = b->k;
+  int rawnk = (int)updiv((size_t)k, (size_t)b->bs);
+  int nk = (int)updiv((size_t)b->kpad, (size_t)b->bs);
+  uint8_t* sp = (uint8_t*)(base + b->s_off);
+  for (int g = 0; g < nk; g++)
+    for (int nn = 0; nn < b->npad; nn++) {
+      float v = (g < rawnk && nn < n) ? S[(size_t)g * n + nn] : 0.f;
+      put_scale(sp, (size_t)g * b->npad + nn, b->scat, v);
+    }
+  if (b->asym) {
+    int8_t* zp = base + b->z_off;
+    for (int g = 0; g < nk; g++)
+      for (int nn = 0; nn < b->npad; nn++) zp[(size_t)g * b->npad + nn] = (g < rawnk && nn < n) ? Z[(size_t)g * n + nn] : 0;
+  }
+  size_t nel = (size_t)b->npad * b->kpad;
+  int8_t* reordered = (int8_t*)malloc(nel);
+  orc_padding_interleave(Q, reordered, k, n, b->kpad, b->npad, ldb, b->kpad, nt, pr);
+  uint8_t* q = (uint8_t*)(base + b->q_off);
+  int bits = dtype_bits(b->dtype);
+  if (bits == 4)
+    orc_compress_s4(reordered, q, nel);
+  else if (bits == 2)
+    orc_compress_s2(reordered, q, nel);
+  else if (bits == 8)
+    memcpy(q, reordered, nel);
+  else {
+    free(reordered);
+    return -3;
+  }
+  free(reordered);
+  if (b->has_red) {
+    /* reduceWeight (bestla_prologue_b.h:455-470) + reduce/RowReduceSum (kernel_ref.h:2132-2141): sequential float
+       sum over the k < K rows of each block of the dequantized weight, stored bf16 */
+    float* deq = (float*)malloc(sizeof(float) * (size_t)k * n);
+    blob_dequant(b, base, deq, n, NULL, NULL, NULL);
+    uint16_t* rp = (uint16_t*)(base + b->r_off);
+    for (int g = 0; g < rawnk; g++)
+      for (int nn = 0; nn < n; nn++) {
+        float t = 0.f;
+        int k0 = g * b->bs, k1 = k0 + b->bs < k ? k0 + b->bs : k;
+        for (int kk = k0; kk < k1; kk++) t += deq[(size_t)kk * n + nn];
+        rp[(size_t)g * b->cstep + nn] = orc_f32_to_bf16(t);
+      }
+    free(deq);
+  }
+  return 0;
+}
+
+void orc_shuffle_indices(const int* g_idx, int k, int blocksize, int* out) {
+  int groups = (int)updiv((size_t)k, (size_t)blocksize);
+  int* cnt = (int*)calloc((size_t)groups, sizeof(int));
+  for (int i = 0; i < k; i++) {
+    int g = g_idx[i];
+    out[(size_t)g * blocksize + cnt[g]] = i;
+    cnt[g]++;
+  }
+  free(cnt);
+}
+
+int orc_blob_pack_q(void* buf, const int8_t* Q, const float* S, const int8_t* Z, int n, int k, int ldb, int blocksize,
+                    uint32_t qtype, uint32_t stype, int asym, uint64_t core_id, const int* g_idx) {
+  blob_t b;
+  blob_describe(&b, n, k, blocksize, qtype, stype, asym, core_id, g_idx != NULL);
+  blob_write_header(&b, (int8_t*)buf);
+  if (g_idx) orc_shuffle_indices(g_idx, k, b.bs, (int*)((int8_t*)buf + b.shf_off));
+  return blob_pack_q_impl(&b, (int8_t*)buf, Q, ldb, S, asym ? Z : NULL);
+}
+
+int orc_blob_quant_pack(void* buf, const float* B, int n, int k, int ldb, int blocksize, uint32_t qtype,
+                        uint32_t stype, int asym, uint64_t core_id, int is_trans) {
+  blob_t b;
+  blob_describe(&b, n, k, blocksize, qtype, stype, asym, core_id, 0);
+  blob_write_header(&b, (int8_t*)buf);
+  /* packTransposeWeight (bestla_prologue_b.h:180-185): B is [N][ldb] -> transpose to [K][N] */
+  float* kn = (float*)malloc(sizeof(float) * (size_t)k * n);
+  for (int kk = 0; kk < k; kk++)
+    for (int nn = 0; nn < n; nn++)
+      kn[(size_t)kk * n + nn] = is_trans ? B[(size_t)nn * ldb + kk] : B[(size_t)kk * ldb + nn];
+  int nk = (int)updiv((size_t)k, (size_t)b.bs);
+  int8_t* q = (int8_t*)malloc((size_t)k * n);
+  float* s = (float*)malloc(sizeof(float) * (size_t)nk * n);
+  int8_t* z = asym ? (int8_t*)malloc((size_t)nk * n) : NULL;
+  /* quantizeWeight (bestla_prologue_b.h:472-488) with bsize = mBlockSize (block rows align to blocksize) */
+  orc_quantize_rowblock(kn, q, k, n, n, n, s, z, b.bs, dtype_bits(qtype));
+  int r = blob_pack_q_impl(&b, (int8_t*)buf, q, n, s, z);
+  free(kn);
+  free(q);
+  free(s);
+  free(z);
+  return r;
+}
+
+int orc_blob_unpack_q(const void* buf, int8_t* Q, float* S, int8_t* Z, int* shuffle) {
+  blob_t b;
+  int r = blob_parse(&b, buf);
+  if (r) return r;
+  blob_dequant(&b, (const int8_t*)buf, NULL, 0, Q, S, Z);
+  if (shuffle && b.has_shf) memcpy(shuffle, (const int8_t*)buf + b.shf_off, (size_t)b.k * 4);
+  return 0;
+}
+
+int orc_blob_unpack_fp32(const void* buf, float* W, int ldb) {
+  blob_t b;
+  int r = blob_parse(&b, buf);
+  if (r) return r;
+  blob_dequant(&b, (const int8_t*)buf, W, ldb, NULL, NULL, NULL);
+  return 0;
+}
+
+void orc_gemm_f64(int m, int n, int k, const float* A, int lda, const float* W, int ldw, float* C, int ldc) {
+  double* acc = (double*)malloc(sizeof(double) * (size_t)n);
+  for (int i = 0; i < m; i++) {
+    for (int j = 0; j < n; j++) acc[j] = 0.0;
+    for (int kk = 0; kk < k; kk++) {
+      double a = A[(size_t)i * lda + kk];
+      const float* w = W + (size_t)kk * ldw;
+      for (int j = 0; j < n; j++) acc[j] += a * (double)w[j];
+    }
+    for (int j = 0; j < n; j++) C[(size_t)i * ldc + j] = (float)acc[j];
+  }
+  free(acc);
+}
+
+int orc_blob_forward(const float* A, const void* blob, float* C, int m, int n, int k, int lda, int ldc) {
+  blob_t b;
+  int r = blob_parse(&b, blob);
+  if (r) return r;
+  if (b.n != n || b.k != k) return -4;
+  float* W = (float*)malloc(sizeof(float) * (size_t)k * n);
+  blob_dequant(&b, (const int8_t*)blob, W, n, NULL, NULL, NULL);
+  const float* Ause = A;
+  float* Ash = NULL;
+  int ld = lda;
+  if (b.has_shf) { /* ShuffleActivationKBlockBase: A'[:, j] = A[:, idx[j]] (kernel_ref.h:27-37) */
+    const int* idx = (const int*)((const int8_t*)blob + b.shf_off);
+    Ash = (float*)malloc(sizeof(float) * (size_t)m * k);
+    for (int i = 0; i < m; i++)
+      for (int j = 0; j < k; j++) Ash[(size_t)i * k + j] = A[(size_t)i * lda + idx[j]];
+    Ause = Ash;
+    ld = k;
+  }
+  orc_gemm_f64(m, n, k, Ause, ld, W, n, C, ldc);
+  free(W);
+  free(Ash);
+  return 0;
+}
+
+/* kernel_ref.h:2489-2531 / 2712-2760 driven over the NTILE stripes of a PACK_ROW=1 blob as GEMVWrapper::gemv_kblock
+   does (bestla_wrapper.h:364-427); requires K % blocksize == 0 (blks = k / blocksize). */
+int orc_blob_gemv_ref(const float* A, const void* blob, float* C, int m, int lda, int ldc) {
+  blob_t b;
+  int r = blob_parse(&b, blob);
+  if (r) return r;
+  int nt = orc_core_ntile(b.coreid);
+  if (orc_core_packrow(b.coreid) != 1 || m > 8 || b.has_shf) return -5;
+  int bits = dtype_bits(b.dtype);
+  if (bits != 4 && bits != 2) return -6;
+  const uint8_t* q = (const uint8_t*)((const int8_t*)blob + b.q_off);
+  const uint8_t* sp = (const uint8_t*)((const int8_t*)blob + b.s_off);
+  const int8_t* zp = b.asym ? (const int8_t*)blob + b.z_off : NULL;
+  int blks = b.k / b.bs;
+  float* acc = (float*)malloc(sizeof(float) * (size_t)nt * m);
+  for (int n0 = 0; n0 < b.n; n0 += nt) {
+    memset(acc, 0, sizeof(float) * (size_t)nt * m);
+    const uint8_t* bp = q + (size_t)n0 * b.kpad * bits / 8;
+    for (int ib = 0; ib < blks; ib++) {
+      for (int ik = 0; ik < b.bs; ik++) {
+        int kk = ib * b.bs + ik;
+        for (int im = 0; im < m; im++) {
+          float aval = A[(size_t)im * lda + kk];
+          for (int in = 0; in < nt; in++) {
+            size_t ci = (size_t)ib * b.cstep + n0 + in;
+            int qv;
+            if (bits == 4)
+              qv = ((bp[(size_t)kk * nt / 2 + in / 2] >> (4 * (in & 1))) & 0xF) - 8;
+            else
+              qv = ((bp[((size_t)kk * nt + in) / 4] >> (2 * (in & 3))) & 3) - 2;
+            float z = zp ? (float)zp[ci] : 0.f;
+            if (bits == 4) /* kernel_ref.h:2505-2506: aval * (q - zp) * s */
+              acc[im * nt + in] += aval * ((float)qv - z) * get_scale(sp, ci, b.scat);
+            else /* kernel_ref.h:2733-2735: bval = (q - zp) * s; acc += aval * bval */
+              acc[im * nt + in] += aval * (((float)qv - z) * get_scale(sp, ci, b.scat));
+          }
+        }
+      }
+    }
+    for (int im = 0; im < m; im++)
+      for (int in = 0; in < nt && n0 + in < b.n; in++) C[(size_t)im * ldc + n0 + in] = acc[im * nt + in];
+  }
+  free(acc);
+  return 0;
+}
+
+int orc_blob_gemv_timed(const float* A, const void* blob, float* C, int m, int lda, int ldc, int iters) {
+  int r = 0;
+  for (int it = 0; it < iters && r == 0; it++) r = orc_blob_gemv_ref(A, blob, C, m, lda, ldc);
+  return r;
+}

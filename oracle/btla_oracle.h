@@ -1,0 +1,102 @@
+/*
+ * btla_oracle.h -- CPU restatement of the reference (hoivb612/neural, BesTLA) weight-only-quantization
+ * algorithms on the WOQ matmul hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Nothing under oracle/ is part of the product: only tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline leg may load it, and only as the checker.
+ *
+ * Parity pinning: every integer/byte transform here is checked bit-for-bit against goldens produced by
+ * oracle/_ref/ref_golden, a driver compiled from the reference's own bestla/bestla/kernel_ref.h +
+ * bestla_utils.h (see oracle/ref/Makefile and tests/golden/make_golden.py).  The blob (de)serializer is
+ * restated from bestla_storage.h text (not compilable here: it pulls xbyak) and pinned by the reference's
+ * own round-trip rule (UT_StorageMemCheck, bestla/bestla/ut/bestla_prologue_b.cpp:290-331) plus the
+ * field-by-field layout of bestla_storage.h:22-357,697-834.
+ */
+#ifndef NAD_BTLA_ORACLE_H
+#define NAD_BTLA_ORACLE_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* BTLA_DTYPE values (bestla/bestla/bestla.h:38-87) */
+#define ORC_F32 32u
+#define ORC_F16 16u
+#define ORC_BF16 (16u | (1u << 16))
+#define ORC_S8 (8u | 0x100u)
+#define ORC_S4 (4u | 0x100u)
+#define ORC_S2 (2u | 0x100u)
+
+/* fp16/bf16 conversions (bestla/bestla/bestla_utils.h:116-229) */
+uint16_t orc_f32_to_bf16(float v);
+float orc_bf16_to_f32(uint16_t x);
+uint16_t orc_f32_to_fp16_bestla(float v); /* utils::fp16::operator=(float), bestla_utils.h:184-196 */
+uint16_t orc_f32_to_fp16_rne(float v);    /* IEEE RNE, = vcvtps2ph on AVX512-FP16/F16C hosts */
+float orc_fp16_to_f32(uint16_t x);        /* bestla_utils.h:197-206 */
+
+/* kernel_ref.h:1608-1719 quantize_f32_sign_int_rowblock (sNauto sym / asym paths) */
+void orc_quantize_rowblock(const float* src, int8_t* dst, int row, int col, int ld_src, int ld_dst, float* scales,
+                           int8_t* zero_points, int blocksize, int bits);
+
+/* kernel_ref.h:39-59 padding_interleave / kernel_ref.h:62-80 revert_padding_interleave (int8) */
+void orc_padding_interleave(const int8_t* src, int8_t* dst, int row, int col, int rowpad, int colpad, int src_step,
+                            int dst_step, int ntile, int rowpack);
+void orc_revert_padding_interleave(const int8_t* src, int8_t* dst, int row, int col, int rowpad, int colpad,
+                                   int src_step, int dst_step, int ntile, int rowpack);
+
+/* kernel_ref.h:155-165 compress_s8_s4, :330-341 compress_2bit, and the matching decompress_s4_s8/s2_s8 */
+void orc_compress_s4(const int8_t* src, uint8_t* dst, size_t n);
+void orc_compress_s2(const int8_t* src, uint8_t* dst, size_t n);
+void orc_decompress_s4(const uint8_t* src, int8_t* dst, size_t n);
+void orc_decompress_s2(const uint8_t* src, int8_t* dst, size_t n);
+
+/* Core ids (bestla_gemm.h:83-93 CoreAttr::make_core_id; typedefs neural_speed/core/layers/bestla_defs.h:36-54) */
+uint64_t orc_core_id(const char* name); /* "avx2","avx512f","amx_bf16","amx_fp16","avx512_vnni_kblock",
+                                           "avx512bw_kblock","avx_vnni_kblock","avx2_vnni_kblock","amx_int8_kblock" */
+int orc_core_ntile(uint64_t id);
+int orc_core_packrow(uint64_t id);
+int orc_core_ktile(uint64_t id);
+int orc_core_is_int(uint64_t id);
+
+/* ne_comp_type (neural_speed/core/data_types.h:57-63) -> core selection of BTLAGemmPackBSizeLocal
+   (neural_speed/core/layers/bestla_gemm.cpp:241-300) for an emulated host ISA profile:
+   profile 0 = Sapphire Rapids (AMX-INT8/BF16, AVX512-VNNI/BF16/FP16), 1 = AVX512-VNNI, 2 = AVX512F, 3 = AVX2 */
+uint64_t orc_select_core(int comp_type, uint32_t qtype, int blocksize, int asym, int profile);
+
+/* Packed blob (StorageWeightKBlockNInteger, bestla_storage.h:697-834) */
+size_t orc_blob_size(int n, int k, int blocksize, uint32_t qtype, uint32_t stype, int asym, uint64_t core_id,
+                     int shuffle);
+/* full quantize + pack (BTLAGemmQuantPackB, bestla_gemm.cpp:321-398 -> WeightKBlockNInteger::packWeight) */
+int orc_blob_quant_pack(void* buf, const float* B, int n, int k, int ldb, int blocksize, uint32_t qtype,
+                        uint32_t stype, int asym, uint64_t core_id, int is_trans);
+/* pre-quantized pack (BTLAGemmPackB, bestla_gemm.cpp:424-504 -> packQWeight + setShuffleIndices) */
+int orc_blob_pack_q(void* buf, const int8_t* Q, const float* S, const int8_t* Z, int n, int k, int ldb, int blocksize,
+                    uint32_t qtype, uint32_t stype, int asym, uint64_t core_id, const int* g_idx);
+/* header fields: [mSize, prologue, coreid, NPad, KPad, N, K, dtype, blocksize, scaT, zpT, redT, cstep, csize,
+                   asym, has_reduce, has_shuffle, q_off, q_size, s_off, s_size, z_off, z_size, r_off, r_size,
+                   shf_off, shf_size]  (27 int64 values; *_off are byte offsets from the blob base) */
+int orc_blob_info(const void* buf, int64_t* out27);
+/* exact unpack to the integer domain: Q [K][N] signed int8, S [ceil(K/bs)][N] float, Z same shape int8 */
+int orc_blob_unpack_q(const void* buf, int8_t* Q, float* S, int8_t* Z, int* shuffle);
+/* BTLAGemmUnPackB (bestla_gemm.cpp:673-749): W[k][n] = float(q - zp) * s  (kernel_ref.h:1027-1056) */
+int orc_blob_unpack_fp32(const void* buf, float* W, int ldb);
+/* UT_ShuffleIndices LUT (bestla_prologue_b.h:337-356): out[g*bs + j] = j-th k with g_idx[k] == g */
+void orc_shuffle_indices(const int* g_idx, int k, int blocksize, int* out);
+
+/* GEMM oracles */
+/* C[m][n] = sum_k A[m][k] * W[k][n], fp64 accumulation (the bar of bestla_prologue_b.cpp:510-511) */
+void orc_gemm_f64(int m, int n, int k, const float* A, int lda, const float* W, int ldw, float* C, int ldc);
+/* blob forward: applies the shuffle LUT to A (bestla_prologue_a.h:407-422) then unpack + orc_gemm_f64 */
+int orc_blob_forward(const float* A, const void* blob, float* C, int m, int n, int k, int lda, int ldc);
+/* kernel_ref.h:2489-2531 gemv_4bit_fp32_fp32 and :2712-2760 gemv_2bit_fp32_fp32 over a whole PACK_ROW=1 blob,
+   float accumulation in the reference's order (MTILE = m <= 8) */
+int orc_blob_gemv_ref(const float* A, const void* blob, float* C, int m, int lda, int ldc);
+/* single-threaded CPU WOQ GEMV in the reference algorithm's float order, used as the timed cpu_baseline */
+int orc_blob_gemv_timed(const float* A, const void* blob, float* C, int m, int lda, int ldc, int iters);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

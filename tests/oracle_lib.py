@@ -1,0 +1,168 @@
+"""ctypes access to the oracle (oracle/liboracle.so) and the golden fixtures.  Test infrastructure only."""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_DIR = os.path.join(REPO, "oracle")
+GOLDEN = os.path.join(REPO, "tests", "golden")
+
+F32, F16, BF16 = 32, 16, 16 | (1 << 16)
+S8, S4, S2 = 8 | 0x100, 4 | 0x100, 2 | 0x100
+BITS_TO_QTYPE = {8: S8, 4: S4, 2: S2}
+
+_p = C.c_void_p
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data_as(_p)
+
+
+class Oracle:
+    _inst = None
+
+    @classmethod
+    def get(cls):
+        if cls._inst is None:
+            cls._inst = cls()
+        return cls._inst
+
+    def __init__(self):
+        so = os.path.join(ORACLE_DIR, "liboracle.so")
+        src = os.path.join(ORACLE_DIR, "btla_oracle.c")
+        if not os.path.exists(so) or os.path.getmtime(so) < os.path.getmtime(src):
+            subprocess.check_call(["make", "-s", "-C", ORACLE_DIR])
+        L = self.lib = C.CDLL(so)
+        L.orc_blob_size.restype = C.c_size_t
+        L.orc_blob_size.argtypes = [C.c_int, C.c_int, C.c_int, C.c_uint32, C.c_uint32, C.c_int, C.c_uint64, C.c_int]
+        L.orc_core_id.restype = C.c_uint64
+        L.orc_core_id.argtypes = [C.c_char_p]
+        L.orc_select_core.restype = C.c_uint64
+        L.orc_select_core.argtypes = [C.c_int, C.c_uint32, C.c_int, C.c_int, C.c_int]
+        L.orc_blob_quant_pack.argtypes = [_p, _p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint32, C.c_uint32, C.c_int,
+                                          C.c_uint64, C.c_int]
+        L.orc_blob_pack_q.argtypes = [_p, _p, _p, _p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint32, C.c_uint32,
+                                      C.c_int, C.c_uint64, _p]
+        L.orc_blob_info.argtypes = [_p, _p]
+        L.orc_blob_unpack_q.argtypes = [_p, _p, _p, _p, _p]
+        L.orc_blob_unpack_fp32.argtypes = [_p, _p, C.c_int]
+        L.orc_blob_forward.argtypes = [_p, _p, _p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int]
+        L.orc_blob_gemv_ref.argtypes = [_p, _p, _p, C.c_int, C.c_int, C.c_int]
+        L.orc_blob_gemv_timed.argtypes = [_p, _p, _p, C.c_int, C.c_int, C.c_int, C.c_int]
+        L.orc_quantize_rowblock.argtypes = [_p, _p, C.c_int, C.c_int, C.c_int, C.c_int, _p, _p, C.c_int, C.c_int]
+        L.orc_padding_interleave.argtypes = [_p, _p] + [C.c_int] * 8
+        L.orc_revert_padding_interleave.argtypes = [_p, _p] + [C.c_int] * 8
+        for f in ("orc_compress_s4", "orc_compress_s2", "orc_decompress_s4", "orc_decompress_s2"):
+            getattr(L, f).argtypes = [_p, _p, C.c_size_t]
+        L.orc_shuffle_indices.argtypes = [_p, C.c_int, C.c_int, _p]
+        L.orc_f32_to_bf16.restype = C.c_uint16
+        L.orc_f32_to_bf16.argtypes = [C.c_float]
+        L.orc_f32_to_fp16_bestla.restype = C.c_uint16
+        L.orc_f32_to_fp16_bestla.argtypes = [C.c_float]
+        L.orc_f32_to_fp16_rne.restype = C.c_uint16
+        L.orc_f32_to_fp16_rne.argtypes = [C.c_float]
+        L.orc_fp16_to_f32.restype = C.c_float
+        L.orc_fp16_to_f32.argtypes = [C.c_uint16]
+        L.orc_bf16_to_f32.restype = C.c_float
+        L.orc_bf16_to_f32.argtypes = [C.c_uint16]
+        L.orc_core_ktile.argtypes = [C.c_uint64]
+        L.orc_core_ntile.argtypes = [C.c_uint64]
+        L.orc_core_packrow.argtypes = [C.c_uint64]
+
+    # ---- helpers
+    def core(self, name):
+        return self.lib.orc_core_id(name.encode())
+
+    def quantize(self, src_kn, blocksize, bits, asym):
+        src = np.ascontiguousarray(src_kn, dtype=np.float32)
+        row, col = src.shape
+        nblk = -(-row // blocksize)
+        q = np.zeros((row, col), np.int8)
+        s = np.zeros((nblk, col), np.float32)
+        z = np.zeros((nblk, col), np.int8) if asym else None
+        self.lib.orc_quantize_rowblock(_ptr(src), _ptr(q), row, col, col, col, _ptr(s), _ptr(z), blocksize, bits)
+        return q, s, z
+
+    def blob_size(self, n, k, bs, qtype, stype, asym, core, shuffle=False):
+        return self.lib.orc_blob_size(n, k, bs, qtype, stype, int(asym), core, int(shuffle))
+
+    def quant_pack(self, W, n, k, bs, qtype, stype, asym, core, is_trans=True):
+        W = np.ascontiguousarray(W, dtype=np.float32)
+        size = self.blob_size(n, k, bs, qtype, stype, asym, core)
+        buf = np.zeros(size + 64, np.uint8)
+        off = (-buf.ctypes.data) % 64
+        blob = buf[off:off + size]
+        ldb = k if is_trans else n
+        r = self.lib.orc_blob_quant_pack(_ptr(blob), _ptr(W), n, k, ldb, bs, qtype, stype, int(asym), core,
+                                         int(is_trans))
+        assert r == 0, r
+        return blob
+
+    def pack_q(self, Q, S, Z, n, k, bs, qtype, stype, asym, core, g_idx=None):
+        Q = np.ascontiguousarray(Q, dtype=np.int8)
+        S = np.ascontiguousarray(S, dtype=np.float32)
+        Z = None if Z is None else np.ascontiguousarray(Z, dtype=np.int8)
+        gi = None if g_idx is None else np.ascontiguousarray(g_idx, dtype=np.int32)
+        size = self.blob_size(n, k, bs, qtype, stype, asym, core, gi is not None)
+        buf = np.zeros(size + 64, np.uint8)
+        off = (-buf.ctypes.data) % 64
+        blob = buf[off:off + size]
+        r = self.lib.orc_blob_pack_q(_ptr(blob), _ptr(Q), _ptr(S), _ptr(Z), n, k, n, bs, qtype, stype, int(asym),
+                                     core, _ptr(gi))
+        assert r == 0, r
+        return blob
+
+    def info(self, blob):
+        o = np.zeros(27, np.int64)
+        assert self.lib.orc_blob_info(_ptr(blob), _ptr(o)) == 0
+        keys = ["size", "prologue", "coreid", "npad", "kpad", "n", "k", "dtype", "bs", "scat", "zpt", "redt",
+                "cstep", "csize", "asym", "has_reduce", "has_shuffle", "q_off", "q_size", "s_off", "s_size",
+                "z_off", "z_size", "r_off", "r_size", "shf_off", "shf_size"]
+        return dict(zip(keys, (int(v) for v in o)))
+
+    def unpack_q(self, blob):
+        inf = self.info(blob)
+        n, k, bs = inf["n"], inf["k"], inf["bs"]
+        nblk = -(-k // bs)
+        Q = np.zeros((k, n), np.int8)
+        S = np.zeros((nblk, n), np.float32)
+        Z = np.zeros((nblk, n), np.int8)
+        shf = np.zeros(k, np.int32)
+        assert self.lib.orc_blob_unpack_q(_ptr(blob), _ptr(Q), _ptr(S), _ptr(Z), _ptr(shf)) == 0
+        return Q, S, Z, (shf if inf["has_shuffle"] else None)
+
+    def unpack_fp32(self, blob):
+        inf = self.info(blob)
+        W = np.zeros((inf["k"], inf["n"]), np.float32)
+        assert self.lib.orc_blob_unpack_fp32(_ptr(blob), _ptr(W), inf["n"]) == 0
+        return W
+
+    def forward(self, A, blob, n, k):
+        A = np.ascontiguousarray(A, dtype=np.float32)
+        m = A.shape[0]
+        C_ = np.zeros((m, n), np.float32)
+        assert self.lib.orc_blob_forward(_ptr(A), _ptr(blob), _ptr(C_), m, n, k, A.shape[1], n) == 0
+        return C_
+
+    def gemv_ref(self, A, blob, n):
+        A = np.ascontiguousarray(A, dtype=np.float32)
+        m = A.shape[0]
+        C_ = np.zeros((m, n), np.float32)
+        r = self.lib.orc_blob_gemv_ref(_ptr(A), _ptr(blob), _ptr(C_), m, A.shape[1], n)
+        assert r == 0, r
+        return C_
+
+
+def load_ref_golden():
+    """tests/golden/ref/manifest.txt -> {case: {name: array}}"""
+    d = os.path.join(GOLDEN, "ref")
+    out = {}
+    with open(os.path.join(d, "manifest.txt")) as f:
+        for line in f:
+            cs, name, dt, n = line.split()
+            arr = np.fromfile(os.path.join(d, f"{cs}.{name}.bin"), dtype=np.dtype(dt))
+            assert arr.size == int(n)
+            out.setdefault(cs, {})[name] = arr
+    return out
