@@ -1,0 +1,161 @@
+/*
+ * neural_amd.h -- C ABI of the MI355X-native weight-only-quantized (WOQ) matmul core.
+ *
+ * Drop-in for the BesTLA boundary of Neural Speed (hoivb612/neural).  Every entry point below keeps the name,
+ * argument meaning and error behaviour of the reference interface it replaces (cited per group; paths relative to
+ * the reference repo root).  Plain C types only: no torch, no HIP types (a HIP stream is passed as void* "queue").
+ *
+ * Build: `make -C neural_amd` -> neural_amd/libneural_amd.so (gfx950).  Link it in place of
+ * neural_speed/core/layers/ne_bestla.cpp + ne_bestla_sycl.cpp + bestla_gemm.cpp.
+ *
+ * Errors: bool/int functions return false/nonzero; void functions (whose reference counterparts assert(0) or are
+ * silently skipped, e.g. bestla_gemm.cpp:542-590) print "neural_amd: <reason>" to stderr and record it; read it with
+ * nad_last_error().  Nothing is silently skipped.
+ */
+#ifndef NEURAL_AMD_H
+#define NEURAL_AMD_H
+#include <stdbool.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ===== device half: neural_speed/core/ne_bestla.h:85-112 (implemented for SYCL in
+ * neural_speed/core/layers/ne_bestla_sycl.cpp:25-171).  queue == hipStream_t; device == NadDevice*. */
+void* bestla_create_device(bool profile);               /* ne_bestla.h:86 */
+void* bestla_get_device_queue(void* device);            /* ne_bestla.h:87 */
+void bestla_release_device(void* device);               /* ne_bestla.h:88 */
+size_t bestla_device_gmem_size(void* device);           /* ne_bestla.h:89 */
+void* bestla_device_malloc(size_t size, void* queue);   /* ne_bestla.h:90 */
+void bestla_device_free(void* ptr, void* queue);        /* ne_bestla.h:91 */
+void bestla_device_memcpy(void* dstptr, const void* srcptr, size_t size, void* queue);      /* ne_bestla.h:92 */
+void bestla_device_memcpy_sync(void* dstptr, const void* srcptr, size_t size, void* queue); /* ne_bestla.h:93 */
+void bestla_device_sync(void* queue);                   /* ne_bestla.h:94 */
+/* size of the per-tensor device descriptor embedded after ne_tensor (ne_layers.c:946-949) */
+size_t bestla_device_storage_size(void);                /* ne_bestla.h:95 */
+/* parse a host BTLA blob, repack it on the GPU into the MFMA tile layout inside `deviceptr` (which the caller sized
+ * with the blob's byte size, model_files.h:1515-1525) and fill the host descriptor `devstor`. */
+void bestla_device_load_storage(void* hoststor, void* devstor, void* deviceptr, void* queue); /* ne_bestla.h:96 */
+/* Y[m][n] = X[m][k] . W^T, X/Y fp32 device pointers (row strides lda/ldo in elements), asynchronous on queue */
+void bestla_device_f32f32_forward(float* activation, void* weiptr, float* output, int _m, int _n, int _k, int lda,
+                                  int ldo, void* workspace, void* queue); /* ne_bestla.h:97-98 */
+
+/* ===== host half: neural_speed/core/ne_bestla.h:21-83 (CPU implementation: core/layers/inner_product.cpp,
+ * ip_fusion_qkv.cpp, ip_fusion_ffn.cpp, ne_bestla.cpp).  Same host-pointer contract; the work runs on the GPU
+ * (weights uploaded once per blob and cached, activations/outputs staged over PCIe).  Pointers that are already
+ * device memory are used in place. */
+void bestla_init(void);                                 /* ne_bestla.h:31 */
+int bestla_set_threads(int _nth);                       /* ne_bestla.h:23: host packing threads */
+void* bestla_get_thread_handle(void);                   /* ne_bestla.h:25 */
+unsigned long long bestla_f32f32_get_workspace_size(int _m, int _n, int _k, void* wptr); /* ne_bestla.h:33 */
+void bestla_f32f32_forward(float* activation, void* weiptr, float* output, int _m, int _n, int _k, int lda, int ldo,
+                           void* workspace);            /* ne_bestla.h:35-36 */
+bool bestla_fusion_add_f32f32_support(void* weiptr, int _m, int _n, int _k); /* ne_bestla.h:38 */
+void bestla_fusion_add_f32f32_forward(float* activation, void* weiptr, float* bias, float* output, int _m, int _n,
+                                      int _k, int lda, int ldo, bool boardcast_bias, void* workspace); /* :39-40 */
+unsigned long long bestla_fusion_QKV_f32f32_get_workspace_size(int _m, int _n, int _k, void* w1ptr); /* :42 */
+bool bestla_fusion_QKV_f32f32_support(void* wqptr, void* wkptr, void* wvptr, int _m, int _n, int _k); /* :44 */
+void bestla_fusion_QKV_f32f32_forward(float* activation, void* wqptr, void* wkptr, void* wvptr, float* output, int _m,
+                                      int _n, int _k, int lda, int ldo, void* workspace); /* :46-47 */
+unsigned long long bestla_fusion_FFN_f32f32_get_workspace_size(int seq, int fin, int fmid, int fout, void* w1ptr,
+                                                               void* w2ptr); /* :49-50 */
+bool bestla_fusion_FFN_SiLu_f32f32_support(void* w1ptr, void* w2ptr, void* w3ptr, int seq, int fin, int fmid,
+                                           int fout); /* :57 */
+void bestla_fusion_FFN_SiLu_f32f32_forward(float* activation, void* w1ptr, void* w2ptr, void* w3ptr, float* tmp1,
+                                           float* tmp2, float* output, int seq, int fin, int fmid, int fout,
+                                           void* workspace); /* :58-60 */
+bool bestla_fusion_FFN_Gelu_Mul_f32f32_support(void* w1ptr, void* w2ptr, void* w3ptr, int seq, int fin, int fmid,
+                                               int fout); /* :52-53 */
+void bestla_fusion_FFN_Gelu_Mul_f32f32_forward(float* activation, void* w1ptr, void* w2ptr, void* w3ptr, float* tmp1,
+                                               float* tmp2, float* output, int seq, int fin, int fmid, int fout,
+                                               void* workspace); /* :54-56 */
+bool bestla_fusion_FFN_GeLu_f32f32_support(void* w1ptr, void* w2ptr, int seq, int fin, int fmid, int fout); /* :62 */
+void bestla_fusion_FFN_GeLu_f32f32_forward(float* activation, void* w1ptr, void* w2ptr, float* tmp1, float* output,
+                                           int seq, int fin, int fmid, int fout, void* workspace); /* :63-64 */
+bool bestla_fusion_FFN_Add_GeLu_f32f32_support(void* w1ptr, void* w2ptr, int seq, int fin, int fmid,
+                                               int fout); /* :66 */
+void bestla_fusion_FFN_Add_GeLu_f32f32_forward(float* activation, void* w1ptr, void* w2ptr, float* b1ptr,
+                                               float* b2ptr, float* tmp1, float* output, int seq, int fin, int fmid,
+                                               int fout, bool boardcast_bias, void* workspace); /* :67-69 */
+void bestla_unpackweight_fp32(void* wptr, int n, int k, float* fp32data, int ld); /* ne_bestla.h:71 */
+void bestla_packweight_copyattr(const float* f32ptr, void* dstpr, int n, int k, int ld, void* srcptr); /* :73 */
+
+/* ===== pack / format API: neural_speed/core/layers/bestla_gemm.h:30-58 (C++ linkage in the reference; C here).
+ * QuantType/ScaleDtype are BTLA_DTYPE values (bestla/bestla/bestla.h:38-87), CompType is ne_comp_type
+ * (core/data_types.h:57-63).  The core layout is chosen for an emulated host ISA (NAD_HOST_ISA, default
+ * Sapphire Rapids) exactly as BTLAGemmPackBSizeLocal does (bestla_gemm.cpp:241-300). ThreadPool may be NULL. */
+typedef struct BTLA_GEMM_DATA_PACKED_PARAMS {
+  const float* A; /* address of A (float32 matrix) */
+  const void* B;  /* address of B (packed nbits blob) */
+  float* C;       /* address of result matrix */
+  int lda;        /* leading dimension of A */
+  int ldc;        /* leading dimension of C */
+} BTLA_GEMM_DATA_PACKED_PARAMS;     /* bestla_gemm.h:30-36 */
+size_t BTLAGemmPackBSize(size_t N, size_t K, size_t BlkSize, uint32_t QuantType, uint32_t ScaleDtype, bool isAsym,
+                         int CompType, int* shuffle_indice); /* bestla_gemm.h:38-39 */
+bool BTLAGemmQuantPackB(void* PackedBuf, const float* FpData, size_t N, size_t K, size_t ldb, size_t BlkSize,
+                        uint32_t QuantType, uint32_t ScaleDtype, bool isAsym, int CompType, bool isTrans,
+                        void* ThreadPool); /* bestla_gemm.h:41-43 */
+bool BTLAGemmPackB(void* PackedBuf, const int8_t* QData, const float* Scales, const int8_t* Zp, size_t N, size_t K,
+                   size_t ldb, size_t BlkSize, uint32_t QuantType, uint32_t ScaleDtype, bool isAsym, int CompType,
+                   int* shuffle_indice, void* ThreadPool); /* bestla_gemm.h:48-50 */
+bool BTLAGemmUnPackB(float* FpData, const void* PackedBuf, size_t N, size_t K, size_t ldb,
+                     void* ThreadPool); /* bestla_gemm.h:52 */
+bool BTLAGemmBatchDriver(const size_t M, const size_t N, const size_t K, const size_t BatchN,
+                         const BTLA_GEMM_DATA_PACKED_PARAMS* DataParams, int8_t* WorkSpace,
+                         void* ThreadPool); /* bestla_gemm.h:54-55 */
+
+/* ===== native extensions (no reference counterpart) */
+#define NAD_ACT_F32 0
+#define NAD_ACT_F16 1
+#define NAD_ACT_BF16 2
+#define NAD_EPI_NONE 0
+#define NAD_EPI_BIAS 1
+#define NAD_EPI_SILU_MUL 2
+#define NAD_EPI_GELU_MUL 3
+#define NAD_EPI_GELU 4
+#define NAD_EPI_ADD_GELU 5
+#define NAD_EPI_SILU 6
+#define NAD_EPI_RES_ADD 7
+
+const char* nad_last_error(void);
+void nad_clear_error(void);
+/* device bytes the tile layout of this blob needs (<= the blob size for every Llama/Mistral shape) */
+size_t nad_device_weight_size(const void* hostblob);
+/* bestla_device_load_storage with an explicit capacity check and a status return */
+int nad_device_load(const void* hostblob, void* devstor, void* deviceptr, size_t capacity, void* queue);
+/* 64-byte descriptor summary: [magic, bits, n, k, blocksize, ns, nt, ng, scale_t, asym, has_shuffle, bytes] */
+int nad_weight_info(const void* devstor, int64_t* out12);
+/* blob header summary (same fields as the oracle's orc_blob_info) */
+int nad_blob_info(const void* hostblob, int64_t* out27);
+/* Y = epi(X . W^T): X in fp32/fp16/bf16 (act_dtype), Y fp32.  bias: bias[m*bias_ld + n] (bias_ld 0 = broadcast);
+ * res: residual[m*ld_res + n] for NAD_EPI_RES_ADD. */
+int nad_device_forward(const void* act, int act_dtype, const void* devstor, float* out, int m, int n, int k, int lda,
+                       int ldo, int epi, const float* bias, int bias_ld, const float* res, int ld_res, void* queue);
+/* fused Q/K/V (ip_fusion_qkv.cpp:22-93): out_i = X . W_i^T, one launch; W_i share K, blocksize, bits, scale dtype */
+int nad_device_qkv_forward(const void* act, int act_dtype, const void* wq, const void* wk, const void* wv, float* oq,
+                           float* ok, float* ov, int m, int k, int lda, int ldo_q, int ldo_k, int ldo_v, void* queue);
+/* fused FFN (ip_fusion_ffn.cpp:407-457): tmp1 = act1(X.W1^T) [optional], tmp2 = tmp1 * (X.W3^T), out = tmp2 . W2^T.
+ * epi = NAD_EPI_SILU_MUL or NAD_EPI_GELU_MUL. */
+int nad_device_ffn_forward(const void* act, int act_dtype, const void* w1, const void* w2, const void* w3, float* tmp1,
+                           float* tmp2, float* out, int m, int fin, int fmid, int fout, int lda, int epi, void* queue);
+/* tensor-parallel slicing of a packed blob without re-quantization (the reference re-quantizes,
+ * model_files.h:1538-1563).  axis 0: split N (TP_1D_ROW, column-parallel); axis 1: split K by whole groups
+ * (TP_1D_COLUMN, row-parallel).  Returns the shard's blob size (dst may be NULL to query). */
+size_t nad_blob_split(const void* src, int axis, int rank, int world, void* dst, size_t dst_capacity);
+/* the [begin, end) range of N (axis 0) or K (axis 1) that `rank` owns */
+int nad_split_range(const void* src, int axis, int rank, int world, int* begin, int* end);
+/* synthetic device weight of the given geometry (random packed values, scales U[smin,smax], zps) for benchmarks */
+int nad_synthetic_weight(void* devstor, void* deviceptr, size_t capacity, int bits, int n, int k, int blocksize,
+                         int scale_t, int asym, uint64_t seed, void* queue);
+/* device bytes of nad_synthetic_weight's layout */
+size_t nad_synthetic_weight_size(int bits, int n, int k, int blocksize, int scale_t, int asym);
+/* host convenience: (re)pack one blob into fp32 dequantized [K][N] from the device tile layout (round-trip check) */
+int nad_device_unpack_fp32(const void* devstor, float* host_out, void* queue);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NEURAL_AMD_H */

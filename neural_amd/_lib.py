@@ -1,0 +1,116 @@
+"""Loader for libneural_amd.so (the C-ABI of include/neural_amd.h).
+
+There is no fallback: if the shared library is missing or fails to load, every entry point raises.
+"""
+import ctypes as C
+import os
+import re
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libneural_amd.so")
+HEADER = os.path.join(os.path.dirname(_HERE), "include", "neural_amd.h")
+
+_p = C.c_void_p
+_i = C.c_int
+_sz = C.c_size_t
+_u32 = C.c_uint32
+_u64 = C.c_uint64
+_b = C.c_bool
+
+# name -> (restype, argtypes)
+SIGNATURES = {
+    "bestla_create_device": (_p, [_b]),
+    "bestla_get_device_queue": (_p, [_p]),
+    "bestla_release_device": (None, [_p]),
+    "bestla_device_gmem_size": (_sz, [_p]),
+    "bestla_device_malloc": (_p, [_sz, _p]),
+    "bestla_device_free": (None, [_p, _p]),
+    "bestla_device_memcpy": (None, [_p, _p, _sz, _p]),
+    "bestla_device_memcpy_sync": (None, [_p, _p, _sz, _p]),
+    "bestla_device_sync": (None, [_p]),
+    "bestla_device_storage_size": (_sz, []),
+    "bestla_device_load_storage": (None, [_p, _p, _p, _p]),
+    "bestla_device_f32f32_forward": (None, [_p, _p, _p, _i, _i, _i, _i, _i, _p, _p]),
+    "bestla_init": (None, []),
+    "bestla_set_threads": (_i, [_i]),
+    "bestla_get_thread_handle": (_p, []),
+    "bestla_f32f32_get_workspace_size": (C.c_ulonglong, [_i, _i, _i, _p]),
+    "bestla_f32f32_forward": (None, [_p, _p, _p, _i, _i, _i, _i, _i, _p]),
+    "bestla_fusion_add_f32f32_support": (_b, [_p, _i, _i, _i]),
+    "bestla_fusion_add_f32f32_forward": (None, [_p, _p, _p, _p, _i, _i, _i, _i, _i, _b, _p]),
+    "bestla_fusion_QKV_f32f32_get_workspace_size": (C.c_ulonglong, [_i, _i, _i, _p]),
+    "bestla_fusion_QKV_f32f32_support": (_b, [_p, _p, _p, _i, _i, _i]),
+    "bestla_fusion_QKV_f32f32_forward": (None, [_p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _p]),
+    "bestla_fusion_FFN_f32f32_get_workspace_size": (C.c_ulonglong, [_i, _i, _i, _i, _p, _p]),
+    "bestla_fusion_FFN_SiLu_f32f32_support": (_b, [_p, _p, _p, _i, _i, _i, _i]),
+    "bestla_fusion_FFN_SiLu_f32f32_forward": (None, [_p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _p]),
+    "bestla_fusion_FFN_Gelu_Mul_f32f32_support": (_b, [_p, _p, _p, _i, _i, _i, _i]),
+    "bestla_fusion_FFN_Gelu_Mul_f32f32_forward": (None, [_p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _p]),
+    "bestla_fusion_FFN_GeLu_f32f32_support": (_b, [_p, _p, _i, _i, _i, _i]),
+    "bestla_fusion_FFN_GeLu_f32f32_forward": (None, [_p, _p, _p, _p, _p, _i, _i, _i, _i, _p]),
+    "bestla_fusion_FFN_Add_GeLu_f32f32_support": (_b, [_p, _p, _i, _i, _i, _i]),
+    "bestla_fusion_FFN_Add_GeLu_f32f32_forward": (None, [_p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _b, _p]),
+    "bestla_unpackweight_fp32": (None, [_p, _i, _i, _p, _i]),
+    "bestla_packweight_copyattr": (None, [_p, _p, _i, _i, _i, _p]),
+    "BTLAGemmPackBSize": (_sz, [_sz, _sz, _sz, _u32, _u32, _b, _i, _p]),
+    "BTLAGemmQuantPackB": (_b, [_p, _p, _sz, _sz, _sz, _sz, _u32, _u32, _b, _i, _b, _p]),
+    "BTLAGemmPackB": (_b, [_p, _p, _p, _p, _sz, _sz, _sz, _sz, _u32, _u32, _b, _i, _p, _p]),
+    "BTLAGemmUnPackB": (_b, [_p, _p, _sz, _sz, _sz, _p]),
+    "BTLAGemmBatchDriver": (_b, [_sz, _sz, _sz, _sz, _p, _p, _p]),
+    "nad_last_error": (C.c_char_p, []),
+    "nad_clear_error": (None, []),
+    "nad_device_weight_size": (_sz, [_p]),
+    "nad_device_load": (_i, [_p, _p, _p, _sz, _p]),
+    "nad_weight_info": (_i, [_p, _p]),
+    "nad_blob_info": (_i, [_p, _p]),
+    "nad_device_forward": (_i, [_p, _i, _p, _p, _i, _i, _i, _i, _i, _i, _p, _i, _p, _i, _p]),
+    "nad_device_qkv_forward": (_i, [_p, _i, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _p]),
+    "nad_device_ffn_forward": (_i, [_p, _i, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _p]),
+    "nad_blob_split": (_sz, [_p, _i, _i, _i, _p, _sz]),
+    "nad_split_range": (_i, [_p, _i, _i, _i, _p, _p]),
+    "nad_synthetic_weight": (_i, [_p, _p, _sz, _i, _i, _i, _i, _i, _i, _u64, _p]),
+    "nad_synthetic_weight_size": (_sz, [_i, _i, _i, _i, _i, _i]),
+    "nad_device_unpack_fp32": (_i, [_p, _p, _p]),
+}
+
+
+class NativeLibraryMissing(RuntimeError):
+    pass
+
+
+_LIB = None
+
+
+def lib():
+    """The loaded libneural_amd.so (raises NativeLibraryMissing if it cannot be loaded)."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(LIB_PATH):
+        raise NativeLibraryMissing(f"{LIB_PATH} not found: build it with `make -C neural_amd` "
+                                   "(or __graft_entry__.build()); there is no non-native fallback")
+    L = C.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _LIB = L
+    return L
+
+
+def header_symbols():
+    """Function names declared in include/neural_amd.h."""
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    names = re.findall(r"\b([A-Za-z_][A-Za-z0-9_]*)\s*\(", text)
+    skip = {"if", "defined", "sizeof", "extern"}
+    return sorted({n for n in names if n not in skip and not n.isupper()})
+
+
+def last_error():
+    return lib().nad_last_error().decode()
+
+
+def check(rc, what):
+    if rc != 0:
+        raise RuntimeError(f"{what} failed: {last_error()}")

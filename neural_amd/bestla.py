@@ -1,0 +1,273 @@
+"""Python mirror of Neural Speed's BesTLA operator surface, backed by the MI355X C-ABI (libneural_amd.so).
+
+Reference entry points mirrored (paths relative to the reference repo root):
+  quantize()        <- bestla_quantize          neural_speed/models/model_utils/quant_utils.cpp:269-354
+  qpack()           <- bestla_qpack / Model.np_bestla_qpack
+                                                quant_utils.cpp:226-266, application/main_pybind.cpp:378-402
+  pack_size()       <- BTLAGemmPackBSize        neural_speed/core/layers/bestla_gemm.h:38-39
+  unpack()          <- BTLAGemmUnPackB / bestla_unpackweight_fp32
+  DeviceWeight      <- bestla_device_load_storage (ne_bestla.h:96; SYCL impl ne_bestla_sycl.cpp:94-144)
+  DeviceWeight.forward / f32f32_forward
+                    <- bestla_device_f32f32_forward (ne_bestla.h:97-98) / bestla_f32f32_forward (inner_product.cpp:28-36)
+  qkv_forward()     <- bestla_fusion_QKV_f32f32_forward (ip_fusion_qkv.cpp)
+  ffn_forward()     <- bestla_fusion_FFN_SiLu_f32f32_forward / _Gelu_Mul_ (ip_fusion_ffn.cpp:734-755)
+  split()           <- TP weight split of model_files.h:1538-1660 (here exact: no re-quantization)
+
+Device buffers are torch tensors (plumbing only); every arithmetic op on the path runs in the HIP kernels.
+"""
+import ctypes as C
+
+import numpy as np
+
+from ._lib import check, last_error, lib
+
+# BTLA_DTYPE (bestla/bestla/bestla.h:38-87)
+F32, F16, BF16 = 32, 16, 16 | (1 << 16)
+S8, S4, S2 = 8 | 0x100, 4 | 0x100, 2 | 0x100
+# ne_comp_type (neural_speed/core/data_types.h:57-63)
+COMP_UNDEF, COMP_F32, COMP_BF16, COMP_F16, COMP_INT8 = 0, 1, 2, 3, 4
+# activation dtypes / epilogues of the native API
+ACT_F32, ACT_F16, ACT_BF16 = 0, 1, 2
+EPI_NONE, EPI_BIAS, EPI_SILU_MUL, EPI_GELU_MUL, EPI_GELU, EPI_ADD_GELU, EPI_SILU, EPI_RES_ADD = range(8)
+
+_WEIGHT_DTYPES = {"int4": S4, "int8": S8, "int2": S2}
+_SCALE_DTYPES = {"fp32": F32, "bf16": BF16, "fp16": F16}
+_COMP = {"int8": COMP_INT8, "bf16": COMP_BF16, "fp16": COMP_F16, "fp32": COMP_F32, "auto": COMP_UNDEF}
+BITS = {S4: 4, S2: 2, S8: 8}
+
+
+def _ptr(a):
+    if a is None:
+        return None
+    if isinstance(a, np.ndarray):
+        return a.ctypes.data_as(C.c_void_p)
+    return C.c_void_p(a.data_ptr())
+
+
+def _aligned_buffer(size):
+    """64-byte aligned, zero-filled uint8 numpy buffer (the blob serializer aligns relative to the base)."""
+    raw = np.zeros(size + 64, np.uint8)
+    off = (-raw.ctypes.data) % 64
+    return raw[off:off + size]
+
+
+def parse_weight_dtype(s):
+    if s not in _WEIGHT_DTYPES:
+        raise ValueError(f"unsupported weight_dtype {s!r} (supported: {sorted(_WEIGHT_DTYPES)})")
+    return _WEIGHT_DTYPES[s]
+
+
+def pack_size(n, k, block_size, weight_dtype=S4, scale_dtype=F32, asym=False, comp=COMP_INT8, shuffle=False):
+    L = lib()
+    dummy = C.c_int(0)
+    return L.BTLAGemmPackBSize(n, k, block_size, weight_dtype, scale_dtype, bool(asym), comp,
+                               C.byref(dummy) if shuffle else None)
+
+
+def quantize(w_nk, group_size=32, weight_dtype="int4", scale_dtype="fp32", alg="sym", compute_dtype="int8"):
+    """bestla_quantize (quant_utils.cpp:269-354): fp32 torch-layout weight [N][K] -> packed BTLA blob (uint8)."""
+    w = np.ascontiguousarray(w_nk, dtype=np.float32)
+    n, k = w.shape
+    qt = parse_weight_dtype(weight_dtype)
+    st = _SCALE_DTYPES[scale_dtype]
+    gsize = k if group_size == -1 else group_size
+    asym = alg == "asym"
+    comp = _COMP[compute_dtype]
+    size = pack_size(n, k, gsize, qt, st, asym, comp)
+    if not size:
+        raise RuntimeError(f"no packing core for this configuration: {last_error()}")
+    blob = _aligned_buffer(size)
+    if not lib().BTLAGemmQuantPackB(_ptr(blob), _ptr(w), n, k, k, gsize, qt, st, asym, comp, True, None):
+        raise RuntimeError(f"BTLAGemmQuantPackB failed: {last_error()}")
+    return blob
+
+
+def qpack(int_weight, scales, zeros=None, g_idx=None, weight_dtype="int4", group_size=128, alg="sym",
+          scale_dtype="fp32", compute_dtype="int8"):
+    """bestla_qpack / np_bestla_qpack: pre-quantized int8 [K][N] (+ scales [K/g][N], zeros, g_idx) -> blob.
+    As in the reference (quant_utils.cpp:248-254) fp16 scale requests are stored as bf16."""
+    q = np.ascontiguousarray(int_weight, dtype=np.int8)
+    k, n = q.shape
+    s = np.ascontiguousarray(scales, dtype=np.float32)
+    asym = alg == "asym"
+    z = np.ascontiguousarray(zeros, dtype=np.int8) if (asym and zeros is not None and np.size(zeros)) else None
+    gi = np.ascontiguousarray(g_idx, dtype=np.int32) if (g_idx is not None and np.size(g_idx)) else None
+    qt = parse_weight_dtype(weight_dtype)
+    st = F32 if scale_dtype == "fp32" else BF16
+    gsize = k if group_size == -1 else group_size
+    comp = _COMP[compute_dtype]
+    size = pack_size(n, k, gsize, qt, st, asym, comp, gi is not None)
+    if not size:
+        raise RuntimeError(f"no packing core for this configuration: {last_error()}")
+    blob = _aligned_buffer(size)
+    if not lib().BTLAGemmPackB(_ptr(blob), _ptr(q), _ptr(s), _ptr(z), n, k, n, gsize, qt, st, asym, comp,
+                               _ptr(gi), None):
+        raise RuntimeError(f"BTLAGemmPackB failed: {last_error()}")
+    return blob
+
+
+BLOB_FIELDS = ["size", "prologue", "coreid", "npad", "kpad", "n", "k", "dtype", "bs", "scat", "zpt", "redt",
+               "cstep", "csize", "asym", "has_reduce", "has_shuffle", "q_off", "q_size", "s_off", "s_size",
+               "z_off", "z_size", "r_off", "r_size", "shf_off", "shf_size"]
+
+
+def blob_info(blob):
+    o = np.zeros(27, np.int64)
+    check(lib().nad_blob_info(_ptr(blob), _ptr(o)), "nad_blob_info")
+    return dict(zip(BLOB_FIELDS, (int(v) for v in o)))
+
+
+def unpack(blob):
+    """BTLAGemmUnPackB: dequantized fp32 [K][N]."""
+    inf = blob_info(blob)
+    out = np.zeros((inf["k"], inf["n"]), np.float32)
+    if not lib().BTLAGemmUnPackB(_ptr(out), _ptr(blob), inf["n"], inf["k"], inf["n"], None):
+        raise RuntimeError(f"BTLAGemmUnPackB failed: {last_error()}")
+    return out
+
+
+def split(blob, axis, rank, world):
+    """Exact TP shard of a blob: axis 0 splits N (TP_1D_ROW), axis 1 splits K by whole groups (TP_1D_COLUMN)."""
+    L = lib()
+    size = L.nad_blob_split(_ptr(blob), axis, rank, world, None, 0)
+    if not size:
+        raise RuntimeError(f"nad_blob_split failed: {last_error()}")
+    out = _aligned_buffer(size)
+    if L.nad_blob_split(_ptr(blob), axis, rank, world, _ptr(out), size) != size:
+        raise RuntimeError(f"nad_blob_split failed: {last_error()}")
+    return out
+
+
+def split_range(blob, axis, rank, world):
+    b, e = C.c_int(0), C.c_int(0)
+    check(lib().nad_split_range(_ptr(blob), axis, rank, world, C.byref(b), C.byref(e)), "nad_split_range")
+    return b.value, e.value
+
+
+# ---------------------------------------------------------------------------------------------------- device
+def _torch():
+    import torch
+    if not torch.cuda.is_available():
+        raise RuntimeError("neural_amd device ops need a ROCm GPU (torch.cuda.is_available() is False)")
+    return torch
+
+
+def _stream(stream=None):
+    torch = _torch()
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return C.c_void_p(s.cuda_stream)
+
+
+_ACT = {}
+
+
+def _act_code(t):
+    torch = _torch()
+    if not _ACT:
+        _ACT.update({torch.float32: ACT_F32, torch.float16: ACT_F16, torch.bfloat16: ACT_BF16})
+    if t.dtype not in _ACT:
+        raise TypeError(f"activation dtype {t.dtype} not supported (float32/float16/bfloat16)")
+    return _ACT[t.dtype]
+
+
+class DeviceWeight:
+    """A WOQ weight resident in HBM in the MFMA tile layout (woq_layout.h); the reference's ne_tensor device
+    storage: `desc` plays the role of the embedded descriptor (devstor), `mem` of the device buffer."""
+
+    def __init__(self, blob=None, device=None, stream=None, _desc=None, _mem=None):
+        torch = _torch()
+        L = lib()
+        self.desc = (C.c_uint8 * L.bestla_device_storage_size())()
+        if blob is not None:
+            blob = np.ascontiguousarray(blob)
+            need = L.nad_device_weight_size(_ptr(blob))
+            if not need:
+                raise RuntimeError(f"unsupported blob: {last_error()}")
+            self.mem = torch.empty(need, dtype=torch.uint8, device=device or "cuda")
+            check(L.nad_device_load(_ptr(blob), self.desc, _ptr(self.mem), need, _stream(stream)),
+                  "nad_device_load")
+        else:
+            self.mem = _mem
+            C.memmove(self.desc, _desc, len(self.desc))
+        o = np.zeros(12, np.int64)
+        check(L.nad_weight_info(self.desc, _ptr(o)), "nad_weight_info")
+        (_, self.bits, self.n, self.k, self.blocksize, self.ns, self.nt, self.ng, self.scale_t, self.asym,
+         self.has_shuffle, self.bytes) = (int(v) for v in o)
+
+    @classmethod
+    def synthetic(cls, bits, n, k, group_size=128, scale_dtype="fp16", asym=False, seed=0, device=None, stream=None):
+        torch = _torch()
+        L = lib()
+        st = {"fp32": 0, "bf16": 1, "fp16": 2}[scale_dtype]
+        need = L.nad_synthetic_weight_size(bits, n, k, group_size, st, int(asym))
+        mem = torch.empty(need, dtype=torch.uint8, device=device or "cuda")
+        desc = (C.c_uint8 * L.bestla_device_storage_size())()
+        check(L.nad_synthetic_weight(desc, _ptr(mem), need, bits, n, k, group_size, st, int(asym), seed,
+                                     _stream(stream)), "nad_synthetic_weight")
+        return cls(_desc=desc, _mem=mem)
+
+    def forward(self, x, out=None, epilogue=EPI_NONE, bias=None, residual=None, stream=None):
+        """out[m][n] = epi(sum_k x[m][k] * W[n][k]); x: cuda [M][K] fp32/fp16/bf16 (row stride honoured)."""
+        torch = _torch()
+        m, k = x.shape
+        assert k == self.k, (k, self.k)
+        if out is None:
+            out = torch.empty((m, self.n), dtype=torch.float32, device=x.device)
+        bias_ld = 0 if bias is None or bias.dim() == 1 else bias.stride(0)
+        check(lib().nad_device_forward(_ptr(x), _act_code(x), self.desc, _ptr(out), m, self.n, k, x.stride(0),
+                                       out.stride(0), epilogue, _ptr(bias), bias_ld, _ptr(residual),
+                                       residual.stride(0) if residual is not None else 0, _stream(stream)),
+              "nad_device_forward")
+        return out
+
+    __call__ = forward
+
+    def unpack(self, stream=None):
+        """dequantized fp32 [K][N] read back from the device tile layout (repack exactness check)."""
+        out = np.zeros((self.k, self.n), np.float32)
+        check(lib().nad_device_unpack_fp32(self.desc, _ptr(out), _stream(stream)), "nad_device_unpack_fp32")
+        return out
+
+
+def f32f32_forward(activation, weight, output, m, n, k, lda, ldo, stream=None):
+    """bestla_device_f32f32_forward with raw device tensors (void result; errors via last_error)."""
+    L = lib()
+    L.nad_clear_error()
+    L.bestla_device_f32f32_forward(_ptr(activation), weight.desc, _ptr(output), m, n, k, lda, ldo, None,
+                                   _stream(stream))
+    err = last_error()
+    if err:
+        raise RuntimeError(err)
+    return output
+
+
+def qkv_forward(x, wq, wk, wv, out=None, stream=None):
+    """Fused Q/K/V: returns (q, k, v) fp32, written into out[3][M][N] when given (reference layout)."""
+    torch = _torch()
+    m = x.shape[0]
+    if out is None:
+        oq = torch.empty((m, wq.n), dtype=torch.float32, device=x.device)
+        ok = torch.empty((m, wk.n), dtype=torch.float32, device=x.device)
+        ov = torch.empty((m, wv.n), dtype=torch.float32, device=x.device)
+    else:
+        oq, ok, ov = out[0], out[1], out[2]
+    check(lib().nad_device_qkv_forward(_ptr(x), _act_code(x), wq.desc, wk.desc, wv.desc, _ptr(oq), _ptr(ok),
+                                       _ptr(ov), m, x.shape[1], x.stride(0), oq.stride(0), ok.stride(0),
+                                       ov.stride(0), _stream(stream)), "nad_device_qkv_forward")
+    return oq, ok, ov
+
+
+def ffn_forward(x, w1, w2, w3, act="silu", tmp1=None, tmp2=None, out=None, stream=None):
+    """Fused FFN: out = (act(x.W1^T) * (x.W3^T)) . W2^T  (ip_fusion_ffn.cpp:407-457)."""
+    torch = _torch()
+    m, fin = x.shape
+    fmid, fout = w1.n, w2.n
+    dev = x.device
+    tmp1 = torch.empty((m, fmid), dtype=torch.float32, device=dev) if tmp1 is None else tmp1
+    tmp2 = torch.empty((m, fmid), dtype=torch.float32, device=dev) if tmp2 is None else tmp2
+    out = torch.empty((m, fout), dtype=torch.float32, device=dev) if out is None else out
+    epi = EPI_SILU_MUL if act == "silu" else EPI_GELU_MUL
+    check(lib().nad_device_ffn_forward(_ptr(x), _act_code(x), w1.desc, w2.desc, w3.desc, _ptr(tmp1), _ptr(tmp2),
+                                       _ptr(out), m, fin, fmid, fout, x.stride(0), epi, _stream(stream)),
+          "nad_device_ffn_forward")
+    return out

@@ -1,0 +1,507 @@
+// btla_format.cpp -- bit-exact reader/writer/packer for Neural Speed's BTLA weight blobs (host side).
+// Compiled with g++ -ffp-contract=off: the quantizer must round exactly like the reference's scalar code.
+#include "btla_format.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <limits>
+#include <thread>
+#include <vector>
+
+namespace nad {
+
+namespace {
+
+template <typename F>
+void parallel_for(int n, F&& f) {
+  int hw = int(std::thread::hardware_concurrency());
+  const char* env = std::getenv("NAD_HOST_THREADS");
+  if (env) hw = std::atoi(env);
+  int nth = std::max(1, std::min({hw, n, 32}));
+  if (nth <= 1) {
+    for (int i = 0; i < n; i++) f(i);
+    return;
+  }
+  std::vector<std::thread> th;
+  th.reserve(nth);
+  for (int t = 0; t < nth; t++)
+    th.emplace_back([&, t]() {
+      for (int i = t; i < n; i += nth) f(i);
+    });
+  for (auto& x : th) x.join();
+}
+
+inline size_t updiv(size_t a, size_t b) { return (a + b - 1) / b; }
+inline size_t padto(size_t a, size_t b) { return updiv(a, b) * b; }
+
+struct Writer {
+  int8_t* p;
+  template <typename T>
+  void put(T v) {
+    std::memcpy(p, &v, sizeof(T));
+    p += sizeof(T);
+  }
+};
+struct Reader {
+  const int8_t* p;
+  template <typename T>
+  T get() {
+    T v;
+    std::memcpy(&v, p, sizeof(T));
+    p += sizeof(T);
+    return v;
+  }
+};
+
+// ObjectAlignedBuffer<64> (bestla_storage.h:59-110): {size, offset-to-64B-boundary, pad, bytes}
+uint64_t put_aligned(Writer& w, const int8_t* base, uint64_t bytes) {
+  w.put<uint64_t>(bytes);
+  uintptr_t tmp = reinterpret_cast<uintptr_t>(w.p + sizeof(uint64_t));
+  uint64_t off = ((tmp + 63) / 64) * 64 - tmp;
+  w.put<uint64_t>(off);
+  w.p += off;
+  uint64_t at = uint64_t(w.p - base);
+  w.p += bytes;
+  return at;
+}
+uint64_t get_aligned(Reader& r, const int8_t* base, uint64_t* bytes) {
+  *bytes = r.get<uint64_t>();
+  uint64_t off = r.get<uint64_t>();
+  r.p += off;
+  uint64_t at = uint64_t(r.p - base);
+  r.p += *bytes;
+  return at;
+}
+
+// std::min/std::max argument-order semantics, and x86 cvttss2si for float->int (NaN/overflow -> INT_MIN)
+inline float smax(float a, float b) { return (a < b) ? b : a; }
+inline float smin(float a, float b) { return (b < a) ? b : a; }
+inline int32_t f2i(float x) {
+  if (std::isnan(x) || x >= 2147483648.0f || x < -2147483648.0f) return std::numeric_limits<int32_t>::min();
+  return int32_t(x);
+}
+inline int32_t wrap_add(int32_t a, int32_t b) { return int32_t(uint32_t(a) + uint32_t(b)); }
+
+}  // namespace
+
+// ----------------------------------------------------------------------------------------------- cores
+static uint64_t make_core(int ntile, int packrow, int comp, int isa) {
+  return uint64_t(ntile) | (uint64_t(packrow) << 8) | (uint64_t(comp) << 16) | (uint64_t(isa) << 32);
+}
+
+uint64_t core_id_by_name(const std::string& s) {
+  // typedefs of neural_speed/core/layers/bestla_defs.h:36-54; ISA ids bestla.h:23-36; CompType bestla_gemm.h:22-50
+  if (s == "avx2") return make_core(24, 1, 0x000, 2);
+  if (s == "avx512f") return make_core(48, 1, 0x000, 4);
+  if (s == "amx_bf16") return make_core(48, 2, 0x011, 9);
+  if (s == "amx_fp16") return make_core(48, 2, 0x022, 11);
+  if (s == "avx512_vnni_kblock") return make_core(48, 4, 0x034, 6);
+  if (s == "avx512bw_kblock") return make_core(48, 4, 0x034, 5);
+  if (s == "avx_vnni_kblock") return make_core(24, 4, 0x034, 3);
+  if (s == "avx2_vnni_kblock") return make_core(24, 4, 0x034, 2);
+  if (s == "amx_int8_kblock") return make_core(48, 4, 0x034, 10);
+  if (s == "amx_int8_ss_kblock") return make_core(48, 4, 0x033, 10);
+  return 0;
+}
+
+CoreInfo core_info(uint64_t id) {
+  CoreInfo c;
+  c.ntile = int(id & 0xff);
+  c.packrow = int((id >> 8) & 0xff);
+  int comp = int((id >> 16) & 0xffff);
+  int isa = int((id >> 32) & 0xff);
+  int bt = (comp >> 4) & 0xf;  // CompTypeHelper::get_B
+  c.int_comp = (bt == 3 || bt == 4);
+  if (c.packrow == 1)
+    c.ktile = 1;  // Avx2N8P1 / Avx512fN16P1
+  else if (isa == 9 || isa == 11)
+    c.ktile = 32;  // Amx{bf16,fp16}N16P2
+  else if (isa == 10)
+    c.ktile = 64;  // Amxint8N16P4
+  else
+    c.ktile = 4;  // VNNI / BW kblock cores
+  return c;
+}
+
+int host_isa_profile() {
+  const char* e = std::getenv("NAD_HOST_ISA");
+  if (!e) return 0;
+  std::string s(e);
+  if (s == "avx512_vnni") return 1;
+  if (s == "avx512f") return 2;
+  if (s == "avx2") return 3;
+  return 0;
+}
+
+uint64_t select_core(int comp, uint32_t qtype, int bs, bool asym, int profile) {
+  const bool amx = profile == 0, vnni = profile <= 1, a512 = profile <= 2;
+  switch (comp) {
+    case kCompInt8:
+      if (dtype_is_int(qtype) && !(qtype == kS8 && asym)) {
+        if (amx && bs % 64 == 0) return core_id_by_name("amx_int8_kblock");
+        if (vnni && bs % 4 == 0) return core_id_by_name("avx512_vnni_kblock");
+        if (a512 && bs % 4 == 0) return core_id_by_name("avx512bw_kblock");
+        if (bs % 4 == 0) return core_id_by_name("avx2_vnni_kblock");
+      }
+      [[fallthrough]];
+    case kCompBF16:
+      if (amx && bs % 32 == 0) return core_id_by_name("amx_bf16");
+      [[fallthrough]];
+    case kCompF16:  // no AMX-FP16 on the emulated profiles
+    case kCompF32:
+    case kCompUndef:
+      return a512 ? core_id_by_name("avx512f") : core_id_by_name("avx2");
+    default:
+      return 0;
+  }
+}
+
+// ----------------------------------------------------------------------------------------------- blob
+Blob Blob::describe(int n, int k, int blocksize, uint32_t qtype, uint32_t scale_t, bool asym, uint64_t core_id,
+                    bool shuffle) {
+  Blob b;
+  CoreInfo ci = core_info(core_id);
+  b.core_id = core_id;
+  b.n = n;
+  b.k = k;
+  b.kpad = int(padto(size_t(k), size_t(ci.ktile)));
+  b.npad = int(padto(size_t(n), size_t(ci.ntile)));
+  b.blocksize = blocksize <= 0 ? b.kpad : blocksize;
+  b.qtype = qtype;
+  b.scale_t = scale_t;
+  b.zp_t = kS8;
+  b.red_t = kBF16;
+  b.asym = asym;
+  b.has_reduce = ci.int_comp;
+  b.has_shuffle = shuffle;
+  b.q_size = updiv(uint64_t(b.npad) * b.kpad * dtype_bits(qtype), 8);
+  b.cstep = b.npad;
+  b.csize = uint64_t(b.ngroups()) * b.npad;
+  b.s_size = b.csize * b.scale_bytes();
+  b.z_size = asym ? b.csize : 0;
+  b.r_size = b.has_reduce ? b.csize * 2 : 0;
+  b.shf_size = shuffle ? uint64_t(k) * 4 : 0;
+  // update_size(): every aligned buffer is charged size + 16 + 64, optional ones + 1 flag byte
+  uint64_t sz = 48 + (16 + b.q_size + 64) + 24 + (16 + b.s_size + 64);
+  sz += 1 + (asym ? 16 + b.z_size + 64 : 0);
+  sz += 1 + (b.has_reduce ? 16 + b.r_size + 64 : 0);
+  sz += 1;
+  sz += 1 + (shuffle ? 16 + b.shf_size + 64 : 0);
+  b.size = padto(sz, 64);
+  return b;
+}
+
+void Blob::write_header(int8_t* base) {
+  Writer w{base};
+  w.put<uint64_t>(size);
+  w.put<uint32_t>(prologue);
+  w.put<uint64_t>(core_id);
+  w.put<int32_t>(npad);
+  w.put<int32_t>(kpad);
+  w.put<int32_t>(n);
+  w.put<int32_t>(k);
+  w.put<uint32_t>(qtype);
+  w.put<int32_t>(blocksize);
+  w.put<int32_t>(dq_blocksize);
+  q_off = put_aligned(w, base, q_size);
+  w.put<uint32_t>(scale_t);
+  w.put<uint32_t>(zp_t);
+  w.put<uint32_t>(red_t);
+  w.put<int32_t>(cstep);
+  w.put<uint64_t>(csize);
+  s_off = put_aligned(w, base, s_size);
+  w.put<uint8_t>(asym ? 1 : 0);
+  if (asym) z_off = put_aligned(w, base, z_size);
+  w.put<uint8_t>(has_reduce ? 1 : 0);
+  if (has_reduce) r_off = put_aligned(w, base, r_size);
+  w.put<uint8_t>(0);
+  w.put<uint8_t>(has_shuffle ? 1 : 0);
+  if (has_shuffle) shf_off = put_aligned(w, base, shf_size);
+}
+
+bool Blob::parse(const void* buf, std::string* err) {
+  auto fail = [&](const char* m) {
+    if (err) *err = m;
+    return false;
+  };
+  if (!buf) return fail("null blob");
+  const int8_t* base = static_cast<const int8_t*>(buf);
+  Reader r{base};
+  size = r.get<uint64_t>();
+  prologue = r.get<uint32_t>();
+  if (prologue != 1) return fail("only WeightKBlockNInteger blobs (integer N-bit weights) are supported");
+  core_id = r.get<uint64_t>();
+  npad = r.get<int32_t>();
+  kpad = r.get<int32_t>();
+  n = r.get<int32_t>();
+  k = r.get<int32_t>();
+  qtype = r.get<uint32_t>();
+  blocksize = r.get<int32_t>();
+  dq_blocksize = r.get<int32_t>();
+  if (n <= 0 || k <= 0 || npad < n || kpad < k || blocksize <= 0) return fail("corrupt blob header");
+  q_off = get_aligned(r, base, &q_size);
+  scale_t = r.get<uint32_t>();
+  zp_t = r.get<uint32_t>();
+  red_t = r.get<uint32_t>();
+  cstep = r.get<int32_t>();
+  csize = r.get<uint64_t>();
+  s_off = get_aligned(r, base, &s_size);
+  asym = r.get<uint8_t>() != 0;
+  if (asym) z_off = get_aligned(r, base, &z_size);
+  has_reduce = r.get<uint8_t>() != 0;
+  if (has_reduce) r_off = get_aligned(r, base, &r_size);
+  if (r.get<uint8_t>() != 0) return fail("double-quantized (DQ8_BNB) scales are not supported");
+  has_shuffle = r.get<uint8_t>() != 0;
+  if (has_shuffle) shf_off = get_aligned(r, base, &shf_size);
+  if (qtype != kS4 && qtype != kS2 && qtype != kS8) return fail("weight dtype must be S4_CLIP, S2_CLIP or S8");
+  if (scale_t != kF32 && scale_t != kBF16 && scale_t != kF16) return fail("scale dtype must be F32, BF16 or F16");
+  CoreInfo ci = core_info(core_id);
+  if (ci.ntile <= 0 || (ci.packrow != 1 && ci.packrow != 2 && ci.packrow != 4)) return fail("unknown core id");
+  if (npad % ci.ntile || kpad % ci.packrow) return fail("blob padding does not match its core");
+  return true;
+}
+
+// ----------------------------------------------------------------------------------------------- scales
+uint16_t f32_to_bf16_rne(float v) {
+  uint32_t u;
+  std::memcpy(&u, &v, 4);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return uint16_t(u >> 16);
+}
+float bf16_to_f32(uint16_t x) {
+  uint32_t u = uint32_t(x) << 16;
+  float f;
+  std::memcpy(&f, &u, 4);
+  return f;
+}
+uint16_t f32_to_f16_rne(float v) {
+  uint32_t x;
+  std::memcpy(&x, &v, 4);
+  uint32_t sign = (x >> 16) & 0x8000u, ax = x & 0x7FFFFFFFu;
+  if (ax > 0x7F800000u) return uint16_t(sign | 0x7E00u | ((ax >> 13) & 0x3FFu));
+  if (ax >= 0x477FF000u) return uint16_t(sign | 0x7C00u);
+  if (ax < 0x38800000u) {
+    if (ax < 0x33000000u) return uint16_t(sign);
+    uint32_t e = ax >> 23, mant = (ax & 0x7FFFFFu) | 0x800000u, sh = 126 - e;
+    uint32_t q = mant >> sh, rem = mant & ((1u << sh) - 1), half = 1u << (sh - 1);
+    if (rem > half || (rem == half && (q & 1u))) q++;
+    return uint16_t(sign | q);
+  }
+  uint32_t q = (((ax >> 23) - 112) << 10) | ((ax & 0x7FFFFFu) >> 13), rem = ax & 0x1FFFu;
+  if (rem > 0x1000u || (rem == 0x1000u && (q & 1u))) q++;
+  return uint16_t(sign | q);
+}
+float f16_to_f32(uint16_t h) {
+  uint32_t sign = uint32_t(h & 0x8000u) << 16, e = (h >> 10) & 0x1f, m = h & 0x3ff, u;
+  if (e == 0) {
+    if (m == 0) {
+      u = sign;
+    } else {  // subnormal: normalise
+      int sh = 0;
+      while (!(m & 0x400)) {
+        m <<= 1;
+        sh++;
+      }
+      u = sign | (uint32_t(113 - sh) << 23) | ((m & 0x3ff) << 13);
+    }
+  } else if (e == 31) {
+    u = sign | 0x7F800000u | (m << 13);
+  } else {
+    u = sign | ((e + 112) << 23) | (m << 13);
+  }
+  float f;
+  std::memcpy(&f, &u, 4);
+  return f;
+}
+
+static inline void store_scale(uint8_t* sp, size_t i, uint32_t t, float v) {
+  if (t == kF32) {
+    std::memcpy(sp + i * 4, &v, 4);
+  } else {
+    uint16_t h = (t == kBF16) ? f32_to_bf16_rne(v) : f32_to_f16_rne(v);
+    std::memcpy(sp + i * 2, &h, 2);
+  }
+}
+static inline float load_scale(const uint8_t* sp, size_t i, uint32_t t) {
+  if (t == kF32) {
+    float v;
+    std::memcpy(&v, sp + i * 4, 4);
+    return v;
+  }
+  uint16_t h;
+  std::memcpy(&h, sp + i * 2, 2);
+  return t == kBF16 ? bf16_to_f32(h) : f16_to_f32(h);
+}
+
+// ----------------------------------------------------------------------------------------------- quantizer
+void quantize_kblock(const float* src, int K, int N, int ld_src, int bs, int bits, int8_t* q, float* scales,
+                     int8_t* zp) {
+  const int full = 1 << (bits - 1), sym = full - 1;
+  auto clip = [&](int32_t s) { return s < -full ? -full : (s > sym ? sym : s); };
+  const int nblk = int(updiv(size_t(K), size_t(bs)));
+  // parallel over (column chunk): each column is independent in the reference algorithm
+  const int CH = 64;
+  parallel_for(int(updiv(size_t(N), CH)), [&](int c) {
+    int n0 = c * CH, n1 = std::min(N, n0 + CH);
+    for (int i = n0; i < n1; i++) {
+      for (int g = 0; g < nblk; g++) {
+        int j = g * bs, len = std::min(bs, K - j);
+        if (!zp) {  // sNauto sym (kernel_ref.h:1650-1671)
+          float maxval = std::numeric_limits<float>::min(), minval = std::numeric_limits<float>::max(), absmax = 0;
+          for (int t = 0; t < len; t++) {
+            float x = src[size_t(j + t) * ld_src + i];
+            maxval = smax(maxval, x);
+            minval = smin(minval, x);
+            absmax = smax(absmax, std::fabs(x));
+          }
+          float nval = float(sym) + 0.5f, sum = maxval + minval;
+          if (std::fabs(sum) >= absmax / float(full)) nval = sum > 0.f ? float(-full) : float(full);
+          float scale = absmax / nval, rscale = 1.f / scale;
+          scales[size_t(g) * N + i] = scale;
+          for (int t = 0; t < len; t++) {
+            float v = std::roundf(src[size_t(j + t) * ld_src + i] * rscale);  // cast<float,int8_t>
+            v = smax(smin(v, 127.f), -128.f);
+            q[size_t(j + t) * N + i] = int8_t(clip(int8_t(f2i(v))));
+          }
+        } else {  // sNauto asym (kernel_ref.h:1673-1693)
+          float maxval = 0.f, minval = 0.f;
+          for (int t = 0; t < len; t++) {
+            float x = src[size_t(j + t) * ld_src + i];
+            maxval = smax(maxval, x);
+            minval = smin(minval, x);
+          }
+          float scale = (maxval - minval) / float((1 << bits) - 1), rscale = 1.f / scale;
+          scales[size_t(g) * N + i] = scale;
+          int32_t z = clip(wrap_add(f2i(std::roundf((0 - minval) * rscale)), -full));
+          zp[size_t(g) * N + i] = int8_t(z);
+          for (int t = 0; t < len; t++)
+            q[size_t(j + t) * N + i] =
+                int8_t(clip(wrap_add(f2i(std::roundf(src[size_t(j + t) * ld_src + i] * rscale)), z)));
+        }
+      }
+    }
+  });
+}
+
+// ----------------------------------------------------------------------------------------------- pack
+// element (k, n) -> flat index in the [NPad/NTILE][KPad/PR][NTILE][PR] interleave (kernel_ref.h:39-59)
+static inline size_t ilv_index(int k, int n, int kpad, int ntile, int pr) {
+  return size_t(n / ntile) * ntile * kpad + size_t(k / pr) * ntile * pr + size_t(n % ntile) * pr + (k % pr);
+}
+
+bool pack_quantized(Blob& b, int8_t* base, const int8_t* Q, int ldq, const float* S, const int8_t* Z,
+                    const int* g_idx, std::string* err) {
+  const CoreInfo ci = core_info(b.core_id);
+  const int bits = dtype_bits(b.qtype);
+  if (bits != 4 && bits != 2 && bits != 8) {
+    if (err) *err = "unsupported weight bits";
+    return false;
+  }
+  const int rawnk = b.ngroups_k(), nk = b.ngroups();
+  // setQuantCorrection (bestla_prologue_b.h:244-335): scales/zp with zero padding rows and columns
+  uint8_t* sp = reinterpret_cast<uint8_t*>(base + b.s_off);
+  parallel_for(nk, [&](int g) {
+    for (int n = 0; n < b.npad; n++)
+      store_scale(sp, size_t(g) * b.npad + n, b.scale_t, (g < rawnk && n < b.n) ? S[size_t(g) * b.n + n] : 0.f);
+    if (b.asym) {
+      int8_t* zp = base + b.z_off;
+      for (int n = 0; n < b.npad; n++)
+        zp[size_t(g) * b.npad + n] = (g < rawnk && n < b.n) ? Z[size_t(g) * b.n + n] : 0;
+    }
+  });
+  if (b.has_shuffle) {  // setShuffleIndices (bestla_prologue_b.h:337-356)
+    int* lut = reinterpret_cast<int*>(base + b.shf_off);
+    std::vector<int> cnt(size_t(b.ngroups_k()), 0);
+    for (int i = 0; i < b.k; i++) {
+      int g = g_idx[i];
+      if (g < 0 || g >= b.ngroups_k() || cnt[g] >= b.blocksize) {
+        if (err) *err = "g_idx out of range or group overfull";
+        return false;
+      }
+      lut[size_t(g) * b.blocksize + cnt[g]++] = i;
+    }
+  }
+  // reorderWeight + compressWeight: walk the interleaved order directly, packing as we go
+  uint8_t* qp = reinterpret_cast<uint8_t*>(base + b.q_off);
+  const int ntile = ci.ntile, pr = ci.packrow, kpad = b.kpad;
+  const int per_byte = 8 / bits;
+  const int8_t bias = int8_t(bits == 8 ? 0 : (1 << (bits - 1)));
+  const size_t stripe_elems = size_t(ntile) * kpad;
+  parallel_for(b.npad / ntile, [&](int st) {
+    size_t e0 = size_t(st) * stripe_elems;
+    for (size_t e = 0; e < stripe_elems; e += per_byte) {
+      uint8_t byte = 0;
+      for (int t = 0; t < per_byte; t++) {
+        size_t el = e + t;  // within stripe: [KPad/PR][NTILE][PR]
+        int kk = int(el / (size_t(ntile) * pr)) * pr + int(el % pr);
+        int nn = st * ntile + int((el / pr) % ntile);
+        int8_t v = (kk < b.k && nn < b.n) ? Q[size_t(kk) * ldq + nn] : 0;
+        if (bits == 8) {
+          qp[e0 + e] = uint8_t(v);
+        } else {
+          byte |= uint8_t((uint8_t(v + bias) & ((1u << bits) - 1)) << (bits * t));
+        }
+      }
+      if (bits != 8) qp[(e0 + e) / per_byte] = byte;
+    }
+  });
+  (void)ilv_index;
+  if (b.has_reduce) {  // reduceWeight (bestla_prologue_b.h:455-470): sequential float sum per (block, n) -> bf16
+    uint16_t* rp = reinterpret_cast<uint16_t*>(base + b.r_off);
+    parallel_for(rawnk, [&](int g) {
+      int k0 = g * b.blocksize, k1 = std::min(b.k, k0 + b.blocksize);
+      for (int n = 0; n < b.n; n++) {
+        float s = load_scale(sp, size_t(g) * b.cstep + n, b.scale_t);
+        int z = b.asym ? (base + b.z_off)[size_t(g) * b.cstep + n] : 0;
+        float t = 0.f;
+        for (int kk = k0; kk < k1; kk++) t += float(Q[size_t(kk) * ldq + n] - z) * s;
+        rp[size_t(g) * b.cstep + n] = f32_to_bf16_rne(t);
+      }
+    });
+  }
+  return true;
+}
+
+static inline int8_t read_q(const Blob& b, const uint8_t* qp, const CoreInfo& ci, int kk, int nn) {
+  size_t e = ilv_index(kk, nn, b.kpad, ci.ntile, ci.packrow);
+  int bits = dtype_bits(b.qtype);
+  if (bits == 8) return int8_t(qp[e]);
+  int per = 8 / bits;
+  int v = (qp[e / per] >> (bits * (e % per))) & ((1 << bits) - 1);
+  return int8_t(v - (1 << (bits - 1)));
+}
+
+void unpack_quantized(const Blob& b, const int8_t* base, int8_t* Q, float* S, int8_t* Z, int* shuffle) {
+  const CoreInfo ci = core_info(b.core_id);
+  const uint8_t* qp = reinterpret_cast<const uint8_t*>(base + b.q_off);
+  const uint8_t* sp = reinterpret_cast<const uint8_t*>(base + b.s_off);
+  if (Q)
+    parallel_for(b.k, [&](int kk) {
+      for (int nn = 0; nn < b.n; nn++) Q[size_t(kk) * b.n + nn] = read_q(b, qp, ci, kk, nn);
+    });
+  for (int g = 0; g < b.ngroups_k(); g++)
+    for (int nn = 0; nn < b.n; nn++) {
+      size_t ci2 = size_t(g) * b.cstep + nn;
+      if (S) S[size_t(g) * b.n + nn] = load_scale(sp, ci2, b.scale_t);
+      if (Z) Z[size_t(g) * b.n + nn] = b.asym ? base[b.z_off + ci2] : 0;
+    }
+  if (shuffle && b.has_shuffle) std::memcpy(shuffle, base + b.shf_off, size_t(b.k) * 4);
+}
+
+void unpack_fp32(const Blob& b, const int8_t* base, float* W, int ldw) {
+  const CoreInfo ci = core_info(b.core_id);
+  const uint8_t* qp = reinterpret_cast<const uint8_t*>(base + b.q_off);
+  const uint8_t* sp = reinterpret_cast<const uint8_t*>(base + b.s_off);
+  parallel_for(b.k, [&](int kk) {
+    int g = kk / b.blocksize;
+    for (int nn = 0; nn < b.n; nn++) {
+      size_t c = size_t(g) * b.cstep + nn;
+      int z = b.asym ? base[b.z_off + c] : 0;
+      W[size_t(kk) * ldw + nn] = float(read_q(b, qp, ci, kk, nn) - z) * load_scale(sp, c, b.scale_t);
+    }
+  });
+}
+
+}  // namespace nad

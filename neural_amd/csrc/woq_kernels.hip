@@ -1,0 +1,641 @@
+// woq_kernels.hip -- hand-written CDNA4 (gfx950) kernels for the weight-only-quantized matmul hot path.
+//
+//   nad_repack_kernel   : BTLA blob (any core layout, NTILE 24/48, PACK_ROW 1/2/4; S4/S2/S8) -> tile layout
+//                         (woq_layout.h).  Replaces convertTransStorage + fromHost of the SYCL backend
+//                         (bestla/bestla/bestla_prologue_b.h:129-150, neural_speed/core/layers/ne_bestla_sycl.cpp:94-144).
+//   woq_skinny_kernel   : M <= 16 ("GEMV", decode).  Replaces GEMVWrapper::gemv_kblock -> gemv_{4,2}bit_fp32_fp32
+//                         (bestla/bestla/bestla_wrapper.h:364-468, kernel_ref.h:2489-2531,2712-2760).
+//                         One wave streams one 16-column stripe over a K slice with fully coalesced 16 B/lane loads
+//                         of 1 KiB tiles, dequantizes nibbles/crumbs/bytes to exact integer fp16 with the 0x6400
+//                         magic (no LUT, no shuffles), and runs v_mfma_f32_16x16x32_f16 with the activation rows in
+//                         the A operand.  fp32 activations are split hi+lo into the 16 MFMA rows (M<=8) or into two
+//                         MFMA passes (M<=16) so the result is fp32-accurate; group scales are applied in fp32 once
+//                         per group; the K slices of a stripe are reduced in LDS inside the workgroup (deterministic,
+//                         no atomics).  HBM-bound by design: every weight byte is read exactly once.
+//   woq_gemm_kernel     : M > 16 (prefill).  Replaces LauncherBase::gemm/run_block + getFpWeight + the AMX/AVX512
+//                         GemmCore (bestla_wrapper.h:481-542, bestla_prologue_b.h:732-838).  128x128 block tile,
+//                         4 waves of 64x64; A staged fp32->fp16 into an XOR-swizzled LDS tile; B tiles go HBM ->
+//                         VGPR -> exact-integer fp16 fragments with no LDS round trip; per-group fp32 scaling of a
+//                         group accumulator keeps the weight dequant exact.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "woq_kernels.h"
+
+namespace nad {
+
+typedef _Float16 h2_t __attribute__((ext_vector_type(2)));
+typedef _Float16 h8_t __attribute__((ext_vector_type(8)));
+typedef float f4_t __attribute__((ext_vector_type(4)));
+typedef uint32_t u4_t __attribute__((ext_vector_type(4)));
+
+// ------------------------------------------------------------------------------------------------ helpers
+__device__ __forceinline__ float bf16_bits_to_f32(uint16_t x) { return __uint_as_float(uint32_t(x) << 16); }
+__device__ __forceinline__ float f16_bits_to_f32(uint16_t x) {
+  return float(__builtin_bit_cast(_Float16, x));
+}
+
+__device__ __forceinline__ float load_scale(const void* p, size_t i, int st) {
+  if (st == kScaleF32) return static_cast<const float*>(p)[i];
+  uint16_t h = static_cast<const uint16_t*>(p)[i];
+  return st == kScaleBF16 ? bf16_bits_to_f32(h) : f16_bits_to_f32(h);
+}
+
+__device__ __forceinline__ h2_t as_h2(uint32_t v) { return __builtin_bit_cast(h2_t, v); }
+
+// One MFMA step's B fragment (8 fp16 = exact integers q - zp) from the packed dwords.
+//   c2 = (-(1024 + bias + zp)) broadcast as half2.
+template <int BITS>
+__device__ __forceinline__ h8_t dequant_step(const u4_t& b, int d, h2_t c2) {
+  h2_t p0, p1, p2, p3;
+  if constexpr (BITS == 4) {
+    uint32_t w = b[d];
+    p0 = as_h2(((w >> 0) & 0x000F000Fu) | 0x64006400u);
+    p1 = as_h2(((w >> 4) & 0x000F000Fu) | 0x64006400u);
+    p2 = as_h2(((w >> 8) & 0x000F000Fu) | 0x64006400u);
+    p3 = as_h2(((w >> 12) & 0x000F000Fu) | 0x64006400u);
+  } else if constexpr (BITS == 2) {
+    uint32_t w = b[d >> 1];
+    int sh = (d & 1) * 8;
+    p0 = as_h2(((w >> (sh + 0)) & 0x00030003u) | 0x64006400u);
+    p1 = as_h2(((w >> (sh + 2)) & 0x00030003u) | 0x64006400u);
+    p2 = as_h2(((w >> (sh + 4)) & 0x00030003u) | 0x64006400u);
+    p3 = as_h2(((w >> (sh + 6)) & 0x00030003u) | 0x64006400u);
+  } else {
+    uint32_t w0 = b[2 * d], w1 = b[2 * d + 1];
+    p0 = as_h2(__builtin_amdgcn_perm(0x64646464u, w0, 0x04010400u));
+    p1 = as_h2(__builtin_amdgcn_perm(0x64646464u, w0, 0x04030402u));
+    p2 = as_h2(__builtin_amdgcn_perm(0x64646464u, w1, 0x04010400u));
+    p3 = as_h2(__builtin_amdgcn_perm(0x64646464u, w1, 0x04030402u));
+  }
+  p0 += c2;
+  p1 += c2;
+  p2 += c2;
+  p3 += c2;
+  h8_t r;
+  r[0] = p0[0];
+  r[1] = p0[1];
+  r[2] = p1[0];
+  r[3] = p1[1];
+  r[4] = p2[0];
+  r[5] = p2[1];
+  r[6] = p3[0];
+  r[7] = p3[1];
+  return r;
+}
+
+template <int BITS>
+__device__ __forceinline__ constexpr int bias_of() {
+  return BITS == 4 ? 8 : (BITS == 2 ? 2 : 128);
+}
+
+__device__ __forceinline__ h2_t zp_const(int bias_plus_zp) {
+  _Float16 c = _Float16(-(1024 + bias_plus_zp));
+  h2_t r;
+  r[0] = c;
+  r[1] = c;
+  return r;
+}
+
+// activation element loaders -> float
+template <int AT>
+__device__ __forceinline__ float a_elem(const void* A, size_t idx) {
+  if constexpr (AT == kActF32) return static_cast<const float*>(A)[idx];
+  if constexpr (AT == kActF16) return float(static_cast<const _Float16*>(A)[idx]);
+  return bf16_bits_to_f32(static_cast<const uint16_t*>(A)[idx]);
+}
+
+// load 8 consecutive activation values A[row][k0..k0+7] (zero beyond K), optional act-order gather
+template <int AT>
+__device__ __forceinline__ void load_a8(const void* A, int lda, int row, int k0, int K, const int32_t* shf, bool vec_ok,
+                                        float (&v)[8]) {
+  const size_t base = size_t(row) * lda;
+  if (shf == nullptr && vec_ok && k0 + 8 <= K) {
+    if constexpr (AT == kActF32) {
+      const float4* p = reinterpret_cast<const float4*>(static_cast<const float*>(A) + base + k0);
+      float4 x = p[0], y = p[1];
+      v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
+      v[4] = y.x; v[5] = y.y; v[6] = y.z; v[7] = y.w;
+    } else {
+      uint4 x = *reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(A) + base + k0);
+      uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        if constexpr (AT == kActF16) {
+          h2_t h = as_h2(w[i]);
+          v[2 * i] = float(h[0]);
+          v[2 * i + 1] = float(h[1]);
+        } else {
+          v[2 * i] = __uint_as_float(w[i] << 16);
+          v[2 * i + 1] = __uint_as_float(w[i] & 0xFFFF0000u);
+        }
+      }
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      int k = k0 + j;
+      v[j] = 0.f;
+      if (k < K) v[j] = a_elem<AT>(A, base + (shf ? shf[k] : k));
+    }
+  }
+}
+
+__device__ __forceinline__ float silu_f(float x) { return x / (1.0f + __expf(-x)); }
+__device__ __forceinline__ float gelu_f(float x) {
+  return 0.5f * x * (1.f + tanhf(0.7978845834732056f * (x + 0.044714998453855515f * x * x * x)));
+}
+
+// ------------------------------------------------------------------------------------------------ repack
+// One thread per output dword of the tile layout.
+__global__ void nad_repack_kernel(RepackArgs a) {
+  const uint64_t total = uint64_t(a.ns) * a.nt * 256;
+  const int KT = a.bits == 4 ? 128 : (a.bits == 2 ? 256 : 64);
+  for (uint64_t gid = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; gid < total;
+       gid += uint64_t(gridDim.x) * blockDim.x) {
+    const int dw = int(gid & 3);
+    const int lane = int((gid >> 2) & 63);
+    const uint64_t tile = gid >> 8;
+    const int t = int(tile % a.nt);
+    const int s = int(tile / a.nt);
+    const int n = s * 16 + (lane & 15);
+    const int kq = lane >> 4;
+    uint32_t out = 0;
+    const int per = 32 / a.bits;  // elements per dword
+    for (int p = 0; p < per; p++) {
+      int k;
+      if (a.bits == 4) {
+        int j = 2 * (p & 3) + (p >> 2);
+        k = t * KT + dw * 32 + kq * 8 + j;
+      } else if (a.bits == 2) {
+        int h = (p & 7) >> 2, j = 2 * (p & 3) + (p >> 3);
+        int d = dw * 2 + h;
+        k = t * KT + d * 32 + kq * 8 + j;
+      } else {
+        int d = dw >> 1, j = (dw & 1) * 4 + p;
+        k = t * KT + d * 32 + kq * 8 + j;
+      }
+      uint32_t v;
+      if (n < a.n && k < a.k) {
+        const uint64_t e = uint64_t(n / a.ntile) * a.ntile * a.kpad + uint64_t(k / a.packrow) * a.ntile * a.packrow +
+                           uint64_t(n % a.ntile) * a.packrow + uint64_t(k % a.packrow);
+        if (a.bits == 4) {
+          v = (a.src_q[e >> 1] >> (4 * (e & 1))) & 0xF;  // stored nibble = q + 8
+        } else if (a.bits == 2) {
+          v = (a.src_q[e >> 2] >> (2 * (e & 3))) & 0x3;  // stored crumb = q + 2
+        } else {
+          v = uint32_t(uint8_t(a.src_q[e]) ^ 0x80u);     // S8 stores q; device stores q + 128
+        }
+      } else {
+        v = a.bits == 4 ? 8u : (a.bits == 2 ? 2u : 128u);  // q = 0 padding
+      }
+      out |= v << (a.bits * p);
+    }
+    a.dst_tiles[gid] = out;
+  }
+}
+
+__global__ void nad_repack_scales_kernel(RepackArgs a) {
+  const int total = a.ns * a.ng * 16;
+  const int ssz = a.scale_t == kScaleF32 ? 4 : 2;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int c = i & 15, g = (i >> 4) % a.ng, s = (i >> 4) / a.ng;
+    const int n = s * 16 + c;
+    const bool ok = n < a.n;
+    const uint64_t src = uint64_t(g) * a.cstep + n;
+    if (ssz == 4) {
+      static_cast<float*>(a.dst_scales)[i] = ok ? reinterpret_cast<const float*>(a.src_s)[src] : 0.f;
+    } else {
+      static_cast<uint16_t*>(a.dst_scales)[i] = ok ? reinterpret_cast<const uint16_t*>(a.src_s)[src] : 0;
+    }
+    if (a.dst_zps) a.dst_zps[i] = ok ? a.src_z[src] : 0;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------ skinny (M<=16)
+// LDS: scales (float) [NWI][ng][16] and zp constants (half2 bits) [NWI][ng][16], then reduction scratch.
+template <int BITS, int AT, int HILO, int CH>
+__global__ __launch_bounds__(1024) void woq_skinny_kernel(SkinnyArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int KT = BITS == 4 ? 128 : (BITS == 2 ? 256 : 64);
+  constexpr int SPT = KT / 32;
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int nwaves = blockDim.x >> 6;
+  const bool dual = a.epi == kEpiSiluMul || a.epi == kEpiGeluMul;
+
+  // which weight and stripe does this workgroup own
+  int wsel = 0;
+  int sid = blockIdx.x;
+  if (!dual) {
+#pragma unroll
+    for (int i = 1; i < 3; i++)
+      if (i < a.nw && sid >= a.stripe_base[i]) wsel = i;
+    sid -= a.stripe_base[wsel];
+  }
+  const int nwi = dual ? 2 : 1;           // weights handled by this WG
+  const int KS = nwaves / nwi;            // K slices per weight
+  const int my_w = dual ? (wave / KS) : wsel;
+  const int ks = wave % KS;
+  const SkinnyWeight& W = a.w[my_w];
+  const int s = sid;
+  const int nt = W.nt, ng = W.ng, bs = W.bs;
+
+  float* lds_scale = reinterpret_cast<float*>(smem);
+  uint32_t* lds_zc = reinterpret_cast<uint32_t*>(smem + size_t(nwi) * ng * 16 * 4);
+
+  // 1) issue this wave's first B chunk early (before the scale preload barrier)
+  const int tpw = a.tiles_per_wave;
+  const int tw0 = ks * tpw;
+  const int tw1 = min(nt, tw0 + tpw);
+  const u4_t* tile_base = reinterpret_cast<const u4_t*>(W.tiles) + size_t(s) * nt * 64 + lane;
+  u4_t b[CH];
+#pragma unroll
+  for (int i = 0; i < CH; i++) {
+    int t = min(tw0 + i, nt - 1);
+    b[i] = __builtin_nontemporal_load(tile_base + size_t(t) * 64);
+  }
+
+  // 2) cooperative preload of the group scales (and zp constants) of this WG's stripe(s) into LDS
+  for (int wi = 0; wi < nwi; wi++) {
+    const SkinnyWeight& Wl = a.w[dual ? wi : wsel];
+    const int cnt = ng * 16;
+    const size_t soff = size_t(s) * ng * 16;
+    for (int i = threadIdx.x; i < cnt; i += blockDim.x) {
+      lds_scale[wi * cnt + i] = load_scale(Wl.scales, soff + i, a.scale_t);
+      int zp = Wl.zps ? int(Wl.zps[soff + i]) : 0;
+      h2_t c = zp_const(bias_of<BITS>() + zp);
+      lds_zc[wi * cnt + i] = __builtin_bit_cast(uint32_t, c);
+    }
+  }
+  __syncthreads();
+
+  const int m = lane & 15;      // A-operand row this lane feeds
+  const int kq = lane >> 4;     // k-quarter of the 32-k step
+  const int M = a.M;
+  // HILO==1: rows 0..7 carry hi(A[m]), rows 8..15 carry lo(A[m-8]); HILO==2: two passes; HILO==0: fp16 A as is.
+  int arow;
+  bool aact;
+  bool is_lo = false;
+  if (HILO == 1) {
+    arow = m & 7;
+    is_lo = m >= 8;
+    aact = arow < M;
+  } else {
+    arow = m;
+    aact = m < M;
+  }
+  const bool vec_ok = a.vec_ok != 0;
+  const int32_t* shf = W.shuffle;
+  const float* sc_l = lds_scale + (dual ? my_w : 0) * ng * 16 + (lane & 15);
+  const uint32_t* zc_l = lds_zc + (dual ? my_w : 0) * ng * 16 + (lane & 15);
+
+  f4_t acc = {0.f, 0.f, 0.f, 0.f};
+  f4_t accg = {0.f, 0.f, 0.f, 0.f};
+  const int last_step = tw1 * SPT - 1;
+
+  for (int c0 = tw0; c0 < tw1; c0 += CH) {
+    if (c0 != tw0) {
+#pragma unroll
+      for (int i = 0; i < CH; i++) {
+        int t = min(c0 + i, nt - 1);
+        b[i] = __builtin_nontemporal_load(tile_base + size_t(t) * 64);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < CH; i++) {
+      const int t = c0 + i;
+      if (t < tw1) {
+#pragma unroll
+        for (int d = 0; d < SPT; d++) {
+          const int st = t * SPT + d;
+          const int k0 = st * 32 + kq * 8;
+          const int g = min((st * 32) / bs, ng - 1);
+          const h2_t c2 = as_h2(zc_l[g * 16]);
+          const h8_t bf = dequant_step<BITS>(b[i], d, c2);
+          float av[8];
+          if (aact) {
+            load_a8<AT>(a.A, a.lda, arow, k0, a.K, shf, vec_ok, av);
+          } else {
+#pragma unroll
+            for (int j = 0; j < 8; j++) av[j] = 0.f;
+          }
+          h8_t ah, al;
+#pragma unroll
+          for (int j = 0; j < 8; j++) {
+            _Float16 h = _Float16(av[j]);
+            ah[j] = h;
+            if (HILO != 0) al[j] = _Float16(av[j] - float(h));
+          }
+          if (HILO == 1) {
+            h8_t af = is_lo ? al : ah;
+            accg = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, bf, accg, 0, 0, 0);
+          } else if (HILO == 2) {
+            accg = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bf, accg, 0, 0, 0);
+            accg = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bf, accg, 0, 0, 0);
+          } else {
+            accg = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bf, accg, 0, 0, 0);
+          }
+          const bool gend = (((st + 1) * 32) % bs == 0) || st == last_step;
+          if (gend) {
+            const float sc = sc_l[g * 16];
+            acc += accg * sc;
+            accg = f4_t{0.f, 0.f, 0.f, 0.f};
+          }
+        }
+      }
+    }
+  }
+
+  // 3) rows: HILO==1 folds lo rows (8..15, lanes 32..63) onto hi rows (0..7, lanes 0..31)
+  if (HILO == 1) {
+#pragma unroll
+    for (int i = 0; i < 4; i++) acc[i] += __shfl_down(acc[i], 32, 64);
+  }
+  // 4) reduce the KS slices through LDS (reuse the scale region after a barrier)
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(smem);
+  *reinterpret_cast<f4_t*>(red + (size_t(wave) * 64 + lane) * 4) = acc;
+  __syncthreads();
+  // each (weight-in-wg, m, nn) output is produced by one thread
+  const int outs = 16 * 16;
+  for (int o = threadIdx.x; o < outs * (dual ? 1 : 1); o += blockDim.x) {
+    const int mm = o >> 4, nn = o & 15;
+    if (mm >= M) continue;
+    const int src_lane = (mm >> 2) * 16 + nn, reg = mm & 3;
+    float y0 = 0.f, y1 = 0.f;
+    for (int w = 0; w < KS; w++) y0 += red[(size_t(w) * 64 + src_lane) * 4 + reg];
+    if (dual)
+      for (int w = 0; w < KS; w++) y1 += red[(size_t(KS + w) * 64 + src_lane) * 4 + reg];
+    const SkinnyWeight& Wo = a.w[dual ? 0 : wsel];
+    const int n = s * 16 + nn;
+    if (n >= Wo.n) continue;
+    float v = y0;
+    switch (a.epi) {
+      case kEpiBias:
+        v += Wo.bias[size_t(mm) * Wo.bias_ld + n];
+        break;
+      case kEpiAddGelu:
+        v = gelu_f(v + Wo.bias[size_t(mm) * Wo.bias_ld + n]);
+        break;
+      case kEpiGelu:
+        v = gelu_f(v);
+        break;
+      case kEpiSilu:
+        v = silu_f(v);
+        break;
+      case kEpiResAdd:
+        v += a.res[size_t(mm) * a.ld_res + n];
+        break;
+      case kEpiSiluMul: {
+        float t1 = silu_f(y0);
+        if (a.aux) a.aux[size_t(mm) * a.ld_aux + n] = t1;
+        v = t1 * y1;
+        break;
+      }
+      case kEpiGeluMul: {
+        float t1 = gelu_f(y0);
+        if (a.aux) a.aux[size_t(mm) * a.ld_aux + n] = t1;
+        v = t1 * y1;
+        break;
+      }
+      default:
+        break;
+    }
+    Wo.out[size_t(mm) * Wo.ldo + n] = v;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------ GEMM (M>16)
+// Block 256 threads = 4 waves (2 x 2); block tile BM x BN = 128 x 128 (8 stripes); K step = one tile (KT).
+// LDS A tile: [128 rows][KT fp16] with 16-B chunk XOR swizzle (chunk ^= row & 15).
+template <int BITS, int AT>
+__global__ __launch_bounds__(256, 1) void woq_gemm_kernel(GemmArgs a) {
+  constexpr int KT = BITS == 4 ? 128 : (BITS == 2 ? 256 : 64);
+  constexpr int SPT = KT / 32;
+  constexpr int BM = 128, BN = 128;
+  constexpr int ROWB = KT * 2;            // bytes per LDS row (fp16)
+  constexpr int CHUNKS = ROWB / 16;       // 16-B chunks per row
+  __shared__ __attribute__((aligned(16))) char lds_a[BM * ROWB];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const SkinnyWeight& W = a.w;
+
+  // XCD-aware remap: consecutive workgroups (same N tile, different M tiles) land on one XCD's L2
+  const int nbm = (a.M + BM - 1) / BM;
+  const int nbn = (W.ns + 7) / 8;
+  const int nwg = nbm * nbn;
+  int bid = blockIdx.x;
+  {
+    const int q = nwg / 8, r = nwg % 8, x = bid % 8, o = bid / 8;
+    bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + o;
+  }
+  const int bn = bid / nbm, bm = bid % nbm;
+  const int m0 = bm * BM;
+  const int s0 = bn * 8 + wn * 4;         // first stripe of this wave
+  const int nt = W.nt, bs = W.bs;
+
+  f4_t acc[4][4], accg[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; i++)
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      acc[i][j] = f4_t{0.f, 0.f, 0.f, 0.f};
+      accg[i][j] = f4_t{0.f, 0.f, 0.f, 0.f};
+    }
+
+  // A staging map: 256 threads cover BM rows x KT k; each thread handles rows r0 + 32*i, chunk ch (8 k values)
+  constexpr int TPR = CHUNKS;              // threads per row chunk group
+  constexpr int ROWS_PER_PASS = 256 / TPR;
+  constexpr int PASSES = BM / ROWS_PER_PASS;
+  const int ch = threadIdx.x % TPR;
+  const int r0 = threadIdx.x / TPR;
+  const bool vec_ok = a.vec_ok != 0;
+  const int32_t* shf = W.shuffle;
+
+  const u4_t* tiles = reinterpret_cast<const u4_t*>(W.tiles);
+  u4_t bcur[4], bnext[4];
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    int s = min(s0 + j, W.ns - 1);
+    bcur[j] = tiles[(size_t(s) * nt + 0) * 64 + lane];
+  }
+
+  for (int t = 0; t < nt; t++) {
+    // stage A(t) into LDS (fp32/bf16/fp16 -> fp16)
+#pragma unroll
+    for (int p = 0; p < PASSES; p++) {
+      const int r = r0 + p * ROWS_PER_PASS;
+      const int row = m0 + r;
+      float v[8];
+      if (row < a.M) {
+        load_a8<AT>(a.A, a.lda, row, t * KT + ch * 8, a.K, shf, vec_ok, v);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; j++) v[j] = 0.f;
+      }
+      h8_t hv;
+#pragma unroll
+      for (int j = 0; j < 8; j++) hv[j] = _Float16(v[j]);
+      const int sw = ch ^ (r & 15 & (CHUNKS - 1));
+      *reinterpret_cast<h8_t*>(lds_a + r * ROWB + sw * 16) = hv;
+    }
+    // prefetch next B tiles
+    if (t + 1 < nt) {
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        int s = min(s0 + j, W.ns - 1);
+        bnext[j] = tiles[(size_t(s) * nt + t + 1) * 64 + lane];
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int d = 0; d < SPT; d++) {
+      const int st = t * SPT + d;
+      const int g = min((st * 32) / bs, W.ng - 1);
+      h8_t bf[4];
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const int s = min(s0 + j, W.ns - 1);
+        const size_t zi = (size_t(s) * W.ng + g) * 16 + (lane & 15);
+        const int zp = W.zps ? int(W.zps[zi]) : 0;
+        bf[j] = dequant_step<BITS>(bcur[j], d, zp_const(bias_of<BITS>() + zp));
+      }
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        const int r = wm * 64 + i * 16 + (lane & 15);
+        const int chunk = d * 4 + (lane >> 4);
+        const int sw = chunk ^ (r & 15 & (CHUNKS - 1));
+        const h8_t af = *reinterpret_cast<const h8_t*>(lds_a + r * ROWB + sw * 16);
+#pragma unroll
+        for (int j = 0; j < 4; j++) accg[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, bf[j], accg[i][j], 0, 0, 0);
+      }
+      const bool gend = (((st + 1) * 32) % bs == 0) || (st == nt * SPT - 1);
+      if (gend) {
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          const int s = min(s0 + j, W.ns - 1);
+          const float sc = load_scale(W.scales, (size_t(s) * W.ng + g) * 16 + (lane & 15), a.scale_t);
+#pragma unroll
+          for (int i = 0; i < 4; i++) {
+            acc[i][j] += accg[i][j] * sc;
+            accg[i][j] = f4_t{0.f, 0.f, 0.f, 0.f};
+          }
+        }
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 4; j++) bcur[j] = bnext[j];
+  }
+
+  // epilogue: C layout col = lane & 15, row = (lane >> 4) * 4 + reg
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    const int n = (s0 + j) * 16 + (lane & 15);
+    if (s0 + j >= W.ns || n >= W.n) continue;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+#pragma unroll
+      for (int rr = 0; rr < 4; rr++) {
+        const int row = m0 + wm * 64 + i * 16 + (lane >> 4) * 4 + rr;
+        if (row >= a.M) continue;
+        float v = acc[i][j][rr];
+        switch (a.epi) {
+          case kEpiBias:
+            v += W.bias[size_t(row) * W.bias_ld + n];
+            break;
+          case kEpiAddGelu:
+            v = gelu_f(v + W.bias[size_t(row) * W.bias_ld + n]);
+            break;
+          case kEpiGelu:
+            v = gelu_f(v);
+            break;
+          case kEpiSilu:
+            v = silu_f(v);
+            break;
+          case kEpiResAdd:
+            v += a.res[size_t(row) * a.ld_res + n];
+            break;
+          case kEpiSiluMul:  // second pass of the FFN: out = silu(tmp1) * (x.w3), aux holds silu(x.w1)
+            v = a.aux[size_t(row) * a.ld_aux + n] * v;
+            break;
+          default:
+            break;
+        }
+        W.out[size_t(row) * W.ldo + n] = v;
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------ launchers
+hipError_t launch_repack(const RepackArgs& a, hipStream_t stream) {
+  const uint64_t total = uint64_t(a.ns) * a.nt * 256;
+  int blocks = int(std::min<uint64_t>((total + 255) / 256, 65535));
+  hipLaunchKernelGGL(nad_repack_kernel, dim3(blocks), dim3(256), 0, stream, a);
+  int total_s = a.ns * a.ng * 16;
+  int bs2 = std::min((total_s + 255) / 256, 65535);
+  hipLaunchKernelGGL(nad_repack_scales_kernel, dim3(bs2), dim3(256), 0, stream, a);
+  return hipGetLastError();
+}
+
+template <int BITS, int AT, int HILO>
+static hipError_t skinny_dispatch_ch(const SkinnyArgs& a, int ch, dim3 grid, dim3 block, size_t lds,
+                                     hipStream_t stream) {
+  if (ch == 4)
+    hipLaunchKernelGGL((woq_skinny_kernel<BITS, AT, HILO, 4>), grid, block, lds, stream, a);
+  else
+    hipLaunchKernelGGL((woq_skinny_kernel<BITS, AT, HILO, 8>), grid, block, lds, stream, a);
+  return hipGetLastError();
+}
+
+template <int BITS>
+static hipError_t skinny_dispatch_bits(const SkinnyArgs& a, int at, int hilo, int ch, dim3 g, dim3 b, size_t lds,
+                                       hipStream_t st) {
+  if (at == kActF16) return skinny_dispatch_ch<BITS, kActF16, 0>(a, ch, g, b, lds, st);
+  if (at == kActF32) {
+    if (hilo == 1) return skinny_dispatch_ch<BITS, kActF32, 1>(a, ch, g, b, lds, st);
+    return skinny_dispatch_ch<BITS, kActF32, 2>(a, ch, g, b, lds, st);
+  }
+  if (hilo == 1) return skinny_dispatch_ch<BITS, kActBF16, 1>(a, ch, g, b, lds, st);
+  return skinny_dispatch_ch<BITS, kActBF16, 2>(a, ch, g, b, lds, st);
+}
+
+hipError_t launch_skinny(const SkinnyArgs& a, int bits, int act_t, int waves_per_wg, int stripes, int ch,
+                         hipStream_t stream) {
+  const bool dual = a.epi == kEpiSiluMul || a.epi == kEpiGeluMul;
+  const int nwi = dual ? 2 : 1;
+  int ngmax = 0;
+  for (int i = 0; i < a.nw; i++) ngmax = std::max(ngmax, a.w[i].ng);
+  size_t lds = std::max(size_t(nwi) * ngmax * 16 * 8, size_t(waves_per_wg) * 64 * 16);
+  const int hilo = act_t == kActF16 ? 0 : (a.M <= 8 ? 1 : 2);
+  dim3 grid(stripes), block(waves_per_wg * 64);
+  if (bits == 4) return skinny_dispatch_bits<4>(a, act_t, hilo, ch, grid, block, lds, stream);
+  if (bits == 2) return skinny_dispatch_bits<2>(a, act_t, hilo, ch, grid, block, lds, stream);
+  return skinny_dispatch_bits<8>(a, act_t, hilo, ch, grid, block, lds, stream);
+}
+
+template <int BITS>
+static hipError_t gemm_dispatch_bits(const GemmArgs& a, int at, dim3 g, hipStream_t st) {
+  if (at == kActF32)
+    hipLaunchKernelGGL((woq_gemm_kernel<BITS, kActF32>), g, dim3(256), 0, st, a);
+  else if (at == kActF16)
+    hipLaunchKernelGGL((woq_gemm_kernel<BITS, kActF16>), g, dim3(256), 0, st, a);
+  else
+    hipLaunchKernelGGL((woq_gemm_kernel<BITS, kActBF16>), g, dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_gemm(const GemmArgs& a, int bits, int act_t, hipStream_t stream) {
+  const int nbm = (a.M + 127) / 128, nbn = (a.w.ns + 7) / 8;
+  dim3 grid(nbm * nbn);
+  if (bits == 4) return gemm_dispatch_bits<4>(a, act_t, grid, stream);
+  if (bits == 2) return gemm_dispatch_bits<2>(a, act_t, grid, stream);
+  return gemm_dispatch_bits<8>(a, act_t, grid, stream);
+}
+
+}  // namespace nad

@@ -1,0 +1,107 @@
+// woq_layout.h -- the MI355X-native device layout of a weight-only-quantized matrix, and the descriptor that
+// bestla_device_load_storage writes into the caller's `devstor` (ne_tensor's embedded device storage,
+// neural_speed/core/ne_layers.c:946-949,1022-1024).
+//
+// Layout (one "stripe" = 16 output features n, one "tile" = 1 KiB of packed weights):
+//   tiles  : [ns][nt][64 lanes][16 B]      ns = ceil(N/16), nt = ceil(K/KT), KT = 128 (int4) / 256 (int2) / 64 (int8)
+//            Lane l of a tile owns column n = 16*s + (l & 15) and k-quarter kq = l >> 4.  Its 16 bytes are the
+//            B fragments of KT/32 consecutive v_mfma_f32_16x16x32_f16 steps: step d covers k = t*KT + 32*d + 8*kq + j,
+//            j = 0..7, i.e. exactly the B-operand lane map of 16x16x32 (lane l: B[k = 8(l>>4)+j][n = l&15]).
+//            A wave therefore streams a tile with one fully coalesced global_load_dwordx4 and feeds MFMA directly.
+//   values : stored biased/unsigned: int4 q+8, int2 q+2, int8 q+128.  Inside a dword the element order is chosen so
+//            that ((w >> s) & mask) | 0x6400 yields fp16 pairs (1024 + v_j, 1024 + v_j+1) with no shuffles:
+//              int4 dword (one step):   nibble position p holds element j = 2p (p<4) / 2(p-4)+1 (p>=4)
+//              int2 dword (two steps):  crumb position p (0..15): step h = (p&7)>>2, j = 2*(p&3) + (p>>3)
+//              int8 dword pair (step):  byte b of dword w holds element j = 4w + b (v_perm places it)
+//   scales : [ns][ngroups][16] in the blob's scale dtype (f32 / bf16 / f16)
+//   zps    : [ns][ngroups][16] int8 (asym only)
+//   shuffle: [K] int32 act-order LUT (GPTQ desc_act), applied as a gather on the A operand
+#pragma once
+#include <cstdint>
+
+#if defined(__HIPCC__)
+#define NAD_HD __host__ __device__
+#else
+#define NAD_HD
+#endif
+
+namespace nad {
+
+constexpr uint32_t kWeightMagic = 0x5744414eu;  // "NADW"
+
+enum ScaleType : int32_t { kScaleF32 = 0, kScaleBF16 = 1, kScaleF16 = 2 };
+
+struct DeviceWeight {
+  uint32_t magic;
+  int32_t bits;       // 2, 4, 8
+  int32_t n, k;       // logical shape: out features, in features
+  int32_t blocksize;  // quantization group along K
+  int32_t ns, nt, ng; // stripes, tiles along K, groups along K
+  int32_t scale_t;    // ScaleType
+  int32_t asym;
+  int32_t has_shuffle;
+  int32_t pad0;
+  uint64_t bytes;     // device bytes used from the caller's buffer
+  uint64_t src_core_id;
+  void* tiles;
+  void* scales;
+  int8_t* zps;
+  int32_t* shuffle;
+  void* owner;        // non-null when the library allocated the device memory itself (nad_* helpers)
+};
+
+NAD_HD inline int tile_k(int bits) { return bits == 4 ? 128 : (bits == 2 ? 256 : 64); }
+NAD_HD inline int steps_per_tile(int bits) { return tile_k(bits) / 32; }
+
+inline uint64_t align256(uint64_t x) { return (x + 255) & ~uint64_t(255); }
+
+// fill the geometry of a DeviceWeight and return the device bytes it needs
+inline uint64_t layout_geometry(DeviceWeight& w, int bits, int n, int k, int blocksize, int scale_t, bool asym,
+                                bool shuffle) {
+  w.magic = kWeightMagic;
+  w.bits = bits;
+  w.n = n;
+  w.k = k;
+  w.blocksize = blocksize;
+  w.ns = (n + 15) / 16;
+  w.nt = (k + tile_k(bits) - 1) / tile_k(bits);
+  w.ng = (k + blocksize - 1) / blocksize;
+  w.scale_t = scale_t;
+  w.asym = asym ? 1 : 0;
+  w.has_shuffle = shuffle ? 1 : 0;
+  uint64_t tiles = uint64_t(w.ns) * w.nt * 1024;
+  uint64_t sbytes = uint64_t(w.ns) * w.ng * 16 * (scale_t == kScaleF32 ? 4 : 2);
+  uint64_t zbytes = asym ? uint64_t(w.ns) * w.ng * 16 : 0;
+  uint64_t shf = shuffle ? uint64_t(k) * 4 : 0;
+  return align256(tiles) + align256(sbytes) + align256(zbytes) + align256(shf);
+}
+
+inline void layout_assign(DeviceWeight& w, void* base) {
+  char* p = static_cast<char*>(base);
+  uint64_t tiles = uint64_t(w.ns) * w.nt * 1024;
+  uint64_t sbytes = uint64_t(w.ns) * w.ng * 16 * (w.scale_t == kScaleF32 ? 4 : 2);
+  uint64_t zbytes = w.asym ? uint64_t(w.ns) * w.ng * 16 : 0;
+  w.tiles = p;
+  p += align256(tiles);
+  w.scales = p;
+  p += align256(sbytes);
+  w.zps = w.asym ? reinterpret_cast<int8_t*>(p) : nullptr;
+  p += align256(zbytes);
+  w.shuffle = w.has_shuffle ? reinterpret_cast<int32_t*>(p) : nullptr;
+  p += w.has_shuffle ? align256(uint64_t(w.k) * 4) : 0;
+  w.bytes = uint64_t(p - static_cast<char*>(base));
+}
+
+// epilogues (bestla_epilogue.h:114-166; neural_speed/core/layers/bestla_common.hpp:121-216)
+enum Epilogue : int32_t {
+  kEpiNone = 0,     // AccumulatorWriteBack
+  kEpiBias = 1,     // ip_add: + bias[n] (broadcast) or + bias[m][n]
+  kEpiSiluMul = 2,  // FFN: silu(W0.a) * (W1.a)       (ip_fusion_ffn.cpp:407-433)
+  kEpiGeluMul = 3,  // FFN: gelu(W0.a) * (W1.a)
+  kEpiGelu = 4,     // gelu(W0.a)
+  kEpiAddGelu = 5,  // gelu(W0.a + bias)
+  kEpiSilu = 6,     // swish
+  kEpiResAdd = 7,   // + residual[m][n]
+};
+
+}  // namespace nad

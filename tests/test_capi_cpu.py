@@ -1,0 +1,132 @@
+"""C-ABI tests that need no GPU: the library loads, exports every symbol of include/neural_amd.h, and its host
+pack/unpack/split paths are bit-exact against the oracle (which is pinned to the reference's own goldens)."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from neural_amd import _lib, bestla
+from tests.oracle_lib import F32, BF16, F16, S4, S2, S8
+
+
+def test_library_exports_every_header_symbol():
+    L = _lib.lib()
+    names = _lib.header_symbols()
+    assert len(names) >= 50
+    missing = [n for n in names if not hasattr(L, n)]
+    assert not missing, missing
+    # and the Python signature table covers all of them
+    assert set(names) <= set(_lib.SIGNATURES), set(names) - set(_lib.SIGNATURES)
+
+
+def test_storage_descriptor_size():
+    assert _lib.lib().bestla_device_storage_size() >= 96
+
+
+CFGS = [
+    # n, k, bs, qtype, stype, asym, comp
+    (96, 256, 32, S4, F32, False, bestla.COMP_F32),
+    (100, 300, 32, S4, BF16, True, bestla.COMP_F32),
+    (77, 256, 128, S4, F16, False, bestla.COMP_INT8),   # amx_int8 kblock, PACK_ROW 4, reduce buffer
+    (48, 512, 32, S4, F32, True, bestla.COMP_INT8),     # avx512_vnni kblock (32 % 64 != 0)
+    (64, 256, 64, S2, F32, False, bestla.COMP_F32),
+    (50, 256, 64, S2, BF16, True, bestla.COMP_INT8),
+    (40, 128, 32, S8, F32, False, bestla.COMP_F32),
+    (40, 128, 128, S8, F32, False, bestla.COMP_INT8),
+    (96, 256, 32, S4, F32, False, bestla.COMP_BF16),    # amx_bf16: PACK_ROW 2, KTILE 32
+    (33, 160, 32, S4, F32, False, bestla.COMP_F32),     # ragged N
+]
+
+
+@pytest.mark.parametrize("cfg", CFGS)
+def test_quant_pack_bit_exact_vs_oracle(oracle, cfg):
+    n, k, bs, qt, st, asym, comp = cfg
+    rng = np.random.default_rng(n * 1000 + k)
+    W = rng.uniform(-0.5, 0.5, size=(n, k)).astype(np.float32)
+    W[0, :bs] = 0.0  # an all-zero block
+    blob = bestla.quantize(W, group_size=bs, weight_dtype={S4: "int4", S2: "int2", S8: "int8"}[qt],
+                           scale_dtype={F32: "fp32", BF16: "bf16", F16: "fp16"}[st],
+                           alg="asym" if asym else "sym",
+                           compute_dtype={bestla.COMP_F32: "fp32", bestla.COMP_INT8: "int8", bestla.COMP_BF16: "bf16"}[comp])
+    core = oracle.lib.orc_select_core(comp, qt, bs, int(asym), 0)
+    ref = oracle.quant_pack(W, n, k, bs, qt, st, asym, core, is_trans=True)
+    assert blob.size == ref.size
+    np.testing.assert_array_equal(blob, ref)
+    # unpack matches the oracle's dequantization exactly
+    np.testing.assert_array_equal(bestla.unpack(blob).view(np.uint32), oracle.unpack_fp32(ref).view(np.uint32))
+
+
+def test_qpack_gptq_with_g_idx_bit_exact(oracle):
+    rng = np.random.default_rng(7)
+    k, n, gs = 256, 64, 32
+    q = rng.integers(-8, 8, size=(k, n)).astype(np.int8)
+    s = rng.uniform(0.001, 0.005, size=(k // gs, n)).astype(np.float32)
+    z = rng.integers(-8, 8, size=(k // gs, n)).astype(np.int8)
+    g_idx = rng.permutation(np.arange(k) // gs).astype(np.int32)
+    blob = bestla.qpack(q, s, z, g_idx, "int4", gs, "asym", "fp32", "int8")
+    core = oracle.lib.orc_select_core(bestla.COMP_INT8, S4, gs, 1, 0)
+    ref = oracle.pack_q(q, s, z, n, k, gs, S4, F32, True, core, g_idx)
+    np.testing.assert_array_equal(blob, ref)
+    Q, S, Z, shf = oracle.unpack_q(blob)
+    np.testing.assert_array_equal(Q, q)
+    expect = np.zeros(k, np.int32)
+    oracle.lib.orc_shuffle_indices(g_idx.ctypes.data, k, gs, expect.ctypes.data)
+    np.testing.assert_array_equal(shf, expect)
+
+
+def test_blob_info_matches_oracle(oracle):
+    rng = np.random.default_rng(3)
+    W = rng.uniform(-0.5, 0.5, size=(80, 256)).astype(np.float32)
+    blob = bestla.quantize(W, 64, "int4", "bf16", "asym", "int8")
+    assert bestla.blob_info(blob) == oracle.info(blob)
+
+
+@pytest.mark.parametrize("axis,world", [(0, 2), (0, 4), (1, 2), (1, 8)])
+def test_tp_split_is_exact(oracle, axis, world):
+    rng = np.random.default_rng(11)
+    n, k, bs = 96, 86 * 32, 32  # 86 groups: uneven K split (11,11,11,11,11,11,10,10) at world 8
+    W = rng.uniform(-0.5, 0.5, size=(n, k)).astype(np.float32)
+    blob = bestla.quantize(W, bs, "int4", "bf16", "asym", "int8")
+    full = bestla.unpack(blob)
+    Qf, Sf, Zf, _ = oracle.unpack_q(blob)
+    covered = 0
+    for r in range(world):
+        lo, hi = bestla.split_range(blob, axis, r, world)
+        shard = bestla.split(blob, axis, r, world)
+        part = bestla.unpack(shard)
+        if axis == 0:
+            np.testing.assert_array_equal(part, full[:, lo:hi])
+        else:
+            assert lo % bs == 0
+            np.testing.assert_array_equal(part, full[lo:hi, :])
+            # the shard's reduce buffer (int8 compute) equals the slice of the full one
+            Qs, Ss, Zs, _ = oracle.unpack_q(shard)
+            np.testing.assert_array_equal(Qs, Qf[lo:hi])
+            np.testing.assert_array_equal(Ss, Sf[lo // bs:hi // bs])
+        covered += hi - lo
+    assert covered == (n if axis == 0 else k)
+
+
+def test_packweight_copyattr_and_unpack_abi(oracle):
+    L = _lib.lib()
+    rng = np.random.default_rng(5)
+    n, k = 64, 256
+    W = rng.uniform(-0.5, 0.5, size=(n, k)).astype(np.float32)
+    src = bestla.quantize(W, 32, "int4", "fp32", "sym", "fp32")
+    dst = bestla._aligned_buffer(src.size)
+    W2 = rng.uniform(-0.5, 0.5, size=(n, k)).astype(np.float32)
+    L.bestla_packweight_copyattr(W2.ctypes.data_as(C.c_void_p), dst.ctypes.data_as(C.c_void_p), n, k, k,
+                                 src.ctypes.data_as(C.c_void_p))
+    np.testing.assert_array_equal(dst, bestla.quantize(W2, 32, "int4", "fp32", "sym", "fp32"))
+    out = np.zeros((k, n), np.float32)
+    L.bestla_unpackweight_fp32(dst.ctypes.data_as(C.c_void_p), n, k, out.ctypes.data_as(C.c_void_p), n)
+    np.testing.assert_array_equal(out, oracle.unpack_fp32(dst))
+
+
+def test_unsupported_inputs_fail_loudly():
+    L = _lib.lib()
+    bad = np.zeros(256, np.uint8)
+    assert L.nad_device_weight_size(bad.ctypes.data_as(C.c_void_p)) == 0
+    assert "WeightKBlockNInteger" in _lib.last_error() or "corrupt" in _lib.last_error()
+    with pytest.raises(ValueError):
+        bestla.quantize(np.zeros((16, 64), np.float32), 32, "nf4")
