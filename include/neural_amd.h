@@ -142,11 +142,13 @@ int nad_device_qkv_forward(const void* act, int act_dtype, const void* wq, const
 int nad_device_ffn_forward(const void* act, int act_dtype, const void* w1, const void* w2, const void* w3, float* tmp1,
                            float* tmp2, float* out, int m, int fin, int fmid, int fout, int lda, int epi, void* queue);
 /* tensor-parallel slicing of a packed blob without re-quantization (the reference re-quantizes,
- * model_files.h:1538-1563).  axis 0: split N (TP_1D_ROW, column-parallel); axis 1: split K by whole groups
- * (TP_1D_COLUMN, row-parallel).  Returns the shard's blob size (dst may be NULL to query). */
-size_t nad_blob_split(const void* src, int axis, int rank, int world, void* dst, size_t dst_capacity);
+ * model_files.h:1538-1563).  axis 0: split N (TP_1D_ROW, column-parallel) into near-equal chunks of `unit` columns
+ * (use the consumer's K group / head size so column shards line up with the next row-parallel weight's K shards);
+ * axis 1: split K by whole quantization groups (TP_1D_COLUMN, row-parallel; `unit` ignored).
+ * Returns the shard's blob size (dst may be NULL to query). */
+size_t nad_blob_split(const void* src, int axis, int rank, int world, int unit, void* dst, size_t dst_capacity);
 /* the [begin, end) range of N (axis 0) or K (axis 1) that `rank` owns */
-int nad_split_range(const void* src, int axis, int rank, int world, int* begin, int* end);
+int nad_split_range(const void* src, int axis, int rank, int world, int unit, int* begin, int* end);
 /* synthetic device weight of the given geometry (random packed values, scales U[smin,smax], zps) for benchmarks */
 int nad_synthetic_weight(void* devstor, void* deviceptr, size_t capacity, int bits, int n, int k, int blocksize,
                          int scale_t, int asym, uint64_t seed, void* queue);

@@ -126,21 +126,22 @@ def unpack(blob):
     return out
 
 
-def split(blob, axis, rank, world):
-    """Exact TP shard of a blob: axis 0 splits N (TP_1D_ROW), axis 1 splits K by whole groups (TP_1D_COLUMN)."""
+def split(blob, axis, rank, world, unit=1):
+    """Exact TP shard of a blob: axis 0 splits N (TP_1D_ROW) in chunks of `unit` columns, axis 1 splits K by whole
+    quantization groups (TP_1D_COLUMN)."""
     L = lib()
-    size = L.nad_blob_split(_ptr(blob), axis, rank, world, None, 0)
+    size = L.nad_blob_split(_ptr(blob), axis, rank, world, unit, None, 0)
     if not size:
         raise RuntimeError(f"nad_blob_split failed: {last_error()}")
     out = _aligned_buffer(size)
-    if L.nad_blob_split(_ptr(blob), axis, rank, world, _ptr(out), size) != size:
+    if L.nad_blob_split(_ptr(blob), axis, rank, world, unit, _ptr(out), size) != size:
         raise RuntimeError(f"nad_blob_split failed: {last_error()}")
     return out
 
 
-def split_range(blob, axis, rank, world):
+def split_range(blob, axis, rank, world, unit=1):
     b, e = C.c_int(0), C.c_int(0)
-    check(lib().nad_split_range(_ptr(blob), axis, rank, world, C.byref(b), C.byref(e)), "nad_split_range")
+    check(lib().nad_split_range(_ptr(blob), axis, rank, world, unit, C.byref(b), C.byref(e)), "nad_split_range")
     return b.value, e.value
 
 

@@ -263,6 +263,7 @@ static bool vec_aligned(const void* A, int lda, int act_t) {
 static void skinny_geometry(int total_stripes, int nt, int nwi, int* ks, int* tpw, int* ch) {
   const int target_waves = 4096;
   int k = (target_waves + total_stripes - 1) / total_stripes;
+  k = std::max(k, (nt + 7) / 8);  // one chunk of <= 8 tiles per wave when possible
   k = std::max(1, std::min({k, 16 / nwi, nt}));
   int t = (nt + k - 1) / k;
   k = (nt + t - 1) / t;
@@ -299,6 +300,8 @@ static int run_skinny(const void* act, int act_t, int lda, int m, int k, int nw,
   int ks, tpw, ch;
   skinny_geometry(stripes, ws[0]->nt, dual ? 2 : 1, &ks, &tpw, &ch);
   a.tiles_per_wave = tpw;
+  a.steps_per_group = ws[0]->blocksize / 32;
+  a.a_fast = (a.vec_ok && ws[0]->shuffle == nullptr && k % (act_t == kActF32 ? 4 : 8) == 0) ? 1 : 0;
   hipError_t e = launch_skinny(a, ws[0]->bits, act_t, ks * (dual ? 2 : 1), stripes, ch, st);
   if (e != hipSuccess) {
     set_err("skinny kernel launch failed: %s", hipGetErrorString(e));
@@ -1037,7 +1040,7 @@ extern "C" void bestla_packweight_copyattr(const float* f32ptr, void* dstpr, int
 }
 
 // ------------------------------------------------------------------------------------------------ TP split
-extern "C" int nad_split_range(const void* src, int axis, int rank, int world, int* begin, int* end) {
+extern "C" int nad_split_range(const void* src, int axis, int rank, int world, int unit, int* begin, int* end) {
   Blob b;
   std::string err;
   if (!b.parse(src, &err)) {
@@ -1048,10 +1051,14 @@ extern "C" int nad_split_range(const void* src, int axis, int rank, int world, i
     set_err("bad rank/world");
     return -1;
   }
-  if (axis == 0) {  // N: contiguous near-equal chunks (the reference requires N % world == 0, model_files.h:193-235)
-    const int base = b.n / world, rem = b.n % world;
-    *begin = rank * base + std::min(rank, rem);
-    *end = *begin + base + (rank < rem ? 1 : 0);
+  if (axis == 0) {  // N: near-equal chunks of `unit` columns (the reference requires N % world == 0,
+                    // model_files.h:193-235, which unit = 1 reproduces)
+    const int u = std::max(1, unit);
+    const int units = (b.n + u - 1) / u;
+    const int base = units / world, rem = units % world;
+    const int u0 = rank * base + std::min(rank, rem), u1 = u0 + base + (rank < rem ? 1 : 0);
+    *begin = std::min(b.n, u0 * u);
+    *end = std::min(b.n, u1 * u);
   } else {  // K: whole quantization groups, near-equal (e.g. Llama down K=11008 = 86 g128 -> 11x6, 10x2)
     const int bs = b.blocksize >= b.k ? b.k : b.blocksize;
     const int groups = (b.k + bs - 1) / bs;
@@ -1067,7 +1074,8 @@ extern "C" int nad_split_range(const void* src, int axis, int rank, int world, i
   return 0;
 }
 
-extern "C" size_t nad_blob_split(const void* src, int axis, int rank, int world, void* dst, size_t dst_capacity) {
+extern "C" size_t nad_blob_split(const void* src, int axis, int rank, int world, int unit, void* dst,
+                                  size_t dst_capacity) {
   Blob b;
   std::string err;
   if (!b.parse(src, &err)) {
@@ -1079,7 +1087,7 @@ extern "C" size_t nad_blob_split(const void* src, int axis, int rank, int world,
     return 0;
   }
   int lo, hi;
-  if (nad_split_range(src, axis, rank, world, &lo, &hi)) return 0;
+  if (nad_split_range(src, axis, rank, world, unit, &lo, &hi)) return 0;
   const int n2 = axis == 0 ? hi - lo : b.n;
   const int k2 = axis == 1 ? hi - lo : b.k;
   const int bs = b.blocksize >= b.kpad ? -1 : b.blocksize;

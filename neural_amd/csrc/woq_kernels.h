@@ -43,9 +43,11 @@ struct SkinnyArgs {
   int nw;               // weights in this launch (1..3); for dual epilogues w[0], w[1] pair up
   int stripe_base[4];   // prefix sums of ns over the weights (non-dual)
   int tiles_per_wave;
+  int steps_per_group;  // blocksize / 32
   int scale_t;
   int epi;
   int vec_ok;           // A rows 16-B aligned (vector loads allowed)
+  int a_fast;           // vec_ok && no act-order shuffle && K % (16 B / elem) == 0
   const float* res;
   int ld_res;
   float* aux;           // dual epilogue: optional silu/gelu(W0.a) output (tmp1 of the reference FFN)

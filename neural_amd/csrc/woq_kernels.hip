@@ -213,19 +213,65 @@ __global__ void nad_repack_scales_kernel(RepackArgs a) {
   }
 }
 
+
+// store one staged activation vector (VEC elements of row `row` at column k) as fp16 hi (+ lo) rows
+template <int AT, int VEC>
+__device__ __forceinline__ void stage_store(char* smem, uint4 x, int row, int k, int Kp, int M) {
+  if constexpr (AT == kActF16) {
+    *reinterpret_cast<uint4*>(smem + (size_t(row) * Kp + k) * 2) = x;
+  } else {
+    float f[VEC];
+    const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+    if constexpr (AT == kActF32) {
+#pragma unroll
+      for (int j = 0; j < 4; j++) f[j] = __uint_as_float(w[j]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        f[2 * j] = __uint_as_float(w[j] << 16);
+        f[2 * j + 1] = __uint_as_float(w[j] & 0xFFFF0000u);
+      }
+    }
+    _Float16 hi[VEC], lo[VEC];
+#pragma unroll
+    for (int j = 0; j < VEC; j++) {
+      hi[j] = _Float16(f[j]);
+      lo[j] = _Float16(f[j] - float(hi[j]));
+    }
+    char* ph = smem + (size_t(row) * Kp + k) * 2;
+    char* pl = smem + (size_t(M + row) * Kp + k) * 2;
+    if constexpr (VEC == 4) {
+      *reinterpret_cast<uint2*>(ph) = __builtin_bit_cast(uint2, hi);
+      *reinterpret_cast<uint2*>(pl) = __builtin_bit_cast(uint2, lo);
+    } else {
+      *reinterpret_cast<uint4*>(ph) = __builtin_bit_cast(uint4, hi);
+      *reinterpret_cast<uint4*>(pl) = __builtin_bit_cast(uint4, lo);
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------------------------ skinny (M<=16)
-// LDS: scales (float) [NWI][ng][16] and zp constants (half2 bits) [NWI][ng][16], then reduction scratch.
-template <int BITS, int AT, int HILO, int CH>
+// Dynamic LDS map:
+//   [0, a_bytes)          ALDS: the activations staged ONCE per workgroup as MFMA-ready fp16 rows [R][Kp]
+//                         (Kp = nt*KT, zero padded past K; the act-order gather of ShuffleActivationKBlock,
+//                         bestla_prologue_a.h:407-422, is applied while staging).  fp32/bf16 inputs are split into
+//                         hi = fp16(a) rows 0..M-1 and lo = fp16(a - hi) rows M..2M-1 (R = 2M), fp16 inputs are copied
+//                         (R = M); a 16-B zero block follows for lanes whose MFMA row is unused.  The main loop then
+//                         does one ds_read_b128 per step for A: no conversion, no global load on the critical path.
+//   [a_bytes, ...)        group scales as fp32, then zp constants (half2 bits), [nwi][ng][16] each
+//   reduction scratch     reuses offset 0 after the main loop
+template <int BITS, int AT, int HILO, int CH, bool ALDS>
 __global__ __launch_bounds__(1024) void woq_skinny_kernel(SkinnyArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int KT = BITS == 4 ? 128 : (BITS == 2 ? 256 : 64);
   constexpr int SPT = KT / 32;
+  constexpr int ESZ = AT == kActF32 ? 4 : 2;
   const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));
   const int nwaves = blockDim.x >> 6;
   const bool dual = a.epi == kEpiSiluMul || a.epi == kEpiGeluMul;
 
-  // which weight and stripe does this workgroup own
+  // which weight and stripe does this workgroup own (all wave-uniform)
   int wsel = 0;
   int sid = blockIdx.x;
   if (!dual) {
@@ -234,18 +280,21 @@ __global__ __launch_bounds__(1024) void woq_skinny_kernel(SkinnyArgs a) {
       if (i < a.nw && sid >= a.stripe_base[i]) wsel = i;
     sid -= a.stripe_base[wsel];
   }
-  const int nwi = dual ? 2 : 1;           // weights handled by this WG
-  const int KS = nwaves / nwi;            // K slices per weight
+  const int nwi = dual ? 2 : 1;
+  const int KS = nwaves / nwi;
   const int my_w = dual ? (wave / KS) : wsel;
   const int ks = wave % KS;
   const SkinnyWeight& W = a.w[my_w];
   const int s = sid;
-  const int nt = W.nt, ng = W.ng, bs = W.bs;
+  const int nt = W.nt, ng = W.ng;
+  const int Kp = nt * KT;
+  const int R = HILO == 0 ? a.M : 2 * a.M;        // staged fp16 rows
+  const int zero_off = R * Kp * 2;                 // 16-B zero block
+  const int a_bytes = ALDS ? zero_off + 16 : 0;
+  float* lds_scale = reinterpret_cast<float*>(smem + a_bytes);
+  uint32_t* lds_zc = reinterpret_cast<uint32_t*>(smem + a_bytes + size_t(nwi) * ng * 16 * 4);
 
-  float* lds_scale = reinterpret_cast<float*>(smem);
-  uint32_t* lds_zc = reinterpret_cast<uint32_t*>(smem + size_t(nwi) * ng * 16 * 4);
-
-  // 1) issue this wave's first B chunk early (before the scale preload barrier)
+  // 1) this wave's weight tiles go out first: one coalesced 16 B/lane nontemporal load per 1 KiB tile
   const int tpw = a.tiles_per_wave;
   const int tw0 = ks * tpw;
   const int tw1 = min(nt, tw0 + tpw);
@@ -257,42 +306,145 @@ __global__ __launch_bounds__(1024) void woq_skinny_kernel(SkinnyArgs a) {
     b[i] = __builtin_nontemporal_load(tile_base + size_t(t) * 64);
   }
 
-  // 2) cooperative preload of the group scales (and zp constants) of this WG's stripe(s) into LDS
-  for (int wi = 0; wi < nwi; wi++) {
-    const SkinnyWeight& Wl = a.w[dual ? wi : wsel];
+  const int32_t* shf = W.shuffle;
+  const bool vec_ok = a.vec_ok != 0;
+  // 2) stage A (whole K, all M rows) and 3) the group scales / zp constants into LDS.  Rounds of fixed-size,
+  //    clamped (never predicated) loads so that the first round is in flight together with the weight tiles: the
+  //    prologue costs one memory round trip.
+  {
+    constexpr int VEC = 16 / ESZ;
+    constexpr int AR = 4;  // A vectors per thread per round
+    constexpr int SR = 4;  // scale entries per thread per round
+    const int bd = blockDim.x;
+    const int a_vecs = ALDS ? (a.M * Kp) / VEC : 0;
     const int cnt = ng * 16;
-    const size_t soff = size_t(s) * ng * 16;
-    for (int i = threadIdx.x; i < cnt; i += blockDim.x) {
-      lds_scale[wi * cnt + i] = load_scale(Wl.scales, soff + i, a.scale_t);
-      int zp = Wl.zps ? int(Wl.zps[soff + i]) : 0;
-      h2_t c = zp_const(bias_of<BITS>() + zp);
-      lds_zc[wi * cnt + i] = __builtin_bit_cast(uint32_t, c);
-    }
+    const bool a_fast = a.a_fast != 0;
+    const int rounds = max((a_vecs + bd * AR - 1) / (bd * AR), (cnt + bd * SR - 1) / (bd * SR));
+    const char* Ab = static_cast<const char*>(a.A);
+    auto stage_round = [&](const int r) {
+      uint4 av[AR];
+      float sv[SR];
+      int zv[SR];
+      if constexpr (ALDS) {
+        if (a_fast) {
+#pragma unroll
+          for (int q = 0; q < AR; q++) {
+            const int v = min((r * AR + q) * bd + int(threadIdx.x), a_vecs - 1);
+            const int idx = v * VEC, row = idx / Kp, k = idx - row * Kp;
+            const int kc = min(k, a.K - VEC);
+            av[q] = *reinterpret_cast<const uint4*>(Ab + (size_t(row) * a.lda + kc) * ESZ);
+          }
+        }
+      }
+      // scales / zero points: loop the (<= 2) weights uniformly so their pointers stay scalar
+      uint32_t sraw[2][SR];
+      int zraw[2][SR];
+#pragma unroll
+      for (int wi = 0; wi < 2; wi++) {
+        if (wi < nwi) {
+          const SkinnyWeight& Wl = a.w[dual ? wi : wsel];
+          const size_t soff = size_t(s) * cnt;
+          // branch-free: a scale is read as two 16-bit halves (stride 2 for f32, the same half twice for bf16/f16)
+          const int sstr = a.scale_t == kScaleF32 ? 2 : 1;
+          const uint16_t* sp = static_cast<const uint16_t*>(Wl.scales) + soff * sstr;
+          const bool hz = Wl.zps != nullptr;
+          const int8_t* zp = hz ? Wl.zps + soff : static_cast<const int8_t*>(Wl.scales);
+          const int zmask = hz ? -1 : 0;
+#pragma unroll
+          for (int q = 0; q < SR; q++) {
+            const int e = min((r * SR + q) * bd + int(threadIdx.x), cnt - 1);
+            const uint32_t lo = sp[e * sstr], hi = sp[e * sstr + sstr - 1];
+            sraw[wi][q] = lo | (hi << (16 * (sstr - 1)));  // f32: lo|hi<<16; 16-bit: lo|lo
+            zraw[wi][q] = int(zp[hz ? e : 0]) & zmask;
+          }
+        }
+      }
+      if constexpr (ALDS) {
+        if (a_fast) {
+#pragma unroll
+          for (int q = 0; q < AR; q++) {
+            const int v = (r * AR + q) * bd + int(threadIdx.x);
+            if (v < a_vecs) {
+              const int idx = v * VEC, row = idx / Kp, k = idx - row * Kp;
+              uint4 x = av[q];
+              if (k >= a.K) x = make_uint4(0u, 0u, 0u, 0u);
+              stage_store<AT, VEC>(smem, x, row, k, Kp, a.M);
+            }
+          }
+        } else {  // act-order gather / unaligned rows: element-wise staging
+          for (int q = 0; q < AR; q++) {
+            const int v = (r * AR + q) * bd + int(threadIdx.x);
+            if (v >= a_vecs) break;
+            const int idx = v * VEC, row = idx / Kp, k = idx - row * Kp;
+            uint32_t w[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+            for (int j = 0; j < VEC; j++) {
+              const int kk = k + j;
+              uint32_t e = 0;
+              if (kk < a.K) {
+                const size_t src = size_t(row) * a.lda + (shf ? shf[kk] : kk);
+                if constexpr (ESZ == 4)
+                  e = static_cast<const uint32_t*>(a.A)[src];
+                else
+                  e = static_cast<const uint16_t*>(a.A)[src];
+              }
+              if constexpr (ESZ == 4)
+                w[j] = e;
+              else
+                w[j >> 1] |= e << (16 * (j & 1));
+            }
+            stage_store<AT, VEC>(smem, make_uint4(w[0], w[1], w[2], w[3]), row, k, Kp, a.M);
+          }
+        }
+        if (threadIdx.x == 0 && r == 0) *reinterpret_cast<uint4*>(smem + zero_off) = make_uint4(0u, 0u, 0u, 0u);
+      }
+#pragma unroll
+      for (int wi = 0; wi < 2; wi++) {
+        if (wi < nwi) {
+#pragma unroll
+          for (int q = 0; q < SR; q++) {
+            const int e = (r * SR + q) * bd + int(threadIdx.x);
+            if (e < cnt) {
+              const uint32_t x = sraw[wi][q];
+              float sc;
+              if (a.scale_t == kScaleF32)
+                sc = __uint_as_float(x);
+              else if (a.scale_t == kScaleBF16)
+                sc = __uint_as_float(x << 16);
+              else
+                sc = f16_bits_to_f32(uint16_t(x));
+              lds_scale[wi * cnt + e] = sc;
+              lds_zc[wi * cnt + e] = __builtin_bit_cast(uint32_t, zp_const(bias_of<BITS>() + zraw[wi][q]));
+            }
+          }
+        }
+      }
+    };
+    stage_round(0);  // straight-line: in flight together with the weight tiles
+    for (int r = 1; r < rounds; r++) stage_round(r);
   }
   __syncthreads();
 
-  const int m = lane & 15;      // A-operand row this lane feeds
-  const int kq = lane >> 4;     // k-quarter of the 32-k step
+  const int m = lane & 15;   // A-operand row fed by this lane
+  const int kq = lane >> 4;  // k-quarter of the 32-k step
   const int M = a.M;
-  // HILO==1: rows 0..7 carry hi(A[m]), rows 8..15 carry lo(A[m-8]); HILO==2: two passes; HILO==0: fp16 A as is.
-  int arow;
-  bool aact;
-  bool is_lo = false;
-  if (HILO == 1) {
-    arow = m & 7;
-    is_lo = m >= 8;
-    aact = arow < M;
-  } else {
-    arow = m;
-    aact = m < M;
-  }
-  const bool vec_ok = a.vec_ok != 0;
-  const int32_t* shf = W.shuffle;
+  // HILO==1: rows 0..7 carry hi(A[m]), rows 8..15 lo(A[m-8]); HILO==2: two MFMA passes; HILO==0: fp16 A as is
+  const int arow = HILO == 1 ? (m & 7) : m;
+  const bool is_lo = HILO == 1 && m >= 8;
+  const bool aact = arow < M;
+  // byte offsets of this lane's staged rows (hi row arow; lo row M + arow)
+  const int a_hi_off = (HILO == 1 && is_lo ? (a.M + arow) : arow) * Kp * 2;
+  const int a_lo_off = (a.M + arow) * Kp * 2;
   const float* sc_l = lds_scale + (dual ? my_w : 0) * ng * 16 + (lane & 15);
   const uint32_t* zc_l = lds_zc + (dual ? my_w : 0) * ng * 16 + (lane & 15);
 
   f4_t acc = {0.f, 0.f, 0.f, 0.f};
   f4_t accg = {0.f, 0.f, 0.f, 0.f};
+  // group bookkeeping in scalars: g = group of the current step, rem = steps left in it
+  const int spg = a.steps_per_group;
+  const int st0 = tw0 * SPT;
+  int g = min(st0 / spg, ng - 1);
+  int rem = spg - (st0 - g * spg);
   const int last_step = tw1 * SPT - 1;
 
   for (int c0 = tw0; c0 < tw1; c0 += CH) {
@@ -311,56 +463,65 @@ __global__ __launch_bounds__(1024) void woq_skinny_kernel(SkinnyArgs a) {
         for (int d = 0; d < SPT; d++) {
           const int st = t * SPT + d;
           const int k0 = st * 32 + kq * 8;
-          const int g = min((st * 32) / bs, ng - 1);
           const h2_t c2 = as_h2(zc_l[g * 16]);
           const h8_t bf = dequant_step<BITS>(b[i], d, c2);
-          float av[8];
-          if (aact) {
-            load_a8<AT>(a.A, a.lda, arow, k0, a.K, shf, vec_ok, av);
+          if constexpr (ALDS) {
+            const h8_t af = *reinterpret_cast<const h8_t*>(smem + (aact ? a_hi_off + k0 * 2 : zero_off));
+            if (HILO == 2) {
+              const h8_t afl = *reinterpret_cast<const h8_t*>(smem + (aact ? a_lo_off + k0 * 2 : zero_off));
+              accg = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, bf, accg, 0, 0, 0);
+              accg = __builtin_amdgcn_mfma_f32_16x16x32_f16(afl, bf, accg, 0, 0, 0);
+            } else {
+              accg = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, bf, accg, 0, 0, 0);
+            }
           } else {
+            float av[8];
+            if (aact) {
+              load_a8<AT>(a.A, a.lda, arow, k0, a.K, shf, vec_ok, av);
+            } else {
 #pragma unroll
-            for (int j = 0; j < 8; j++) av[j] = 0.f;
-          }
-          h8_t ah, al;
+              for (int j = 0; j < 8; j++) av[j] = 0.f;
+            }
+            h8_t ah, al;
 #pragma unroll
-          for (int j = 0; j < 8; j++) {
-            _Float16 h = _Float16(av[j]);
-            ah[j] = h;
-            if (HILO != 0) al[j] = _Float16(av[j] - float(h));
+            for (int j = 0; j < 8; j++) {
+              const _Float16 h = _Float16(av[j]);
+              ah[j] = h;
+              if (HILO != 0) al[j] = _Float16(av[j] - float(h));
+            }
+            if (HILO == 1) {
+              accg = __builtin_amdgcn_mfma_f32_16x16x32_f16(is_lo ? al : ah, bf, accg, 0, 0, 0);
+            } else if (HILO == 2) {
+              accg = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bf, accg, 0, 0, 0);
+              accg = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bf, accg, 0, 0, 0);
+            } else {
+              accg = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bf, accg, 0, 0, 0);
+            }
           }
-          if (HILO == 1) {
-            h8_t af = is_lo ? al : ah;
-            accg = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, bf, accg, 0, 0, 0);
-          } else if (HILO == 2) {
-            accg = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bf, accg, 0, 0, 0);
-            accg = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bf, accg, 0, 0, 0);
-          } else {
-            accg = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bf, accg, 0, 0, 0);
-          }
-          const bool gend = (((st + 1) * 32) % bs == 0) || st == last_step;
-          if (gend) {
-            const float sc = sc_l[g * 16];
-            acc += accg * sc;
+          if (rem == 1 || st == last_step) {
+            acc += accg * sc_l[min(g, ng - 1) * 16];
             accg = f4_t{0.f, 0.f, 0.f, 0.f};
+          }
+          if (--rem == 0) {
+            rem = spg;
+            g = min(g + 1, ng - 1);
           }
         }
       }
     }
   }
 
-  // 3) rows: HILO==1 folds lo rows (8..15, lanes 32..63) onto hi rows (0..7, lanes 0..31)
+  // 4) HILO==1 folds the lo rows (8..15, lanes 32..63) onto the hi rows (0..7, lanes 0..31)
   if (HILO == 1) {
 #pragma unroll
     for (int i = 0; i < 4; i++) acc[i] += __shfl_down(acc[i], 32, 64);
   }
-  // 4) reduce the KS slices through LDS (reuse the scale region after a barrier)
+  // 5) reduce the K slices through LDS
   __syncthreads();
   float* red = reinterpret_cast<float*>(smem);
   *reinterpret_cast<f4_t*>(red + (size_t(wave) * 64 + lane) * 4) = acc;
   __syncthreads();
-  // each (weight-in-wg, m, nn) output is produced by one thread
-  const int outs = 16 * 16;
-  for (int o = threadIdx.x; o < outs * (dual ? 1 : 1); o += blockDim.x) {
+  for (int o = threadIdx.x; o < 256; o += blockDim.x) {
     const int mm = o >> 4, nn = o & 15;
     if (mm >= M) continue;
     const int src_lane = (mm >> 2) * 16 + nn, reg = mm & 3;
@@ -389,13 +550,13 @@ __global__ __launch_bounds__(1024) void woq_skinny_kernel(SkinnyArgs a) {
         v += a.res[size_t(mm) * a.ld_res + n];
         break;
       case kEpiSiluMul: {
-        float t1 = silu_f(y0);
+        const float t1 = silu_f(y0);
         if (a.aux) a.aux[size_t(mm) * a.ld_aux + n] = t1;
         v = t1 * y1;
         break;
       }
       case kEpiGeluMul: {
-        float t1 = gelu_f(y0);
+        const float t1 = gelu_f(y0);
         if (a.aux) a.aux[size_t(mm) * a.ld_aux + n] = t1;
         v = t1 * y1;
         break;
@@ -411,7 +572,7 @@ __global__ __launch_bounds__(1024) void woq_skinny_kernel(SkinnyArgs a) {
 // Block 256 threads = 4 waves (2 x 2); block tile BM x BN = 128 x 128 (8 stripes); K step = one tile (KT).
 // LDS A tile: [128 rows][KT fp16] with 16-B chunk XOR swizzle (chunk ^= row & 15).
 template <int BITS, int AT>
-__global__ __launch_bounds__(256, 1) void woq_gemm_kernel(GemmArgs a) {
+__global__ __launch_bounds__(256, 2) void woq_gemm_kernel(GemmArgs a) {
   constexpr int KT = BITS == 4 ? 128 : (BITS == 2 ? 256 : 64);
   constexpr int SPT = KT / 32;
   constexpr int BM = 128, BN = 128;
@@ -583,27 +744,36 @@ hipError_t launch_repack(const RepackArgs& a, hipStream_t stream) {
   return hipGetLastError();
 }
 
-template <int BITS, int AT, int HILO>
+template <int BITS, int AT, int HILO, bool ALDS>
 static hipError_t skinny_dispatch_ch(const SkinnyArgs& a, int ch, dim3 grid, dim3 block, size_t lds,
                                      hipStream_t stream) {
   if (ch == 4)
-    hipLaunchKernelGGL((woq_skinny_kernel<BITS, AT, HILO, 4>), grid, block, lds, stream, a);
+    hipLaunchKernelGGL((woq_skinny_kernel<BITS, AT, HILO, 4, ALDS>), grid, block, lds, stream, a);
   else
-    hipLaunchKernelGGL((woq_skinny_kernel<BITS, AT, HILO, 8>), grid, block, lds, stream, a);
+    hipLaunchKernelGGL((woq_skinny_kernel<BITS, AT, HILO, 8, ALDS>), grid, block, lds, stream, a);
   return hipGetLastError();
 }
 
-template <int BITS>
-static hipError_t skinny_dispatch_bits(const SkinnyArgs& a, int at, int hilo, int ch, dim3 g, dim3 b, size_t lds,
+template <int BITS, int AT, int HILO>
+static hipError_t skinny_dispatch_alds(const SkinnyArgs& a, bool alds, int ch, dim3 g, dim3 b, size_t lds,
                                        hipStream_t st) {
-  if (at == kActF16) return skinny_dispatch_ch<BITS, kActF16, 0>(a, ch, g, b, lds, st);
-  if (at == kActF32) {
-    if (hilo == 1) return skinny_dispatch_ch<BITS, kActF32, 1>(a, ch, g, b, lds, st);
-    return skinny_dispatch_ch<BITS, kActF32, 2>(a, ch, g, b, lds, st);
-  }
-  if (hilo == 1) return skinny_dispatch_ch<BITS, kActBF16, 1>(a, ch, g, b, lds, st);
-  return skinny_dispatch_ch<BITS, kActBF16, 2>(a, ch, g, b, lds, st);
+  if (alds) return skinny_dispatch_ch<BITS, AT, HILO, true>(a, ch, g, b, lds, st);
+  return skinny_dispatch_ch<BITS, AT, HILO, false>(a, ch, g, b, lds, st);
 }
+
+template <int BITS>
+static hipError_t skinny_dispatch_bits(const SkinnyArgs& a, int at, int hilo, bool alds, int ch, dim3 g, dim3 b,
+                                       size_t lds, hipStream_t st) {
+  if (at == kActF16) return skinny_dispatch_alds<BITS, kActF16, 0>(a, alds, ch, g, b, lds, st);
+  if (at == kActF32) {
+    if (hilo == 1) return skinny_dispatch_alds<BITS, kActF32, 1>(a, alds, ch, g, b, lds, st);
+    return skinny_dispatch_alds<BITS, kActF32, 2>(a, alds, ch, g, b, lds, st);
+  }
+  if (hilo == 1) return skinny_dispatch_alds<BITS, kActBF16, 1>(a, alds, ch, g, b, lds, st);
+  return skinny_dispatch_alds<BITS, kActBF16, 2>(a, alds, ch, g, b, lds, st);
+}
+
+static constexpr size_t kSkinnyLdsBudget = 64 * 1024;
 
 hipError_t launch_skinny(const SkinnyArgs& a, int bits, int act_t, int waves_per_wg, int stripes, int ch,
                          hipStream_t stream) {
@@ -611,12 +781,17 @@ hipError_t launch_skinny(const SkinnyArgs& a, int bits, int act_t, int waves_per
   const int nwi = dual ? 2 : 1;
   int ngmax = 0;
   for (int i = 0; i < a.nw; i++) ngmax = std::max(ngmax, a.w[i].ng);
-  size_t lds = std::max(size_t(nwi) * ngmax * 16 * 8, size_t(waves_per_wg) * 64 * 16);
+  const int KT = bits == 4 ? 128 : (bits == 2 ? 256 : 64);
+  const size_t rows = act_t == kActF16 ? size_t(a.M) : 2 * size_t(a.M);
+  const size_t sc = size_t(nwi) * ngmax * 16 * 8;
+  const size_t abytes = rows * a.w[0].nt * KT * 2 + 16;
+  const bool alds = abytes + sc <= kSkinnyLdsBudget;
+  size_t lds = std::max((alds ? abytes : 0) + sc, size_t(waves_per_wg) * 64 * 16);
   const int hilo = act_t == kActF16 ? 0 : (a.M <= 8 ? 1 : 2);
   dim3 grid(stripes), block(waves_per_wg * 64);
-  if (bits == 4) return skinny_dispatch_bits<4>(a, act_t, hilo, ch, grid, block, lds, stream);
-  if (bits == 2) return skinny_dispatch_bits<2>(a, act_t, hilo, ch, grid, block, lds, stream);
-  return skinny_dispatch_bits<8>(a, act_t, hilo, ch, grid, block, lds, stream);
+  if (bits == 4) return skinny_dispatch_bits<4>(a, act_t, hilo, alds, ch, grid, block, lds, stream);
+  if (bits == 2) return skinny_dispatch_bits<2>(a, act_t, hilo, alds, ch, grid, block, lds, stream);
+  return skinny_dispatch_bits<8>(a, act_t, hilo, alds, ch, grid, block, lds, stream);
 }
 
 template <int BITS>
