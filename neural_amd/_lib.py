@@ -7,7 +7,8 @@ import os
 import re
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libneural_amd.so")
+# NAD_LIB_PATH: development override (tools/trace_skinny.py loads the phase-trace build)
+LIB_PATH = os.environ.get("NAD_LIB_PATH") or os.path.join(_HERE, "libneural_amd.so")
 HEADER = os.path.join(os.path.dirname(_HERE), "include", "neural_amd.h")
 
 _p = C.c_void_p

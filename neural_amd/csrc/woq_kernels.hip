@@ -30,6 +30,41 @@ typedef _Float16 h8_t __attribute__((ext_vector_type(8)));
 typedef float f4_t __attribute__((ext_vector_type(4)));
 typedef uint32_t u4_t __attribute__((ext_vector_type(4)));
 
+// ------------------------------------------------------------------------------------------------ phase trace
+// Development instrumentation (make trace -> libneural_amd_trace.so): per-workgroup wall-clock stamps of the
+// skinny kernel's phases, read back with nad_trace_fetch().  Compiled out of the product library.
+#ifdef NAD_PHASE_TRACE
+constexpr int kTraceSlots = 8, kTraceMaxWg = 16384;
+__device__ unsigned long long nad_trace_buf[kTraceSlots][kTraceMaxWg];
+__device__ int nad_trace_grid;  // record only launches with this many workgroups (0: all)
+#define NAD_TRACE_ON (blockIdx.x < kTraceMaxWg && (nad_trace_grid == 0 || int(gridDim.x) == nad_trace_grid))
+#define NAD_TRACE(slot)                                                                              \
+  do {                                                                                               \
+    if (threadIdx.x == 0 && NAD_TRACE_ON) nad_trace_buf[slot][blockIdx.x] = wall_clock64(); \
+  } while (0)
+#define NAD_TRACE_MAX(slot)                                                                             \
+  do {                                                                                                  \
+    if ((threadIdx.x & 63) == 0 && NAD_TRACE_ON)                                            \
+      atomicMax(&nad_trace_buf[slot][blockIdx.x], (unsigned long long)wall_clock64());                  \
+  } while (0)
+#define NAD_TRACE_ID()                                                                                  \
+  do {                                                                                                  \
+    if (threadIdx.x == 0 && NAD_TRACE_ON)                                                               \
+      nad_trace_buf[kTraceSlots - 1][blockIdx.x] =                                                      \
+          (unsigned long long)__smid() | ((unsigned long long)__builtin_amdgcn_s_getreg((3 << 11) | 20) << 32); \
+  } while (0)
+#else
+#define NAD_TRACE(slot) \
+  do {                  \
+  } while (0)
+#define NAD_TRACE_MAX(slot) \
+  do {                      \
+  } while (0)
+#define NAD_TRACE_ID() \
+  do {                 \
+  } while (0)
+#endif
+
 // ------------------------------------------------------------------------------------------------ helpers
 __device__ __forceinline__ float bf16_bits_to_f32(uint16_t x) { return __uint_as_float(uint32_t(x) << 16); }
 __device__ __forceinline__ float f16_bits_to_f32(uint16_t x) {
@@ -270,6 +305,8 @@ __global__ __launch_bounds__(1024) void woq_skinny_kernel(SkinnyArgs a) {
   const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));
   const int nwaves = blockDim.x >> 6;
   const bool dual = a.epi == kEpiSiluMul || a.epi == kEpiGeluMul;
+  NAD_TRACE(0);
+  NAD_TRACE_ID();
 
   // which weight and stripe does this workgroup own (all wave-uniform)
   int wsel = 0;
@@ -424,6 +461,7 @@ __global__ __launch_bounds__(1024) void woq_skinny_kernel(SkinnyArgs a) {
     for (int r = 1; r < rounds; r++) stage_round(r);
   }
   __syncthreads();
+  NAD_TRACE(1);
 
   const int m = lane & 15;   // A-operand row fed by this lane
   const int kq = lane >> 4;  // k-quarter of the 32-k step
@@ -516,6 +554,7 @@ __global__ __launch_bounds__(1024) void woq_skinny_kernel(SkinnyArgs a) {
 #pragma unroll
     for (int i = 0; i < 4; i++) acc[i] += __shfl_down(acc[i], 32, 64);
   }
+  NAD_TRACE_MAX(2);
   // 5) reduce the K slices through LDS
   __syncthreads();
   float* red = reinterpret_cast<float*>(smem);
@@ -566,6 +605,7 @@ __global__ __launch_bounds__(1024) void woq_skinny_kernel(SkinnyArgs a) {
     }
     Wo.out[size_t(mm) * Wo.ldo + n] = v;
   }
+  NAD_TRACE(3);
 }
 
 // ------------------------------------------------------------------------------------------------ GEMM (M>16)
@@ -814,3 +854,26 @@ hipError_t launch_gemm(const GemmArgs& a, int bits, int act_t, hipStream_t strea
 }
 
 }  // namespace nad
+
+#ifdef NAD_PHASE_TRACE
+extern "C" int nad_trace_clock_khz() {
+  int dev = 0, khz = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return -1;
+  if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess) return -1;
+  return khz;
+}
+
+extern "C" int nad_trace_fetch(void* host, size_t bytes, int clear, int grid_filter) {
+  const size_t n = sizeof(nad::nad_trace_buf) < bytes ? sizeof(nad::nad_trace_buf) : bytes;
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (host && hipMemcpyFromSymbol(host, HIP_SYMBOL(nad::nad_trace_buf), n) != hipSuccess) return -1;
+  if (clear) {
+    void* p = nullptr;
+    if (hipGetSymbolAddress(&p, HIP_SYMBOL(nad::nad_trace_buf)) != hipSuccess) return -1;
+    if (hipMemset(p, 0, sizeof(nad::nad_trace_buf)) != hipSuccess) return -1;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(nad::nad_trace_grid), &grid_filter, sizeof(int)) != hipSuccess) return -1;
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+  }
+  return 0;
+}
+#endif
