@@ -137,6 +137,10 @@ int nad_device_forward(const void* act, int act_dtype, const void* devstor, floa
 /* fused Q/K/V (ip_fusion_qkv.cpp:22-93): out_i = X . W_i^T, one launch; W_i share K, blocksize, bits, scale dtype */
 int nad_device_qkv_forward(const void* act, int act_dtype, const void* wq, const void* wk, const void* wv, float* oq,
                            float* ok, float* ov, int m, int k, int lda, int ldo_q, int ldo_k, int ldo_v, void* queue);
+/* gate/up half of the fused FFN (ip_fusion_ffn.cpp:407-433): tmp2 = act(X.W1^T) * (X.W3^T), tmp1 = act(X.W1^T)
+ * (optional for m <= 16).  epi: NAD_EPI_SILU_MUL / NAD_EPI_GELU_MUL. */
+int nad_device_ffn_gate_up(const void* act, int act_dtype, const void* w1, const void* w3, float* tmp1, float* tmp2,
+                           int m, int fin, int fmid, int lda, int epi, void* queue);
 /* fused FFN (ip_fusion_ffn.cpp:407-457): tmp1 = act1(X.W1^T) [optional], tmp2 = tmp1 * (X.W3^T), out = tmp2 . W2^T.
  * epi = NAD_EPI_SILU_MUL or NAD_EPI_GELU_MUL. */
 int nad_device_ffn_forward(const void* act, int act_dtype, const void* w1, const void* w2, const void* w3, float* tmp1,

@@ -67,6 +67,7 @@ SIGNATURES = {
     "nad_device_forward": (_i, [_p, _i, _p, _p, _i, _i, _i, _i, _i, _i, _p, _i, _p, _i, _p]),
     "nad_device_qkv_forward": (_i, [_p, _i, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _p]),
     "nad_device_ffn_forward": (_i, [_p, _i, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _p]),
+    "nad_device_ffn_gate_up": (_i, [_p, _i, _p, _p, _p, _p, _i, _i, _i, _i, _i, _p]),
     "nad_blob_split": (_sz, [_p, _i, _i, _i, _i, _p, _sz]),
     "nad_split_range": (_i, [_p, _i, _i, _i, _i, _p, _p]),
     "nad_synthetic_weight": (_i, [_p, _p, _sz, _i, _i, _i, _i, _i, _i, _u64, _p]),

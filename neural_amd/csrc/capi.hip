@@ -2,6 +2,7 @@
 // MI355X.  Host-side orchestration only; all arithmetic on the hot path runs in woq_kernels.hip.
 #include <hip/hip_runtime.h>
 
+#include <climits>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -139,8 +140,9 @@ extern "C" int nad_device_load(const void* hostblob, void* devstor, void* device
   DeviceWeight w{};
   // per-channel (group >= K) is one group covering all tiles
   const int bs = b.blocksize >= b.k ? b.kpad : b.blocksize;
-  const uint64_t need =
-      layout_geometry(w, dtype_bits(b.qtype), b.n, b.k, bs, scale_code(b.scale_t), b.asym, b.has_shuffle);
+  const char* km = getenv("NAD_TILE_KMAJOR");  // layout A/B switch (development); default K-major
+  const uint64_t need = layout_geometry(w, dtype_bits(b.qtype), b.n, b.k, bs, scale_code(b.scale_t), b.asym,
+                                        b.has_shuffle, (km && *km) ? atoi(km) : 0);
   if (need > capacity) {
     set_err("device buffer too small for the tile layout: need %llu bytes, have %zu (see nad_device_weight_size)",
             (unsigned long long)need, capacity);
@@ -177,6 +179,7 @@ extern "C" int nad_device_load(const void* hostblob, void* devstor, void* device
   ra.nt = w.nt;
   ra.ng = w.ng;
   ra.scale_t = w.scale_t;
+  ra.kmajor = w.kmajor;
   ra.dst_tiles = static_cast<uint32_t*>(w.tiles);
   ra.dst_scales = w.scales;
   ra.dst_zps = w.zps;
@@ -247,6 +250,7 @@ static SkinnyWeight view(const DeviceWeight& w, float* out, int ldo, const float
   v.nt = w.nt;
   v.ng = w.ng;
   v.bs = w.blocksize;
+  v.kmajor = w.kmajor;
   v.ldo = ldo;
   v.out = out;
   v.bias = bias;
@@ -272,9 +276,94 @@ static void skinny_geometry(int total_stripes, int nt, int nwi, int* ks, int* tp
   *ch = t <= 4 ? 4 : 8;
 }
 
+static int env_int(const char* name, int def) {
+  const char* v = getenv(name);
+  return (v && *v) ? atoi(v) : def;
+}
+
+static int device_cus() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                 hipSuccess || n <= 0)
+      n = 256;
+  }
+  return n;
+}
+
+// The persistent stripe-stream GEMV (woq_gemv.hip) when the launch fits it: M <= 16, the staged activations fit LDS,
+// the group size tiles the K tile, and all weights share one act-order LUT.  Returns 1 if launched, 0 if not eligible,
+// -1 on a launch error.
+static int try_gemv(const void* act, int act_t, int lda, int m, int k, int nw, const DeviceWeight* const* ws,
+                    float* const* outs, const int* ldos, int epi, const float* bias, int bias_ld, const float* res,
+                    int ld_res, float* aux, int ld_aux, hipStream_t st) {
+  if (env_int("NAD_GEMV_DISABLE", 0)) return 0;
+  const DeviceWeight& w0 = *ws[0];
+  for (int i = 1; i < nw; i++)
+    if (ws[i]->shuffle != w0.shuffle || ws[i]->nt != w0.nt || ws[i]->ng != w0.ng || ws[i]->bits != w0.bits ||
+        ws[i]->asym != w0.asym || ws[i]->scale_t != w0.scale_t || ws[i]->blocksize != w0.blocksize)
+      return 0;
+  int tpg = 0;
+  const int gpt = gemv_groups_per_tile(w0.bits, w0.nt, w0.ng, w0.blocksize, &tpg);
+  if (gpt == 0 || (gpt >= 4 && w0.asym)) return 0;
+  GemvArgs a{};
+  a.A = act;
+  a.lda = lda;
+  a.M = m;
+  a.K = k;
+  a.act_t = act_t;
+  a.dual = (epi == kEpiSiluMul || epi == kEpiGeluMul) ? 1 : 0;
+  a.nt = w0.nt;
+  a.ng = w0.ng;
+  a.bs = w0.blocksize;
+  a.tpg_mask = tpg == 0 ? 0x7fffffff : tpg - 1;
+  a.tpg_shift = tpg == 0 ? 31 : __builtin_ctz(unsigned(tpg));
+  a.scale_t = w0.scale_t;
+  a.asym = w0.asym;
+  a.epi = epi;
+  a.shuffle = w0.shuffle;
+  a.a_fast = (vec_aligned(act, lda, act_t) && w0.shuffle == nullptr && k % 8 == 0) ? 1 : 0;
+  a.res = res;
+  a.ld_res = ld_res;
+  a.aux = aux;
+  a.ld_aux = ld_aux;
+  int stripes = 0;
+  for (int i = 0; i < 4; i++) a.stripe_base[i] = INT_MAX;
+  for (int i = 0; i < nw; i++) {
+    a.w[i] = view(*ws[i], outs[i], ldos[i], bias, bias_ld);
+    a.stripe_base[i] = stripes;
+    stripes += ws[i]->ns;
+  }
+  for (int i = nw; i < 3; i++) a.w[i] = a.w[0];
+  a.units = a.dual ? ws[0]->ns : stripes;
+  const int wpc = std::max(1, env_int("NAD_GEMV_WPC", 1));
+  int grid = std::max(1, std::min(a.units, device_cus() * wpc));
+  if (env_int("NAD_GEMV_GRID", 0) > 0) grid = std::min(a.units, env_int("NAD_GEMV_GRID", 0));  // tests / tuning
+  // waves per workgroup: ~4 tiles each, 4..12 (measured on MI355X over the Llama-2-7B decode shapes)
+  const int tiles_wg = ((a.units + grid - 1) / grid) * (a.dual ? 2 : 1) * w0.nt;
+  int waves = std::max(4, std::min(12, tiles_wg / 4));
+  if (env_int("NAD_GEMV_WAVES", 0) > 0) waves = std::min(16, env_int("NAD_GEMV_WAVES", 0));
+  const size_t lds = gemv_lds_bytes(a, w0.bits, waves, grid, &a.part_off, &a.part_bytes);
+  if (lds > 160 * 1024) return 0;
+  // buffer-resource offsets are 32-bit: every tile array, scale array and the activations must stay below 2 GiB
+  const int esz = act_t == kActF32 ? 4 : 2;
+  if (uint64_t(m) * lda * esz >= (1ull << 30)) return 0;
+  for (int i = 0; i < nw; i++)
+    if (uint64_t(ws[i]->ns) * ws[i]->nt * 1024 >= (1ull << 30)) return 0;
+  hipError_t e = launch_gemv(a, w0.bits, waves, grid, lds, st);
+  if (e != hipSuccess) {
+    set_err("gemv kernel launch failed: %s", hipGetErrorString(e));
+    return -1;
+  }
+  return 1;
+}
+
 static int run_skinny(const void* act, int act_t, int lda, int m, int k, int nw, const DeviceWeight* const* ws,
                       float* const* outs, const int* ldos, int epi, const float* bias, int bias_ld, const float* res,
                       int ld_res, float* aux, int ld_aux, hipStream_t st) {
+  const int g = try_gemv(act, act_t, lda, m, k, nw, ws, outs, ldos, epi, bias, bias_ld, res, ld_res, aux, ld_aux, st);
+  if (g != 0) return g < 0 ? -1 : 0;
   SkinnyArgs a{};
   a.A = act;
   a.lda = lda;
@@ -404,6 +493,37 @@ extern "C" int nad_device_qkv_forward(const void* act, int act_dtype, const void
   return 0;
 }
 
+// The gate/up half of the fused FFN (ip_fusion_ffn.cpp:407-433): tmp2 = act(X.W1^T) * (X.W3^T), tmp1 = act(X.W1^T)
+// (optional at M <= 16, required above).  Decode: one dual-weight stream launch; prefill: two GEMM launches.
+extern "C" int nad_device_ffn_gate_up(const void* act, int act_dtype, const void* w1p, const void* w3p, float* tmp1,
+                                      float* tmp2, int m, int fin, int fmid, int lda, int epi, void* queue) {
+  const DeviceWeight* w1 = as_weight(w1p);
+  const DeviceWeight* w3 = as_weight(w3p);
+  if (!w1 || !w3) return -1;
+  if (epi != kEpiSiluMul && epi != kEpiGeluMul) {
+    set_err("ffn epilogue must be SILU_MUL or GELU_MUL");
+    return -1;
+  }
+  if (w1->n != fmid || w3->n != fmid || w1->k != fin || w3->k != fin || !same_kind(*w1, *w3)) {
+    set_err("FFN gate/up shapes do not match (fin=%d fmid=%d)", fin, fmid);
+    return -1;
+  }
+  hipStream_t st = static_cast<hipStream_t>(queue);
+  if (m <= kSkinnyMaxM) {
+    const DeviceWeight* ws[2] = {w1, w3};
+    float* outs[2] = {tmp2, tmp2};
+    int ldos[2] = {fmid, fmid};
+    return run_skinny(act, act_dtype, lda, m, fin, 2, ws, outs, ldos, epi, nullptr, 0, nullptr, 0, tmp1, fmid, st);
+  }
+  if (!tmp1) {
+    set_err("prefill FFN needs the tmp1 buffer");
+    return -1;
+  }
+  const int e1 = epi == kEpiSiluMul ? kEpiSilu : kEpiGelu;
+  if (run_gemm(act, act_dtype, lda, m, fin, *w1, tmp1, fmid, e1, nullptr, 0, nullptr, 0, nullptr, 0, st)) return -1;
+  return run_gemm(act, act_dtype, lda, m, fin, *w3, tmp2, fmid, kEpiSiluMul, nullptr, 0, nullptr, 0, tmp1, fmid, st);
+}
+
 extern "C" int nad_device_ffn_forward(const void* act, int act_dtype, const void* w1p, const void* w2p,
                                       const void* w3p, float* tmp1, float* tmp2, float* out, int m, int fin, int fmid,
                                       int fout, int lda, int epi, void* queue) {
@@ -421,22 +541,7 @@ extern "C" int nad_device_ffn_forward(const void* act, int act_dtype, const void
     return -1;
   }
   hipStream_t st = static_cast<hipStream_t>(queue);
-  if (m <= kSkinnyMaxM) {
-    const DeviceWeight* ws[2] = {w1, w3};
-    float* outs[2] = {tmp2, tmp2};
-    int ldos[2] = {fmid, fmid};
-    if (run_skinny(act, act_dtype, lda, m, fin, 2, ws, outs, ldos, epi, nullptr, 0, nullptr, 0, tmp1, fmid, st))
-      return -1;
-  } else {
-    if (!tmp1) {
-      set_err("prefill FFN needs the tmp1 buffer");
-      return -1;
-    }
-    const int e1 = epi == kEpiSiluMul ? kEpiSilu : kEpiGelu;
-    if (run_gemm(act, act_dtype, lda, m, fin, *w1, tmp1, fmid, e1, nullptr, 0, nullptr, 0, nullptr, 0, st)) return -1;
-    if (run_gemm(act, act_dtype, lda, m, fin, *w3, tmp2, fmid, kEpiSiluMul, nullptr, 0, nullptr, 0, tmp1, fmid, st))
-      return -1;
-  }
+  if (nad_device_ffn_gate_up(act, act_dtype, w1p, w3p, tmp1, tmp2, m, fin, fmid, lda, epi, queue)) return -1;
   if (m <= kSkinnyMaxM) {
     const DeviceWeight* ws[1] = {w2};
     float* outs[1] = {out};
@@ -488,7 +593,8 @@ extern "C" int nad_synthetic_weight(void* devstor, void* deviceptr, size_t capac
     return -1;
   }
   DeviceWeight w{};
-  uint64_t need = layout_geometry(w, bits, n, k, blocksize, scale_t, asym != 0, false);
+  const char* km = getenv("NAD_TILE_KMAJOR");
+  uint64_t need = layout_geometry(w, bits, n, k, blocksize, scale_t, asym != 0, false, (km && *km) ? atoi(km) : 0);
   if (need > capacity) {
     set_err("capacity %zu < needed %llu", capacity, (unsigned long long)need);
     return -1;
@@ -528,7 +634,7 @@ __global__ void nad_unrepack_kernel(DeviceWeight w, float* out) {
     const int s = n / 16, c = n % 16, t = kk / KT, kin = kk % KT;
     const int d = kin / 32, kq = (kin % 32) / 8, j = kin % 8;
     const int lane = kq * 16 + c;
-    const uint32_t* tile = static_cast<const uint32_t*>(w.tiles) + (uint64_t(s) * w.nt + t) * 256 + lane * 4;
+    const uint32_t* tile = static_cast<const uint32_t*>(w.tiles) + tile_index(w.kmajor, w.ns, w.nt, s, t) * 256 + lane * 4;
     uint32_t v;
     int bias;
     if (w.bits == 4) {
@@ -544,7 +650,7 @@ __global__ void nad_unrepack_kernel(DeviceWeight w, float* out) {
       bias = 128;
     }
     const int g = kk / w.blocksize;
-    const uint64_t si = (uint64_t(s) * w.ng + g) * 16 + c;
+    const uint64_t si = scale_row(w.kmajor, w.ns, w.ng, s, g) * 16 + c;
     float sc;
     if (w.scale_t == kScaleF32)
       sc = static_cast<const float*>(w.scales)[si];

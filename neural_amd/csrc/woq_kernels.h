@@ -18,7 +18,7 @@ struct RepackArgs {
   const int8_t* src_z;
   int ntile, packrow, kpad, cstep;
   // destination geometry
-  int bits, n, k, ns, nt, ng, scale_t;
+  int bits, n, k, ns, nt, ng, scale_t, kmajor;
   uint32_t* dst_tiles;
   void* dst_scales;
   int8_t* dst_zps;
@@ -30,11 +30,11 @@ struct SkinnyWeight {
   const int8_t* zps;
   const int32_t* shuffle;
   int n, ns, nt, ng, bs;
+  int kmajor;         // tile / scale order (woq_layout.h tile_index, scale_row)
   int ldo;
   float* out;
   const float* bias;  // bias[m * bias_ld + n] (bias_ld = 0 broadcasts one row)
   int bias_ld;
-  int pad_;
 };
 
 struct SkinnyArgs {
@@ -68,9 +68,39 @@ struct GemmArgs {
   SkinnyWeight w;
 };
 
+// Persistent stripe-stream decode GEMV (woq_gemv.hip).  All weights of one launch share K, group size, scale type and
+// symmetry; for the dual epilogues w[0] = gate, w[1] = up.
+struct GemvArgs {
+  const void* A;
+  int lda, M, K;
+  int act_t;            // ActType
+  int dual;             // units are {w[0] stripe s, w[1] stripe s} pairs (SiLU*mul / GELU*mul)
+  int units;            // stripes (non-dual, summed over the weights) or stripe pairs (dual)
+  int stripe_base[4];   // non-dual: first virtual stripe of each weight (unused entries = INT_MAX)
+  int nt, ng, bs;       // tiles along K, groups along K, group size
+  int tpg_mask;         // GPT == 1: tiles per group - 1 (power of two; 0x7fffffff for one group), group = t >> shift
+  int tpg_shift;
+  int scale_t;
+  int asym;
+  int epi;
+  int a_fast;           // 16-B aligned rows, K % 8 == 0, no act-order shuffle: vector staging
+  const int32_t* shuffle;
+  const float* res;
+  int ld_res;
+  float* aux;
+  int ld_aux;
+  int part_off;         // LDS byte offset of the partial-sum slots
+  int part_bytes;       // their size (the wave range table follows)
+  SkinnyWeight w[3];
+};
+
 hipError_t launch_repack(const RepackArgs& a, hipStream_t stream);
 hipError_t launch_skinny(const SkinnyArgs& a, int bits, int act_t, int waves_per_wg, int stripes, int ch,
                          hipStream_t stream);
 hipError_t launch_gemm(const GemmArgs& a, int bits, int act_t, hipStream_t stream);
+// groups per K tile the GEMV handles (1, 2, 4, 8) for this geometry, 0 if unsupported; *tpg = tiles per group
+int gemv_groups_per_tile(int bits, int nt, int ng, int bs, int* tpg);
+size_t gemv_lds_bytes(const GemvArgs& a, int bits, int waves, int grid, int* part_off, int* part_bytes);
+hipError_t launch_gemv(const GemvArgs& a, int bits, int waves, int grid, size_t lds, hipStream_t stream);
 
 }  // namespace nad

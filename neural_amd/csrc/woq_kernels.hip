@@ -21,166 +21,11 @@
 
 #include <cstdint>
 
+#include "woq_device.h"
 #include "woq_kernels.h"
 
 namespace nad {
 
-typedef _Float16 h2_t __attribute__((ext_vector_type(2)));
-typedef _Float16 h8_t __attribute__((ext_vector_type(8)));
-typedef float f4_t __attribute__((ext_vector_type(4)));
-typedef uint32_t u4_t __attribute__((ext_vector_type(4)));
-
-// ------------------------------------------------------------------------------------------------ phase trace
-// Development instrumentation (make trace -> libneural_amd_trace.so): per-workgroup wall-clock stamps of the
-// skinny kernel's phases, read back with nad_trace_fetch().  Compiled out of the product library.
-#ifdef NAD_PHASE_TRACE
-constexpr int kTraceSlots = 8, kTraceMaxWg = 16384;
-__device__ unsigned long long nad_trace_buf[kTraceSlots][kTraceMaxWg];
-__device__ int nad_trace_grid;  // record only launches with this many workgroups (0: all)
-#define NAD_TRACE_ON (blockIdx.x < kTraceMaxWg && (nad_trace_grid == 0 || int(gridDim.x) == nad_trace_grid))
-#define NAD_TRACE(slot)                                                                              \
-  do {                                                                                               \
-    if (threadIdx.x == 0 && NAD_TRACE_ON) nad_trace_buf[slot][blockIdx.x] = wall_clock64(); \
-  } while (0)
-#define NAD_TRACE_MAX(slot)                                                                             \
-  do {                                                                                                  \
-    if ((threadIdx.x & 63) == 0 && NAD_TRACE_ON)                                            \
-      atomicMax(&nad_trace_buf[slot][blockIdx.x], (unsigned long long)wall_clock64());                  \
-  } while (0)
-#define NAD_TRACE_ID()                                                                                  \
-  do {                                                                                                  \
-    if (threadIdx.x == 0 && NAD_TRACE_ON)                                                               \
-      nad_trace_buf[kTraceSlots - 1][blockIdx.x] =                                                      \
-          (unsigned long long)__smid() | ((unsigned long long)__builtin_amdgcn_s_getreg((3 << 11) | 20) << 32); \
-  } while (0)
-#else
-#define NAD_TRACE(slot) \
-  do {                  \
-  } while (0)
-#define NAD_TRACE_MAX(slot) \
-  do {                      \
-  } while (0)
-#define NAD_TRACE_ID() \
-  do {                 \
-  } while (0)
-#endif
-
-// ------------------------------------------------------------------------------------------------ helpers
-__device__ __forceinline__ float bf16_bits_to_f32(uint16_t x) { return __uint_as_float(uint32_t(x) << 16); }
-__device__ __forceinline__ float f16_bits_to_f32(uint16_t x) {
-  return float(__builtin_bit_cast(_Float16, x));
-}
-
-__device__ __forceinline__ float load_scale(const void* p, size_t i, int st) {
-  if (st == kScaleF32) return static_cast<const float*>(p)[i];
-  uint16_t h = static_cast<const uint16_t*>(p)[i];
-  return st == kScaleBF16 ? bf16_bits_to_f32(h) : f16_bits_to_f32(h);
-}
-
-__device__ __forceinline__ h2_t as_h2(uint32_t v) { return __builtin_bit_cast(h2_t, v); }
-
-// One MFMA step's B fragment (8 fp16 = exact integers q - zp) from the packed dwords.
-//   c2 = (-(1024 + bias + zp)) broadcast as half2.
-template <int BITS>
-__device__ __forceinline__ h8_t dequant_step(const u4_t& b, int d, h2_t c2) {
-  h2_t p0, p1, p2, p3;
-  if constexpr (BITS == 4) {
-    uint32_t w = b[d];
-    p0 = as_h2(((w >> 0) & 0x000F000Fu) | 0x64006400u);
-    p1 = as_h2(((w >> 4) & 0x000F000Fu) | 0x64006400u);
-    p2 = as_h2(((w >> 8) & 0x000F000Fu) | 0x64006400u);
-    p3 = as_h2(((w >> 12) & 0x000F000Fu) | 0x64006400u);
-  } else if constexpr (BITS == 2) {
-    uint32_t w = b[d >> 1];
-    int sh = (d & 1) * 8;
-    p0 = as_h2(((w >> (sh + 0)) & 0x00030003u) | 0x64006400u);
-    p1 = as_h2(((w >> (sh + 2)) & 0x00030003u) | 0x64006400u);
-    p2 = as_h2(((w >> (sh + 4)) & 0x00030003u) | 0x64006400u);
-    p3 = as_h2(((w >> (sh + 6)) & 0x00030003u) | 0x64006400u);
-  } else {
-    uint32_t w0 = b[2 * d], w1 = b[2 * d + 1];
-    p0 = as_h2(__builtin_amdgcn_perm(0x64646464u, w0, 0x04010400u));
-    p1 = as_h2(__builtin_amdgcn_perm(0x64646464u, w0, 0x04030402u));
-    p2 = as_h2(__builtin_amdgcn_perm(0x64646464u, w1, 0x04010400u));
-    p3 = as_h2(__builtin_amdgcn_perm(0x64646464u, w1, 0x04030402u));
-  }
-  p0 += c2;
-  p1 += c2;
-  p2 += c2;
-  p3 += c2;
-  h8_t r;
-  r[0] = p0[0];
-  r[1] = p0[1];
-  r[2] = p1[0];
-  r[3] = p1[1];
-  r[4] = p2[0];
-  r[5] = p2[1];
-  r[6] = p3[0];
-  r[7] = p3[1];
-  return r;
-}
-
-template <int BITS>
-__device__ __forceinline__ constexpr int bias_of() {
-  return BITS == 4 ? 8 : (BITS == 2 ? 2 : 128);
-}
-
-__device__ __forceinline__ h2_t zp_const(int bias_plus_zp) {
-  _Float16 c = _Float16(-(1024 + bias_plus_zp));
-  h2_t r;
-  r[0] = c;
-  r[1] = c;
-  return r;
-}
-
-// activation element loaders -> float
-template <int AT>
-__device__ __forceinline__ float a_elem(const void* A, size_t idx) {
-  if constexpr (AT == kActF32) return static_cast<const float*>(A)[idx];
-  if constexpr (AT == kActF16) return float(static_cast<const _Float16*>(A)[idx]);
-  return bf16_bits_to_f32(static_cast<const uint16_t*>(A)[idx]);
-}
-
-// load 8 consecutive activation values A[row][k0..k0+7] (zero beyond K), optional act-order gather
-template <int AT>
-__device__ __forceinline__ void load_a8(const void* A, int lda, int row, int k0, int K, const int32_t* shf, bool vec_ok,
-                                        float (&v)[8]) {
-  const size_t base = size_t(row) * lda;
-  if (shf == nullptr && vec_ok && k0 + 8 <= K) {
-    if constexpr (AT == kActF32) {
-      const float4* p = reinterpret_cast<const float4*>(static_cast<const float*>(A) + base + k0);
-      float4 x = p[0], y = p[1];
-      v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
-      v[4] = y.x; v[5] = y.y; v[6] = y.z; v[7] = y.w;
-    } else {
-      uint4 x = *reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(A) + base + k0);
-      uint32_t w[4] = {x.x, x.y, x.z, x.w};
-#pragma unroll
-      for (int i = 0; i < 4; i++) {
-        if constexpr (AT == kActF16) {
-          h2_t h = as_h2(w[i]);
-          v[2 * i] = float(h[0]);
-          v[2 * i + 1] = float(h[1]);
-        } else {
-          v[2 * i] = __uint_as_float(w[i] << 16);
-          v[2 * i + 1] = __uint_as_float(w[i] & 0xFFFF0000u);
-        }
-      }
-    }
-  } else {
-#pragma unroll
-    for (int j = 0; j < 8; j++) {
-      int k = k0 + j;
-      v[j] = 0.f;
-      if (k < K) v[j] = a_elem<AT>(A, base + (shf ? shf[k] : k));
-    }
-  }
-}
-
-__device__ __forceinline__ float silu_f(float x) { return x / (1.0f + __expf(-x)); }
-__device__ __forceinline__ float gelu_f(float x) {
-  return 0.5f * x * (1.f + tanhf(0.7978845834732056f * (x + 0.044714998453855515f * x * x * x)));
-}
 
 // ------------------------------------------------------------------------------------------------ repack
 // One thread per output dword of the tile layout.
@@ -227,7 +72,7 @@ __global__ void nad_repack_kernel(RepackArgs a) {
       }
       out |= v << (a.bits * p);
     }
-    a.dst_tiles[gid] = out;
+    a.dst_tiles[tile_index(a.kmajor, a.ns, a.nt, s, t) * 256 + (gid & 255)] = out;
   }
 }
 
@@ -239,12 +84,13 @@ __global__ void nad_repack_scales_kernel(RepackArgs a) {
     const int n = s * 16 + c;
     const bool ok = n < a.n;
     const uint64_t src = uint64_t(g) * a.cstep + n;
+    const uint64_t dst = scale_row(a.kmajor, a.ns, a.ng, s, g) * 16 + c;
     if (ssz == 4) {
-      static_cast<float*>(a.dst_scales)[i] = ok ? reinterpret_cast<const float*>(a.src_s)[src] : 0.f;
+      static_cast<float*>(a.dst_scales)[dst] = ok ? reinterpret_cast<const float*>(a.src_s)[src] : 0.f;
     } else {
-      static_cast<uint16_t*>(a.dst_scales)[i] = ok ? reinterpret_cast<const uint16_t*>(a.src_s)[src] : 0;
+      static_cast<uint16_t*>(a.dst_scales)[dst] = ok ? reinterpret_cast<const uint16_t*>(a.src_s)[src] : 0;
     }
-    if (a.dst_zps) a.dst_zps[i] = ok ? a.src_z[src] : 0;
+    if (a.dst_zps) a.dst_zps[dst] = ok ? a.src_z[src] : 0;
   }
 }
 
@@ -305,8 +151,6 @@ __global__ __launch_bounds__(1024) void woq_skinny_kernel(SkinnyArgs a) {
   const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));
   const int nwaves = blockDim.x >> 6;
   const bool dual = a.epi == kEpiSiluMul || a.epi == kEpiGeluMul;
-  NAD_TRACE(0);
-  NAD_TRACE_ID();
 
   // which weight and stripe does this workgroup own (all wave-uniform)
   int wsel = 0;
@@ -335,12 +179,13 @@ __global__ __launch_bounds__(1024) void woq_skinny_kernel(SkinnyArgs a) {
   const int tpw = a.tiles_per_wave;
   const int tw0 = ks * tpw;
   const int tw1 = min(nt, tw0 + tpw);
-  const u4_t* tile_base = reinterpret_cast<const u4_t*>(W.tiles) + size_t(s) * nt * 64 + lane;
+  const u4_t* tile_base = reinterpret_cast<const u4_t*>(W.tiles) + lane;
+  const int tss = W.kmajor ? 1 : nt, tts = W.kmajor ? W.ns : 1;  // tile (s, t) at s * tss + t * tts
   u4_t b[CH];
 #pragma unroll
   for (int i = 0; i < CH; i++) {
     int t = min(tw0 + i, nt - 1);
-    b[i] = __builtin_nontemporal_load(tile_base + size_t(t) * 64);
+    b[i] = __builtin_nontemporal_load(tile_base + (size_t(s) * tss + size_t(t) * tts) * 64);
   }
 
   const int32_t* shf = W.shuffle;
@@ -380,19 +225,19 @@ __global__ __launch_bounds__(1024) void woq_skinny_kernel(SkinnyArgs a) {
       for (int wi = 0; wi < 2; wi++) {
         if (wi < nwi) {
           const SkinnyWeight& Wl = a.w[dual ? wi : wsel];
-          const size_t soff = size_t(s) * cnt;
           // branch-free: a scale is read as two 16-bit halves (stride 2 for f32, the same half twice for bf16/f16)
           const int sstr = a.scale_t == kScaleF32 ? 2 : 1;
-          const uint16_t* sp = static_cast<const uint16_t*>(Wl.scales) + soff * sstr;
+          const uint16_t* sp = static_cast<const uint16_t*>(Wl.scales);
           const bool hz = Wl.zps != nullptr;
-          const int8_t* zp = hz ? Wl.zps + soff : static_cast<const int8_t*>(Wl.scales);
+          const int8_t* zp = hz ? Wl.zps : static_cast<const int8_t*>(Wl.scales);
           const int zmask = hz ? -1 : 0;
 #pragma unroll
           for (int q = 0; q < SR; q++) {
             const int e = min((r * SR + q) * bd + int(threadIdx.x), cnt - 1);
-            const uint32_t lo = sp[e * sstr], hi = sp[e * sstr + sstr - 1];
+            const size_t ei = scale_row(Wl.kmajor, Wl.ns, Wl.ng, s, e >> 4) * 16 + (e & 15);
+            const uint32_t lo = sp[ei * sstr], hi = sp[ei * sstr + sstr - 1];
             sraw[wi][q] = lo | (hi << (16 * (sstr - 1)));  // f32: lo|hi<<16; 16-bit: lo|lo
-            zraw[wi][q] = int(zp[hz ? e : 0]) & zmask;
+            zraw[wi][q] = int(zp[hz ? ei : 0]) & zmask;
           }
         }
       }
@@ -461,7 +306,6 @@ __global__ __launch_bounds__(1024) void woq_skinny_kernel(SkinnyArgs a) {
     for (int r = 1; r < rounds; r++) stage_round(r);
   }
   __syncthreads();
-  NAD_TRACE(1);
 
   const int m = lane & 15;   // A-operand row fed by this lane
   const int kq = lane >> 4;  // k-quarter of the 32-k step
@@ -490,7 +334,7 @@ __global__ __launch_bounds__(1024) void woq_skinny_kernel(SkinnyArgs a) {
 #pragma unroll
       for (int i = 0; i < CH; i++) {
         int t = min(c0 + i, nt - 1);
-        b[i] = __builtin_nontemporal_load(tile_base + size_t(t) * 64);
+        b[i] = __builtin_nontemporal_load(tile_base + (size_t(s) * tss + size_t(t) * tts) * 64);
       }
     }
 #pragma unroll
@@ -554,7 +398,6 @@ __global__ __launch_bounds__(1024) void woq_skinny_kernel(SkinnyArgs a) {
 #pragma unroll
     for (int i = 0; i < 4; i++) acc[i] += __shfl_down(acc[i], 32, 64);
   }
-  NAD_TRACE_MAX(2);
   // 5) reduce the K slices through LDS
   __syncthreads();
   float* red = reinterpret_cast<float*>(smem);
@@ -605,7 +448,6 @@ __global__ __launch_bounds__(1024) void woq_skinny_kernel(SkinnyArgs a) {
     }
     Wo.out[size_t(mm) * Wo.ldo + n] = v;
   }
-  NAD_TRACE(3);
 }
 
 // ------------------------------------------------------------------------------------------------ GEMM (M>16)
@@ -662,7 +504,7 @@ __global__ __launch_bounds__(256, 2) void woq_gemm_kernel(GemmArgs a) {
 #pragma unroll
   for (int j = 0; j < 4; j++) {
     int s = min(s0 + j, W.ns - 1);
-    bcur[j] = tiles[(size_t(s) * nt + 0) * 64 + lane];
+    bcur[j] = tiles[tile_index(W.kmajor, W.ns, nt, s, 0) * 64 + lane];
   }
 
   for (int t = 0; t < nt; t++) {
@@ -689,7 +531,7 @@ __global__ __launch_bounds__(256, 2) void woq_gemm_kernel(GemmArgs a) {
 #pragma unroll
       for (int j = 0; j < 4; j++) {
         int s = min(s0 + j, W.ns - 1);
-        bnext[j] = tiles[(size_t(s) * nt + t + 1) * 64 + lane];
+        bnext[j] = tiles[tile_index(W.kmajor, W.ns, nt, s, t + 1) * 64 + lane];
       }
     }
     __syncthreads();
@@ -701,7 +543,7 @@ __global__ __launch_bounds__(256, 2) void woq_gemm_kernel(GemmArgs a) {
 #pragma unroll
       for (int j = 0; j < 4; j++) {
         const int s = min(s0 + j, W.ns - 1);
-        const size_t zi = (size_t(s) * W.ng + g) * 16 + (lane & 15);
+        const size_t zi = scale_row(W.kmajor, W.ns, W.ng, s, g) * 16 + (lane & 15);
         const int zp = W.zps ? int(W.zps[zi]) : 0;
         bf[j] = dequant_step<BITS>(bcur[j], d, zp_const(bias_of<BITS>() + zp));
       }
@@ -719,7 +561,7 @@ __global__ __launch_bounds__(256, 2) void woq_gemm_kernel(GemmArgs a) {
 #pragma unroll
         for (int j = 0; j < 4; j++) {
           const int s = min(s0 + j, W.ns - 1);
-          const float sc = load_scale(W.scales, (size_t(s) * W.ng + g) * 16 + (lane & 15), a.scale_t);
+          const float sc = load_scale(W.scales, scale_row(W.kmajor, W.ns, W.ng, s, g) * 16 + (lane & 15), a.scale_t);
 #pragma unroll
           for (int i = 0; i < 4; i++) {
             acc[i][j] += accg[i][j] * sc;
@@ -855,25 +697,3 @@ hipError_t launch_gemm(const GemmArgs& a, int bits, int act_t, hipStream_t strea
 
 }  // namespace nad
 
-#ifdef NAD_PHASE_TRACE
-extern "C" int nad_trace_clock_khz() {
-  int dev = 0, khz = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return -1;
-  if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess) return -1;
-  return khz;
-}
-
-extern "C" int nad_trace_fetch(void* host, size_t bytes, int clear, int grid_filter) {
-  const size_t n = sizeof(nad::nad_trace_buf) < bytes ? sizeof(nad::nad_trace_buf) : bytes;
-  if (hipDeviceSynchronize() != hipSuccess) return -1;
-  if (host && hipMemcpyFromSymbol(host, HIP_SYMBOL(nad::nad_trace_buf), n) != hipSuccess) return -1;
-  if (clear) {
-    void* p = nullptr;
-    if (hipGetSymbolAddress(&p, HIP_SYMBOL(nad::nad_trace_buf)) != hipSuccess) return -1;
-    if (hipMemset(p, 0, sizeof(nad::nad_trace_buf)) != hipSuccess) return -1;
-    if (hipMemcpyToSymbol(HIP_SYMBOL(nad::nad_trace_grid), &grid_filter, sizeof(int)) != hipSuccess) return -1;
-    if (hipDeviceSynchronize() != hipSuccess) return -1;
-  }
-  return 0;
-}
-#endif

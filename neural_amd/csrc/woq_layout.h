@@ -13,8 +13,9 @@
 //              int4 dword (one step):   nibble position p holds element j = 2p (p<4) / 2(p-4)+1 (p>=4)
 //              int2 dword (two steps):  crumb position p (0..15): step h = (p&7)>>2, j = 2*(p&3) + (p>>3)
 //              int8 dword pair (step):  byte b of dword w holds element j = 4w + b (v_perm places it)
-//   scales : [ns][ngroups][16] in the blob's scale dtype (f32 / bf16 / f16)
-//   zps    : [ns][ngroups][16] int8 (asym only)
+//            Tile order: stripe-major [ns][nt] or K-major [nt][ns] (DeviceWeight::kmajor, tile_index()).
+//   scales : [ns][ngroups][16] (or K-major [ngroups][ns][16]) in the blob's scale dtype (f32 / bf16 / f16)
+//   zps    : same order as scales, int8 (asym only)
 //   shuffle: [K] int32 act-order LUT (GPTQ desc_act), applied as a gather on the A operand
 #pragma once
 #include <cstdint>
@@ -40,7 +41,7 @@ struct DeviceWeight {
   int32_t scale_t;    // ScaleType
   int32_t asym;
   int32_t has_shuffle;
-  int32_t pad0;
+  int32_t kmajor;     // tile / scale-row order: 0 = stripe-major [ns][nt], 1 = K-major [nt][ns] (see tile_index)
   uint64_t bytes;     // device bytes used from the caller's buffer
   uint64_t src_core_id;
   void* tiles;
@@ -50,6 +51,16 @@ struct DeviceWeight {
   void* owner;        // non-null when the library allocated the device memory itself (nad_* helpers)
 };
 
+// Tile (s, t) and scale row (s, g) positions.  K-major interleaves the stripes at every K position, so the waves of a
+// decode launch -- which sweep K in near lock-step over different stripes -- read one contiguous front of HBM at any
+// instant (no channel camping), and a prefill block's 8 stripes of one K tile are 8 consecutive KiB.
+NAD_HD inline uint64_t tile_index(int kmajor, int ns, int nt, int s, int t) {
+  return kmajor ? uint64_t(t) * ns + s : uint64_t(s) * nt + t;
+}
+NAD_HD inline uint64_t scale_row(int kmajor, int ns, int ng, int s, int g) {
+  return kmajor ? uint64_t(g) * ns + s : uint64_t(s) * ng + g;
+}
+
 NAD_HD inline int tile_k(int bits) { return bits == 4 ? 128 : (bits == 2 ? 256 : 64); }
 NAD_HD inline int steps_per_tile(int bits) { return tile_k(bits) / 32; }
 
@@ -57,8 +68,9 @@ inline uint64_t align256(uint64_t x) { return (x + 255) & ~uint64_t(255); }
 
 // fill the geometry of a DeviceWeight and return the device bytes it needs
 inline uint64_t layout_geometry(DeviceWeight& w, int bits, int n, int k, int blocksize, int scale_t, bool asym,
-                                bool shuffle) {
+                                bool shuffle, int kmajor = 0) {
   w.magic = kWeightMagic;
+  w.kmajor = kmajor;
   w.bits = bits;
   w.n = n;
   w.k = k;

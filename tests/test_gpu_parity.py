@@ -269,3 +269,73 @@ def test_deterministic_and_graph_capturable(oracle):
     g.replay()
     torch.cuda.synchronize()
     assert torch.equal(out, y0)
+
+
+GEMV_GEOM = [
+    # m, n, k, bs, qtype, stype, asym, comp
+    (1, 4096, 4096, 128, S4, F16, False, 4),
+    (1, 1000, 4096, 256, S4, BF16, True, 4),   # a group spans 2 tiles: wave ranges split groups
+    (2, 200, 1024, 64, S4, F32, True, 1),      # 2 groups per tile
+    (3, 320, 2048, 32, S4, F16, False, 2),     # 4 groups per tile
+    (1, 96, 11008, 128, S4, F16, False, 4),    # Llama down K
+    (5, 130, 2048, 128, S2, BF16, True, 1),
+    (8, 72, 768, 64, S8, F32, True, 4),
+    (12, 64, 512, 128, S4, F32, False, 1),     # M 9..16: two MFMA passes (hi, lo)
+    (1, 50, 4096, 4096, S4, F32, True, 1),     # per-channel
+]
+
+
+@pytest.mark.parametrize("cfg", GEMV_GEOM)
+@pytest.mark.parametrize("geom", [(None, None), ("1", "16"), ("3", "5"), ("7", "1"), ("64", "8")])
+def test_gemv_stream_geometry(oracle, monkeypatch, cfg, geom):
+    """The persistent stripe-stream GEMV with forced grids / wave counts: workgroups owning many stripes, wave ranges
+    crossing stripe and group boundaries, single-wave workgroups.  Same bar as the default launch."""
+    grid, waves = geom
+    if grid:
+        monkeypatch.setenv("NAD_GEMV_GRID", grid)
+        monkeypatch.setenv("NAD_GEMV_WAVES", waves)
+    m, n, k, bs, qt, st, asym, comp = cfg
+    blob = _blob(oracle, n, k, bs, qt, st, asym, comp, seed=m + n + bs)
+    w = bestla.DeviceWeight(blob)
+    A = np.random.default_rng(n).uniform(-0.5, 0.5, size=(m, k)).astype(np.float32)
+    ref = oracle.forward(A, blob, n, k)
+    y = w.forward(torch.from_numpy(A).cuda()).cpu().numpy()
+    assert _rel_err(y, ref) <= TOL_DECODE
+
+
+@pytest.mark.parametrize("geom", [(None, None), ("2", "3"), ("5", "16")])
+def test_gemv_stream_fused(oracle, monkeypatch, geom):
+    """QKV (three weights in one stream) and the dual gate/up stream with SiLU*mul under forced geometries."""
+    grid, waves = geom
+    if grid:
+        monkeypatch.setenv("NAD_GEMV_GRID", grid)
+        monkeypatch.setenv("NAD_GEMV_WAVES", waves)
+    k = 1024
+    blobs = [_blob(oracle, n, k, 128, S4, F16, False, 4, seed=i) for i, n in enumerate((256, 80, 80))]
+    ws = [bestla.DeviceWeight(b) for b in blobs]
+    A = np.random.default_rng(3).uniform(-1, 1, size=(1, k)).astype(np.float32)
+    for y, b, n in zip(bestla.qkv_forward(torch.from_numpy(A).cuda(), *ws), blobs, (256, 80, 80)):
+        assert _rel_err(y.cpu().numpy(), oracle.forward(A, b, n, k)) <= TOL_DECODE
+    fin, fmid, fout = 1024, 688, 512
+    b1 = _blob(oracle, fmid, fin, 128, S4, F16, False, 4, seed=31)
+    b3 = _blob(oracle, fmid, fin, 128, S4, F16, False, 4, seed=33)
+    b2 = _blob(oracle, fout, fmid, 128, S4, F16, False, 4, seed=32)
+    w1, w2, w3 = (bestla.DeviceWeight(b) for b in (b1, b2, b3))
+    y = bestla.ffn_forward(torch.from_numpy(A).cuda(), w1, w2, w3, act="silu").cpu().numpy()
+    h1 = oracle.forward(A, b1, fmid, fin).astype(np.float64)
+    h3 = oracle.forward(A, b3, fmid, fin).astype(np.float64)
+    ref = oracle.forward((h1 / (1 + np.exp(-h1)) * h3).astype(np.float32), b2, fout, fmid)
+    assert _rel_err(y, ref) <= 1e-4
+
+
+@pytest.mark.parametrize("cfg", FWD[:9])
+def test_legacy_skinny_kernel(oracle, monkeypatch, cfg):
+    """The per-stripe woq_skinny_kernel (used when the stream GEMV is not eligible) keeps its own parity."""
+    monkeypatch.setenv("NAD_GEMV_DISABLE", "1")
+    m, n, k, bs, qt, st, asym, comp = cfg
+    blob = _blob(oracle, n, k, bs, qt, st, asym, comp, seed=m * 7 + n)
+    w = bestla.DeviceWeight(blob)
+    A = np.random.default_rng(m + n + k).uniform(-0.5, 0.5, size=(m, k)).astype(np.float32)
+    ref = oracle.forward(A, blob, n, k)
+    y = w.forward(torch.from_numpy(A).cuda()).cpu().numpy()
+    assert _rel_err(y, ref) <= TOL_DECODE
