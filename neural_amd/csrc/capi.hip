@@ -302,8 +302,10 @@ static int try_gemv(const void* act, int act_t, int lda, int m, int k, int nw, c
   const DeviceWeight& w0 = *ws[0];
   for (int i = 1; i < nw; i++)
     if (ws[i]->shuffle != w0.shuffle || ws[i]->nt != w0.nt || ws[i]->ng != w0.ng || ws[i]->bits != w0.bits ||
-        ws[i]->asym != w0.asym || ws[i]->scale_t != w0.scale_t || ws[i]->blocksize != w0.blocksize)
+        ws[i]->asym != w0.asym || ws[i]->scale_t != w0.scale_t || ws[i]->blocksize != w0.blocksize ||
+        ws[i]->kmajor)
       return 0;
+  if (w0.kmajor) return 0;  // the stream stages each stripe's scale block: stripe-major layout only
   int tpg = 0;
   const int gpt = gemv_groups_per_tile(w0.bits, w0.nt, w0.ng, w0.blocksize, &tpg);
   if (gpt == 0 || (gpt >= 4 && w0.asym)) return 0;
@@ -340,11 +342,11 @@ static int try_gemv(const void* act, int act_t, int lda, int m, int k, int nw, c
   const int wpc = std::max(1, env_int("NAD_GEMV_WPC", 1));
   int grid = std::max(1, std::min(a.units, device_cus() * wpc));
   if (env_int("NAD_GEMV_GRID", 0) > 0) grid = std::min(a.units, env_int("NAD_GEMV_GRID", 0));  // tests / tuning
-  // waves per workgroup: ~4 tiles each, 4..12 (measured on MI355X over the Llama-2-7B decode shapes)
-  const int tiles_wg = ((a.units + grid - 1) / grid) * (a.dual ? 2 : 1) * w0.nt;
-  int waves = std::max(4, std::min(12, tiles_wg / 4));
-  if (env_int("NAD_GEMV_WAVES", 0) > 0) waves = std::min(16, env_int("NAD_GEMV_WAVES", 0));
-  const size_t lds = gemv_lds_bytes(a, w0.bits, waves, grid, &a.part_off, &a.part_bytes);
+  int waves = gemv_waves(w0.bits, w0.nt, w0.ng, w0.blocksize);
+  if (env_int("NAD_GEMV_WAVES", 0) > 0) waves = std::min(gpt > 1 ? 8 : 16, env_int("NAD_GEMV_WAVES", 0));
+  a.dq_mask = 0x000F000Fu;
+  a.dq_magic = 0x64006400u;
+  const size_t lds = gemv_lds_layout(a, w0.bits, waves, grid);
   if (lds > 160 * 1024) return 0;
   // buffer-resource offsets are 32-bit: every tile array, scale array and the activations must stay below 2 GiB
   const int esz = act_t == kActF32 ? 4 : 2;

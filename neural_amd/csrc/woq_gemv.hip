@@ -5,19 +5,31 @@
 // (neural_speed/core/layers/ip_fusion_qkv.cpp:22-93, ip_fusion_ffn.cpp:407-457).
 //
 // Shape of the work.  A launch streams `units` stripes (16 output columns x all of K; for the dual SiLU*mul / GELU*mul
-// epilogue a unit is the pair {gate stripe s, up stripe s}).  The grid is sized to the chip (a few workgroups per CU),
+// epilogue a unit is the pair {gate stripe s, up stripe s}).  The grid is sized to the chip (one workgroup per CU),
 // each workgroup owns a contiguous, balanced run of whole units, and its waves split the run's concatenated 1 KiB tiles
-// evenly -- a wave's range may cross stripe boundaries.  So:
-//   * the activations are staged into LDS ONCE per workgroup (not once per stripe) as MFMA-ready fp16 rows (fp32/bf16
-//     inputs split hi = fp16(a), lo = fp16(a - hi) so products are fp32-accurate), with the act-order gather of
-//     ShuffleActivationKBlock (bestla_prologue_a.h:407-422) applied while staging;
-//   * every wave keeps 2 x CH tiles (+ their group scales / zero points) in flight with a double-buffered register
-//     pipeline, so the HBM stream never waits on compute, and no byte is loaded twice;
-//   * per tile: 1 global_load_dwordx4 (16 B/lane, fully coalesced), SPT = KT/32 x {ds_read_b128 of A, 4 v_and_or +
-//     4 v_pk_add_f16 (0x6400 magic dequant -> exact integer fp16), v_mfma_f32_16x16x32_f16}, one fp32 FMA of the group
-//     accumulator by its scale at each group end;
-//   * a wave's partial sums per stripe segment go to an LDS slot; after ONE barrier the workgroup sums the slots of
-//     each stripe in wave order (deterministic, no atomics) and applies the fused epilogue.
+// evenly -- a wave's range may cross stripe boundaries.
+//
+// What the measurements on MI355X (tools/gemv_sweep.py, tools/hbm_probe.hip) shaped:
+//   * a launch of this size is dominated by fixed costs, not arithmetic: everything before the first weight load and
+//     every instruction executed once per launch shows up directly in the time.  So the prologue issues the
+//     activation, scale and weight loads back to back with no waits in between, all bookkeeping is wave-uniform SALU
+//     work (a cursor advanced per tile, the weight / stripe re-derived only at stripe boundaries), and the weight loads
+//     are raw buffer loads that are never predicated -- tiles past a wave's range get an out-of-range offset, which
+//     returns zeros without touching memory -- so every pipeline stage has the same vmcnt footprint and hipcc waits for
+//     exactly one stage instead of draining the queue at control-flow joins;
+//   * the activations are staged into LDS once per workgroup as MFMA-ready fp16 rows (fp32/bf16 inputs split
+//     hi = fp16(a), lo = fp16(a - hi) so the products are fp32-accurate; the act-order gather of
+//     ShuffleActivationKBlock, bestla_prologue_a.h:407-422, is applied while staging), and the workgroup's group scales
+//     loads of each stage are issued with it (one dword per tile: L2-merged 32 B rows);
+//   * wave w owns K-slices w, w + NW, ... (KS = 4 tiles) of every stripe in the run: a pipeline stage is one
+//     (stripe, slice) -- four loads at immediate offsets from one base -- and three stages are in flight per wave
+//     (register ring), the stage being computed the oldest;
+//   * int4 dequantization takes 1 shift + 4 v_and_or + 4 packed fp16 ops per 8 weights (the 0x6400 magic makes
+//     1024 + q and 1024 + 16 q exact fp16 without per-nibble shifts), then one
+//     v_mfma_f32_16x16x32_f16 with the activation rows in the A operand; the group scale multiplies an fp32 group
+//     accumulator once per group, so the weights are dequantized exactly;
+//   * a wave's partial sum per stripe goes to an LDS slot; after ONE barrier the workgroup sums the slots of each
+//     stripe in wave order (deterministic, no atomics) and applies the fused epilogue.
 // HBM-bound by design: weights + scales are read exactly once; the only other traffic is A (L2-resident) once per WG.
 #include <hip/hip_runtime.h>
 
@@ -35,22 +47,14 @@ namespace nad {
 #ifdef NAD_PHASE_TRACE
 constexpr int kTraceSlots = 8, kTraceMaxWg = 16384;
 __device__ unsigned long long nad_trace_buf[kTraceSlots][kTraceMaxWg];
-__device__ int nad_trace_grid;  // record only launches with this many workgroups (0: all)
-#define NAD_TRACE_ON (blockIdx.x < kTraceMaxWg)
-#define NAD_TRACE(slot)                                                                              \
-  do {                                                                                               \
-    if (threadIdx.x == 0 && NAD_TRACE_ON) nad_trace_buf[slot][blockIdx.x] = wall_clock64(); \
+#define NAD_TRACE(slot)                                                                       \
+  do {                                                                                        \
+    if (threadIdx.x == 0 && blockIdx.x < kTraceMaxWg) nad_trace_buf[slot][blockIdx.x] = wall_clock64(); \
   } while (0)
-#define NAD_TRACE_MAX(slot)                                                                             \
-  do {                                                                                                  \
-    if ((threadIdx.x & 63) == 0 && NAD_TRACE_ON)                                            \
-      atomicMax(&nad_trace_buf[slot][blockIdx.x], (unsigned long long)wall_clock64());                  \
-  } while (0)
-#define NAD_TRACE_ID()                                                                                  \
-  do {                                                                                                  \
-    if (threadIdx.x == 0 && NAD_TRACE_ON)                                                               \
-      nad_trace_buf[kTraceSlots - 1][blockIdx.x] =                                                      \
-          (unsigned long long)__smid() | ((unsigned long long)__builtin_amdgcn_s_getreg((3 << 11) | 20) << 32); \
+#define NAD_TRACE_MAX(slot)                                                                               \
+  do {                                                                                                    \
+    if ((threadIdx.x & 63) == 0 && blockIdx.x < kTraceMaxWg)                                              \
+      atomicMax(&nad_trace_buf[slot][blockIdx.x], (unsigned long long)wall_clock64());                    \
   } while (0)
 #else
 #define NAD_TRACE(slot) \
@@ -59,19 +63,9 @@ __device__ int nad_trace_grid;  // record only launches with this many workgroup
 #define NAD_TRACE_MAX(slot) \
   do {                      \
   } while (0)
-#define NAD_TRACE_ID() \
-  do {                 \
-  } while (0)
 #endif
 
-constexpr int kGemvCH = 4;  // tiles per pipeline stage (2 stages in flight per wave)
-
-// a group scale from the dword loaded by load_stage: f32 as is, 16-bit types from the half selected by `sh`
-__device__ __forceinline__ float scale_bits_to_f32(uint32_t x, int st, int sh) {
-  if (st == kScaleF32) return __uint_as_float(x);
-  const uint32_t h = (x >> sh) & 0xFFFFu;
-  return st == kScaleBF16 ? __uint_as_float(h << 16) : f16_bits_to_f32(uint16_t(h));
-}
+constexpr int kOOB = 0x7FFF0000;  // a buffer offset past every resource: the load returns 0 and touches no memory
 
 // virtual stripe -> (weight index, stripe within that weight); all wave-uniform
 __device__ __forceinline__ void vstripe(const GemvArgs& a, int v, int& w, int& s) {
@@ -89,105 +83,144 @@ __device__ __forceinline__ T sel3(int w, T x0, T x1, T x2) {
   return w == 0 ? x0 : (w == 1 ? x1 : x2);
 }
 
-// One pipeline stage: CH weight tiles of this wave's flat range plus the raw group scale / zero-point values they need.
-template <int GPT>
-struct Stage {
-  u4_t b[kGemvCH];
-  uint32_t sc[kGemvCH][GPT];
-  int zp[kGemvCH][GPT];
-};
-
-constexpr int kOOB = 0x7FFF0000;  // a buffer offset past every resource: the load returns 0 and touches no memory
-
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, int bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, bytes, 0x00020000);
 }
 
-// The load cursor: where the next tile / group-scale / zero-point loads of this wave come from.  Everything here is
-// wave-uniform (SGPRs); advancing by one tile is a handful of SALU ops, and the weight / stripe is re-derived only when
-// the cursor crosses a stripe boundary.
-struct LoadCursor {
-  int f, f1;             // flat tile index in the workgroup's run, end of this wave's range
-  int j, t;              // local virtual stripe, tile within it
-  int toff, tstr;        // tile byte offset in the weight's tile array, bytes between consecutive K tiles
-  int soff, gstr;        // scale-row byte offset of the tile's (first) group, bytes between consecutive groups
-  int zoff, zstr;        // the same for the int8 zero points
-  int g0;                // first group of the tile
+// ------------------------------------------------------------------------------------------------ weight stream
+// Wave w owns the K-slices q = w, w + NW, w + 2 NW, ... (KS consecutive tiles each) of EVERY stripe of the workgroup's
+// run, visited stripe-major.  One pipeline stage is one (stripe, slice): KS tile loads at immediate offsets from one
+// stripe base, plus the slice's group scales / zero points -- a few SALU ops per stage, nothing per tile.
+constexpr int KS = 4;
+
+struct StageCursor {
+  int j, q;                      // local virtual stripe, K-slice
+  int s;                         // stripe within its weight
   __amdgpu_buffer_rsrc_t rt, rs, rz;
 };
 
-template <int GPT>
-__device__ __forceinline__ void cursor_seek(const GemvArgs& a, LoadCursor& c, int v0) {
+__device__ __forceinline__ void cursor_stripe(const GemvArgs& a, StageCursor& c, int v0) {
   int w, s;
   vstripe(a, v0 + c.j, w, s);
-  const int nt = a.nt, ng = a.ng;
   const int ns = sel3(w, a.w[0].ns, a.w[1].ns, a.w[2].ns);
-  const int km = sel3(w, a.w[0].kmajor, a.w[1].kmajor, a.w[2].kmajor);
   const int ssz = a.scale_t == kScaleF32 ? 4 : 2;
-  c.rt = rsrc(sel3(w, a.w[0].tiles, a.w[1].tiles, a.w[2].tiles), ns * nt * 1024);
-  c.rs = rsrc(sel3(w, a.w[0].scales, a.w[1].scales, a.w[2].scales), ns * ng * 16 * ssz);
-  c.rz = rsrc(sel3(w, a.w[0].zps, a.w[1].zps, a.w[2].zps), ns * ng * 16);
-  c.toff = int(tile_index(km, ns, nt, s, c.t)) * 1024;
-  c.tstr = km ? ns * 1024 : 1024;
-  c.g0 = GPT == 1 ? (c.t >> a.tpg_shift) : c.t * GPT;
-  const int row = int(scale_row(km, ns, ng, s, c.g0));
-  c.soff = row * 16 * ssz;
-  c.zoff = row * 16;
-  c.gstr = (km ? ns : 1) * 16 * ssz;
-  c.zstr = (km ? ns : 1) * 16;
+  c.s = s;
+  c.rt = rsrc(sel3(w, a.w[0].tiles, a.w[1].tiles, a.w[2].tiles), ns * a.nt * 1024);
+  c.rs = rsrc(sel3(w, a.w[0].scales, a.w[1].scales, a.w[2].scales), ns * a.ng * 16 * ssz);
+  c.rz = rsrc(sel3(w, a.w[0].zps, a.w[1].zps, a.w[2].zps), ns * a.ng * 16);
 }
 
 template <int GPT>
-__device__ __forceinline__ void cursor_next(const GemvArgs& a, LoadCursor& c, int v0) {
-  c.f++;
-  if (++c.t == a.nt) {
-    c.t = 0;
-    c.j++;
-    cursor_seek<GPT>(a, c, v0);
-    return;
-  }
-  c.toff += c.tstr;
-  if constexpr (GPT == 1) {
-    if ((c.t & a.tpg_mask) == 0) {
-      c.g0++;
-      c.soff += c.gstr;
-      c.zoff += c.zstr;
-    }
-  } else {
-    c.g0 += GPT;
-    c.soff += GPT * c.gstr;
-    c.zoff += GPT * c.zstr;
-  }
-}
+struct StageRegs {
+  u4_t b[KS];
+  uint32_t sc[KS][GPT];  // raw scale bits (the dword holding this lane's 16-bit scale, or the f32)
+  int zp[KS][GPT];
+};
 
-// Issue the loads of the next CH tiles: per tile one buffer_load_dwordx4 (nt) of the 1 KiB tile and GPT dword loads of
-// its group scales (+ zero points).  Every load is issued unconditionally -- tiles past the wave's range and groups past
-// K get an out-of-range offset (no memory traffic) -- so every stage has the same vmcnt footprint and the compiler can
-// wait for exactly one stage.  The per-lane work is one v_add per load.
-template <int BITS, int GPT, bool ASYM>
-__device__ __forceinline__ void load_stage(const GemvArgs& a, Stage<GPT>& S, LoadCursor& c, int v0, int lane, int vs) {
+// Issue one stage's loads (never predicated: past-the-end tiles / stages get the out-of-range offset), then advance.
+template <int GPT, bool ASYM>
+__device__ __forceinline__ void load_stage(const GemvArgs& a, StageRegs<GPT>& S, StageCursor& c, int nv, int nsl,
+                                           int wave, int NW, int v0, int lane, int vs) {
+  if (c.j >= nv) {  // past this wave's last stage: the same loads, all out of range, no bookkeeping
 #pragma unroll
-  for (int i = 0; i < kGemvCH; i++) {
-    const bool over = c.f >= c.f1;
-    S.b[i] = __builtin_bit_cast(u4_t, __builtin_amdgcn_raw_buffer_load_b128(c.rt, (over ? kOOB : c.toff) + lane * 16, 0, 2));
+    for (int i = 0; i < KS; i++) {
+      S.b[i] = __builtin_bit_cast(u4_t, __builtin_amdgcn_raw_buffer_load_b128(c.rt, kOOB, 0, 2));
 #pragma unroll
-    for (int q = 0; q < GPT; q++) {
-      const bool gin = !over && (GPT == 1 || c.g0 + q < a.ng);
-#ifdef NAD_EXP_NOSCALE
-      S.sc[i][q] = 0x3C003C00u;
-#else
-      S.sc[i][q] = __builtin_amdgcn_raw_buffer_load_b32(c.rs, (gin ? c.soff + q * c.gstr : kOOB) + vs, 0, 0);
-#endif
-      if constexpr (ASYM) {
-        S.zp[i][q] = int(int8_t(__builtin_amdgcn_raw_buffer_load_b8(c.rz, (gin ? c.zoff + q * c.zstr : kOOB) + (lane & 15), 0, 0)));
-      } else {
-        S.zp[i][q] = 0;
+      for (int g = 0; g < GPT; g++) {
+        S.sc[i][g] = __builtin_amdgcn_raw_buffer_load_b32(c.rs, kOOB, 0, 0);
+        S.zp[i][g] = ASYM ? int(int8_t(__builtin_amdgcn_raw_buffer_load_b8(c.rz, kOOB, 0, 0))) : 0;
       }
     }
-    if (!over) cursor_next<GPT>(a, c, v0);
+    return;
+  }
+  const int nt = a.nt, ng = a.ng;
+  const bool over = false;
+  const int t0 = c.q * KS;
+  const int tb = (c.s * nt + t0) * 1024;
+  const int rowb = a.scale_t == kScaleF32 ? 64 : 32;  // bytes per scale row of 16
+#pragma unroll
+  for (int i = 0; i < KS; i++) {
+    const bool live = !over && t0 + i < nt;
+    S.b[i] = __builtin_bit_cast(u4_t, __builtin_amdgcn_raw_buffer_load_b128(c.rt, (live ? tb + i * 1024 : kOOB) + lane * 16, 0, 2));
+#pragma unroll
+    for (int g = 0; g < GPT; g++) {
+      const int grp = GPT == 1 ? ((t0 + i) >> a.tpg_shift) : (t0 + i) * GPT + g;
+      const bool gl = live && (GPT == 1 || grp < ng);
+      const int row = c.s * ng + grp;
+      S.sc[i][g] = __builtin_amdgcn_raw_buffer_load_b32(c.rs, (gl ? row * rowb : kOOB) + vs, 0, 0);
+      if constexpr (ASYM)
+        S.zp[i][g] = int(int8_t(__builtin_amdgcn_raw_buffer_load_b8(c.rz, (gl ? row * 16 : kOOB) + (lane & 15), 0, 0)));
+      else
+        S.zp[i][g] = 0;
+    }
+  }
+  c.q += NW;
+  if (c.q >= nsl) {
+    c.q = wave;
+    c.j++;
+    if (c.j < nv)
+      cursor_stripe(a, c, v0);
+    else
+      c.rt = c.rs = c.rz = rsrc(a.w[0].tiles, 0);
   }
 }
 
+// ------------------------------------------------------------------------------------------------ dequantization
+// int4: the four nibble pairs of one MFMA step's dword as exact integer fp16 (q - zp).  The 0x6400 magic leaves the
+// ten mantissa bits free, so a nibble can sit at bits 0-3 (value 1024 + q) or bits 4-7 (value 1024 + 16 q):
+//   pair 0 = (w & 0x000F000F) | M          = 1024 + q     -> x - (1024 + 8 + zp)
+//   pair 1 = (w & 0x00F000F0) | M          = 1024 + 16 q  -> x / 16 - (64 + 8 + zp)
+//   pair 2 = ((w >> 8) & 0x000F000F) | M   = 1024 + q
+//   pair 3 = ((w >> 8) & 0x00F000F0) | M   = 1024 + 16 q
+// = 1 shift + 4 v_and_or + 2 v_pk_add_f16 + 2 v_pk_fma_f16 per 8 weights; each pk op rounds an exact value once.
+struct Dq4 {
+  uint32_t m0, m1, mag;  // masks and magic, kept in registers (VOP3 takes no literals on gfx9)
+  h2_t s16;
+};
+
+// (x & m) | c in one VOP3 instruction (hipcc splits it when both constants sit in SGPRs: one constant-bus read on gfx9)
+__device__ __forceinline__ uint32_t and_or(uint32_t x, uint32_t m, uint32_t c) {
+  uint32_t r;
+  asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "s"(m), "v"(c));
+  return r;
+}
+
+__device__ __forceinline__ h8_t dequant4(uint32_t w, const Dq4& q, h2_t c0, h2_t c1) {
+  const uint32_t w8 = w >> 8;
+  const h2_t p0 = as_h2(and_or(w, q.m0, q.mag)) + c0;
+  const h2_t p1 = as_h2(and_or(w, q.m1, q.mag)) * q.s16 + c1;
+  const h2_t p2 = as_h2(and_or(w8, q.m0, q.mag)) + c0;
+  const h2_t p3 = as_h2(and_or(w8, q.m1, q.mag)) * q.s16 + c1;
+  h8_t r;
+  r[0] = p0[0];
+  r[1] = p0[1];
+  r[2] = p1[0];
+  r[3] = p1[1];
+  r[4] = p2[0];
+  r[5] = p2[1];
+  r[6] = p3[0];
+  r[7] = p3[1];
+  return r;
+}
+
+__device__ __forceinline__ h2_t splat(float v) {
+  h2_t r;
+  r[0] = _Float16(v);
+  r[1] = _Float16(v);
+  return r;
+}
+
+// a group scale from the dword load_stage fetched: f32 as is, 16-bit types from the half selected by `sh`
+// (branch-free: the scale type is launch-uniform, selects are cheaper than branches here)
+__device__ __forceinline__ float scale_bits_to_f32(uint32_t x, int st, int sh) {
+  const uint32_t h = (x >> sh) & 0xFFFFu;
+  const float fb = __uint_as_float(h << 16);
+  const float fh = f16_bits_to_f32(uint16_t(h));
+  const float f16or = st == kScaleBF16 ? fb : fh;
+  return st == kScaleF32 ? __uint_as_float(x) : f16or;
+}
+
+// ------------------------------------------------------------------------------------------------ activation staging
 // activation bits -> 8 floats of one staging unit (runtime type: staging runs once per workgroup)
 __device__ __forceinline__ void unit_to_f32(int act_t, uint4 x0, uint4 x1, float (&f)[8]) {
   const uint32_t w[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
@@ -223,7 +256,7 @@ __device__ __forceinline__ void unit_store(char* smem, const float (&f)[8], int 
   if constexpr (HILO != 0) *reinterpret_cast<h8_t*>(smem + (size_t(M + row) * Kp + k) * 2) = lo;
 }
 
-// element-wise staging (act-order gather, unaligned rows, K % 8 != 0): rolled, runs before any weight load
+// element-wise staging (act-order gather, unaligned rows, K % 8 != 0)
 template <int HILO>
 __device__ __forceinline__ void stage_a_slow(const GemvArgs& a, char* smem, int units, int Kp) {
   for (int u = threadIdx.x; u < units; u += blockDim.x) {
@@ -246,12 +279,18 @@ __device__ __forceinline__ void stage_a_slow(const GemvArgs& a, char* smem, int 
   }
 }
 
+// ------------------------------------------------------------------------------------------------ the kernel
+// finer groups carry GPT scale (+ zero-point) registers per tile: those variants run at most 8 waves per workgroup
+template <int GPT>
+constexpr int gemv_max_threads() {
+  return GPT == 1 ? 1024 : 512;
+}
+
 template <int BITS, int HILO, int GPT, bool ASYM>
-__global__ __launch_bounds__(1024) void woq_gemv_kernel(GemvArgs a) {
+__global__ __launch_bounds__(gemv_max_threads<GPT>()) void woq_gemv_kernel(GemvArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int KT = BITS == 4 ? 128 : (BITS == 2 ? 256 : 64);
   constexpr int SPT = KT / 32;
-  constexpr int CH = kGemvCH;
   static_assert(SPT % GPT == 0, "groups must tile the K tile");
   constexpr int SPG = SPT / GPT;  // steps per group when GPT > 1
   const int lane = threadIdx.x & 63;
@@ -259,54 +298,52 @@ __global__ __launch_bounds__(1024) void woq_gemv_kernel(GemvArgs a) {
   const int NW = __builtin_amdgcn_readfirstlane(int(blockDim.x >> 6));
   const int M = a.M, nt = a.nt, Kp = nt * KT;
   const int R = HILO == 0 ? M : 2 * M;
+  const int nsl = (nt + KS - 1) / KS;  // K-slices per stripe
   NAD_TRACE(0);
-  NAD_TRACE_ID();
 
-  // this workgroup's units and this wave's flat tile range (all wave-uniform)
+  // this workgroup's units (wave-uniform)
   const int G = gridDim.x, bid = blockIdx.x;
   const int u0 = int(unsigned(bid) * unsigned(a.units) / unsigned(G));
   const int u1 = int(unsigned(bid + 1) * unsigned(a.units) / unsigned(G));
   const int vpu = a.dual ? 2 : 1;
   const int v0 = u0 * vpu, nv = (u1 - u0) * vpu;
-  const int T = nv * nt;
-  const int f0 = int(unsigned(wave) * unsigned(T) / unsigned(NW));
-  const int f1 = int(unsigned(wave + 1) * unsigned(T) / unsigned(NW));
-
-  // 1) activations -> LDS (once per workgroup) overlapped with the first two weight stages
-  const int a_units = M * (Kp >> 3);
+  const bool idle = wave >= nsl;  // more waves than K-slices: this wave only joins the barriers
+  float* part = reinterpret_cast<float*>(smem + a.part_off);  // [nv][NW][M][16]
   const int bd = blockDim.x;
-  Stage<GPT> S0, S1;
-  LoadCursor lc;
-  lc.f = f0;
-  lc.f1 = f1;
-  {
-    const int j0 = f0 / nt;
-    lc.j = __builtin_amdgcn_readfirstlane(j0);
-    lc.t = __builtin_amdgcn_readfirstlane(f0 - j0 * nt);
-  }
-  cursor_seek<GPT>(a, lc, v0);
-  const int vs = a.scale_t == kScaleF32 ? (lane & 15) * 4 : (lane & 14) * 2;
+
+  // 1) activation loads, then the first three weight stages, back to back
+  const int a_units = M * (Kp >> 3);
+  constexpr int AR = 2;  // activation units per thread issued ahead of the weights
+  const int esz = a.act_t == kActF32 ? 4 : 2;
+  const auto ra = rsrc(a.A, (M - 1) * a.lda * esz + a.K * esz);
+  uint4 x[AR][2];
   if (a.a_fast) {
-    constexpr int AR = 2;  // units per thread issued ahead of the weights
-    const int esz = a.act_t == kActF32 ? 4 : 2;
-    const auto ra = rsrc(a.A, (M - 1) * a.lda * esz + a.K * esz);
-    uint4 x[AR][2];
 #pragma unroll
     for (int q = 0; q < AR; q++) {
       const int u = q * bd + int(threadIdx.x);
       const int row = u / (Kp >> 3), k = (u - row * (Kp >> 3)) * 8;
-#ifdef NAD_EXP_NOA
-      const int off = kOOB;
-#else
       const int off = (u < a_units && k < a.K) ? (row * a.lda + k) * esz : kOOB;
-#endif
       x[q][0] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(ra, off, 0, 0));
       x[q][1] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(ra, off + 16, 0, 0));
     }
-    NAD_TRACE(4);
-    load_stage<BITS, GPT, ASYM>(a, S0, lc, v0, lane, vs);
-    load_stage<BITS, GPT, ASYM>(a, S1, lc, v0, lane, vs);
-    NAD_TRACE(5);
+  }
+  const int vs = a.scale_t == kScaleF32 ? (lane & 15) * 4 : (lane & 14) * 2;
+  StageCursor lc;
+  lc.j = idle ? nv : 0;
+  lc.q = wave;
+  lc.s = 0;
+  lc.rt = rsrc(a.w[0].tiles, 0);  // zero records: every access out of range (idle waves, past-the-end stages)
+  lc.rs = lc.rt;
+  lc.rz = lc.rt;
+  if (!idle && nv > 0) cursor_stripe(a, lc, v0);
+  StageRegs<GPT> S0, S1, S2;
+  load_stage<GPT, ASYM>(a, S0, lc, nv, nsl, wave, NW, v0, lane, vs);
+  load_stage<GPT, ASYM>(a, S1, lc, nv, nsl, wave, NW, v0, lane, vs);
+  load_stage<GPT, ASYM>(a, S2, lc, nv, nsl, wave, NW, v0, lane, vs);
+  NAD_TRACE(4);
+
+  // 2) publish the activations (waits only for the loads issued before the weights)
+  if (a.a_fast) {
 #pragma unroll
     for (int q = 0; q < AR; q++) {
       const int u = q * bd + int(threadIdx.x);
@@ -328,8 +365,6 @@ __global__ __launch_bounds__(1024) void woq_gemv_kernel(GemvArgs a) {
     }
   } else {
     stage_a_slow<HILO>(a, smem, a_units, Kp);
-    load_stage<BITS, GPT, ASYM>(a, S0, lc, v0, lane, vs);
-    load_stage<BITS, GPT, ASYM>(a, S1, lc, v0, lane, vs);
   }
   {
     uint4* zr = reinterpret_cast<uint4*>(smem + size_t(R) * Kp * 2);
@@ -338,8 +373,8 @@ __global__ __launch_bounds__(1024) void woq_gemv_kernel(GemvArgs a) {
   __syncthreads();
   NAD_TRACE(1);
 
-  float* part = reinterpret_cast<float*>(smem + a.part_off);  // [slot][M][16]
-  const int m = lane & 15;   // MFMA A row fed by this lane
+  // 3) the stream
+  const int m = lane & 15;   // MFMA A row fed by this lane (and C column n)
   const int kq = lane >> 4;  // k-quarter of a 32-k step
   const int arow = HILO == 1 ? (m & 7) : m;
   const bool is_lo = HILO == 1 && m >= 8;
@@ -347,122 +382,114 @@ __global__ __launch_bounds__(1024) void woq_gemv_kernel(GemvArgs a) {
   const int row_lo = arow < M ? M + arow : R;
   const char* a_hi = smem + size_t(row_hi) * Kp * 2 + kq * 16;
   const char* a_lo = smem + size_t(row_lo) * Kp * 2 + kq * 16;
-  const h2_t cdef = zp_const(bias_of<BITS>());
   const int ssh = a.scale_t == kScaleF32 ? 0 : (lane & 1) * 16;  // this lane's half of a 16-bit scale pair
+  constexpr int BIAS = BITS == 4 ? 8 : (BITS == 2 ? 2 : 128);
+  Dq4 dq;
+  dq.m0 = __builtin_amdgcn_readfirstlane(a.dq_mask);
+  dq.m1 = dq.m0 << 4;
+  dq.mag = __builtin_amdgcn_readfirstlane(a.dq_magic);
+  dq.s16 = splat(1.f / 16.f);
+  const h2_t zc0 = splat(-(1024.f + BIAS)), zc1 = splat(-(64.f + BIAS));
 
   f4_t acc = {0.f, 0.f, 0.f, 0.f};
-  f4_t accg = {0.f, 0.f, 0.f, 0.f};
+  int cj = idle ? nv : 0, cq = wave;  // compute cursor (wave-uniform)
 
-  // compute cursor (wave-uniform): flat index, local stripe, tile
-  int cf = f0, cj = lc.j, ct = 0;
-  {
-    const int j0 = f0 / nt;
-    cj = __builtin_amdgcn_readfirstlane(j0);
-    ct = __builtin_amdgcn_readfirstlane(f0 - j0 * nt);
-  }
-  auto compute_stage = [&](const Stage<GPT>& S) {
+  auto compute_stage = [&](const StageRegs<GPT>& S) {
+    if (cj >= nv) return;
+    const int t0 = cq * KS;
+    const char* ab = a_hi + t0 * KT * 2;
+    const char* abl = a_lo + t0 * KT * 2;
+    f4_t accg = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int i = 0; i < CH; i++) {
-      if (cf < f1) {
-        const bool seg_end = (ct == nt - 1) || (cf == f1 - 1);
-        const bool tile_gend = GPT == 1 ? (((ct + 1) & a.tpg_mask) == 0 || ct == nt - 1) : true;
-        const int kb = ct * KT * 2;
+    for (int i = 0; i < KS; i++) {
+      if (t0 + i < nt) {
 #pragma unroll
         for (int d = 0; d < SPT; d++) {
-          const int q = GPT == 1 ? 0 : d / SPG;
-          h2_t c2 = cdef;
-          if constexpr (ASYM) c2 = zp_const(bias_of<BITS>() + S.zp[i][q]);
-#ifdef NAD_EXP_NOCOMPUTE
-          if (d == 0) acc[0] += __uint_as_float(S.b[i][0] ^ S.b[i][1] ^ S.b[i][2] ^ S.b[i][3]) + scale_bits_to_f32(S.sc[i][0], a.scale_t, ssh);
-          continue;
-#endif
-          const h8_t bf = dequant_step<BITS>(S.b[i], d, c2);
-          const h8_t af = *reinterpret_cast<const h8_t*>(a_hi + kb + d * 64);
+          const int g = GPT == 1 ? 0 : d / SPG;
+          h8_t bf;
+          if constexpr (BITS == 4) {
+            if constexpr (ASYM) {
+              const float z = float(S.zp[i][g]);
+              bf = dequant4(S.b[i][d], dq, zc0 - splat(z), zc1 - splat(z));
+            } else {
+              bf = dequant4(S.b[i][d], dq, zc0, zc1);
+            }
+          } else {
+            bf = dequant_step<BITS>(S.b[i], d, zp_const(BIAS + S.zp[i][g]));
+          }
+          const h8_t af = *reinterpret_cast<const h8_t*>(ab + i * KT * 2 + d * 64);
           accg = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, bf, accg, 0, 0, 0);
           if constexpr (HILO == 2) {
-            const h8_t afl = *reinterpret_cast<const h8_t*>(a_lo + kb + d * 64);
+            const h8_t afl = *reinterpret_cast<const h8_t*>(abl + i * KT * 2 + d * 64);
             accg = __builtin_amdgcn_mfma_f32_16x16x32_f16(afl, bf, accg, 0, 0, 0);
           }
           if constexpr (GPT > 1) {
             if ((d + 1) % SPG == 0) {
-              acc += accg * scale_bits_to_f32(S.sc[i][q], a.scale_t, ssh);
+              acc += accg * scale_bits_to_f32(S.sc[i][g], a.scale_t, ssh);
               accg = f4_t{0.f, 0.f, 0.f, 0.f};
             }
           }
         }
-        // GPT == 1: the group ends at this tile, or the wave's range ends inside it (a linear partial of the group)
-        if (GPT == 1 && (tile_gend || seg_end)) {
-          acc += accg * scale_bits_to_f32(S.sc[i][0], a.scale_t, ssh);
-          accg = f4_t{0.f, 0.f, 0.f, 0.f};
-        }
-        if (seg_end) {
-          f4_t r = acc;
-          if constexpr (HILO == 1) {
-#pragma unroll
-            for (int x = 0; x < 4; x++) r[x] += __shfl_down(r[x], 32, 64);
+        if constexpr (GPT == 1) {
+          // group end at this tile, or the slice ends inside the group (a linear partial of it)
+          if ((((t0 + i + 1) & a.tpg_mask) == 0) || i == KS - 1 || t0 + i == nt - 1) {
+            acc += accg * scale_bits_to_f32(S.sc[i][0], a.scale_t, ssh);
+            accg = f4_t{0.f, 0.f, 0.f, 0.f};
           }
-          // rows (lane >> 4) * 4 + x live in this lane; slot = local stripe + wave (distinct for all (wave, stripe))
-          float* ps = part + size_t(cj + wave) * M * 16 + (lane & 15);
-#pragma unroll
-          for (int x = 0; x < 4; x++) {
-            const int row = (lane >> 4) * 4 + x;
-            if (row < M && (HILO != 1 || lane < 32)) ps[row * 16] = r[x];
-          }
-          acc = f4_t{0.f, 0.f, 0.f, 0.f};
-        }
-        cf++;
-        if (++ct == nt) {
-          ct = 0;
-          cj++;
         }
       }
     }
+    cq += NW;
+    if (cq >= nsl) {  // this wave's last slice of stripe cj: publish its partial
+      f4_t r = acc;
+      if constexpr (HILO == 1) {
+#pragma unroll
+        for (int xx = 0; xx < 4; xx++) r[xx] += __shfl_down(r[xx], 32, 64);
+      }
+      float* ps = part + (size_t(cj) * NW + wave) * M * 16 + m;
+#pragma unroll
+      for (int xx = 0; xx < 4; xx++) {
+        const int row = (lane >> 4) * 4 + xx;
+        if (row < M && (HILO != 1 || lane < 32)) ps[row * 16] = r[xx];
+      }
+      acc = f4_t{0.f, 0.f, 0.f, 0.f};
+      cq = wave;
+      cj++;
+    }
   };
 
-  bool first = true;
-  while (cf < f1) {
+  while (cj < nv) {
     compute_stage(S0);
-    if (first) NAD_TRACE_MAX(6);
-    first = false;
-    load_stage<BITS, GPT, ASYM>(a, S0, lc, v0, lane, vs);
+    load_stage<GPT, ASYM>(a, S0, lc, nv, nsl, wave, NW, v0, lane, vs);
     compute_stage(S1);
-    load_stage<BITS, GPT, ASYM>(a, S1, lc, v0, lane, vs);
+    load_stage<GPT, ASYM>(a, S1, lc, nv, nsl, wave, NW, v0, lane, vs);
+    compute_stage(S2);
+    load_stage<GPT, ASYM>(a, S2, lc, nv, nsl, wave, NW, v0, lane, vs);
   }
   NAD_TRACE_MAX(2);
   __syncthreads();
 
-  // 2) sum each stripe's slots in wave order and apply the epilogue
+  // 4) sum each stripe's wave slots in wave order and apply the epilogue
   const int nout = (u1 - u0) * M * 16;
+  const int nwl = min(NW, nsl);  // waves that own slices
   for (int o = threadIdx.x; o < nout; o += bd) {
     const int p = o / (M * 16), mm = (o >> 4) % M, nn = o & 15;
     float y[2] = {0.f, 0.f};
 #pragma unroll
     for (int h = 0; h < 2; h++) {
       if (h < vpu) {
-        // waves whose ranges meet stripe j: wave(x) = ((x + 1) * NW - 1) / T holds flat tile x; empty waves skipped
-        const int j = p * vpu + h;
-        const int wlo = int((unsigned(j * nt + 1) * unsigned(NW) - 1u) / unsigned(T));
-        const int whi = int((unsigned((j + 1) * nt) * unsigned(NW) - 1u) / unsigned(T));
-        const float* ps = part + (size_t(j) * M + mm) * 16 + nn;
+        const float* ps = part + (size_t(p * vpu + h) * NW * M + mm) * 16 + nn;
         const size_t wst = size_t(M) * 16;
-        if (T >= NW) {  // no empty waves: four independent LDS reads per step
-          float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-          int w = wlo;
-          for (; w + 3 <= whi; w += 4) {
-            s0 += ps[size_t(w) * wst];
-            s1 += ps[size_t(w + 1) * wst];
-            s2 += ps[size_t(w + 2) * wst];
-            s3 += ps[size_t(w + 3) * wst];
-          }
-          for (; w <= whi; w++) s0 += ps[size_t(w) * wst];
-          y[h] = (s0 + s1) + (s2 + s3);
-        } else {
-          for (int w = wlo; w <= whi; w++) {
-            const bool nonempty =
-                (unsigned(w + 1) * unsigned(T)) / unsigned(NW) > (unsigned(w) * unsigned(T)) / unsigned(NW);
-            if (nonempty) y[h] += ps[size_t(w) * wst];
-          }
+        float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+        int w = 0;
+        for (; w + 3 < nwl; w += 4) {
+          s0 += ps[size_t(w) * wst];
+          s1 += ps[size_t(w + 1) * wst];
+          s2 += ps[size_t(w + 2) * wst];
+          s3 += ps[size_t(w + 3) * wst];
         }
+        for (; w < nwl; w++) s0 += ps[size_t(w) * wst];
+        y[h] = (s0 + s1) + (s2 + s3);
       }
     }
     int wsel, s;
@@ -525,8 +552,8 @@ static hipError_t gemv_launch4(const GemvArgs& a, dim3 g, dim3 b, size_t lds, hi
   return hipGetLastError();
 }
 
-// Instantiated: GPT 1 and 2 (group >= KT/2), sym and asym; GPT 4 (KT/4 groups) sym only.  Finer groups fall back to
-// woq_skinny_kernel (their per-group scale/zero registers would spill).
+// Instantiated: groups of >= KT (GPT 1), KT/2 (GPT 2) and KT/4 (GPT 4), sym and asym.  Finer groups fall back to
+// woq_skinny_kernel.
 template <int BITS, int HILO>
 static hipError_t gemv_launch2(const GemvArgs& a, int gpt, dim3 g, dim3 b, size_t lds, hipStream_t st) {
   constexpr int SPT = (BITS == 4 ? 128 : (BITS == 2 ? 256 : 64)) / 32;
@@ -535,7 +562,9 @@ static hipError_t gemv_launch2(const GemvArgs& a, int gpt, dim3 g, dim3 b, size_
   if (gpt == 2) return a.asym ? gemv_launch4<BITS, HILO, 2, true>(a, g, b, lds, st)
                               : gemv_launch4<BITS, HILO, 2, false>(a, g, b, lds, st);
   if constexpr (SPT % 4 == 0) {
-    if (gpt == 4 && !a.asym) return gemv_launch4<BITS, HILO, 4, false>(a, g, b, lds, st);
+    if (gpt == 4)
+      return a.asym ? gemv_launch4<BITS, HILO, 4, true>(a, g, b, lds, st)
+                    : gemv_launch4<BITS, HILO, 4, false>(a, g, b, lds, st);
   }
   return hipErrorInvalidValue;
 }
@@ -547,16 +576,26 @@ static hipError_t gemv_launch1(const GemvArgs& a, int hilo, int gpt, dim3 g, dim
   return gemv_launch2<BITS, 2>(a, gpt, g, b, lds, st);
 }
 
-size_t gemv_lds_bytes(const GemvArgs& a, int bits, int waves, int grid, int* part_off, int* part_bytes) {
+// LDS layout (and its size) of one launch: activation rows, then the partial-sum slots [nv][waves][M][16]
+size_t gemv_lds_layout(GemvArgs& a, int bits, int waves, int grid) {
   const int KT = bits == 4 ? 128 : (bits == 2 ? 256 : 64);
   const int R = a.act_t == kActF16 ? a.M : 2 * a.M;
   const size_t kp = size_t(a.nt) * KT;
   const size_t abytes = (size_t(R) + 1) * kp * 2;
   const int upw = (a.units + grid - 1) / grid;  // max units per workgroup
-  const size_t slots = size_t(upw) * (a.dual ? 2 : 1) + waves;
-  *part_off = int(abytes);
-  *part_bytes = int(slots * a.M * 16 * 4);
-  return abytes + *part_bytes + (waves + 1) * 4;
+  const size_t nv = size_t(upw) * (a.dual ? 2 : 1);
+  a.part_off = int((abytes + 15) & ~size_t(15));
+  return size_t(a.part_off) + nv * waves * a.M * 16 * 4;
+}
+
+// waves per workgroup: balanced K-slices per wave, at most 16 (8 for groups finer than a K tile)
+int gemv_waves(int bits, int nt, int ng, int bs) {
+  int tpg = 0;
+  const int gpt = gemv_groups_per_tile(bits, nt, ng, bs, &tpg);
+  const int maxw = gpt > 1 ? 8 : 16;
+  const int nsl = (nt + KS - 1) / KS;
+  const int spw = (nsl + maxw - 1) / maxw;  // slices per wave
+  return (nsl + spw - 1) / spw;
 }
 
 int gemv_groups_per_tile(int bits, int nt, int ng, int bs, int* tpg) {
@@ -599,6 +638,7 @@ extern "C" int nad_trace_clock_khz() {
 }
 
 extern "C" int nad_trace_fetch(void* host, size_t bytes, int clear, int grid_filter) {
+  (void)grid_filter;
   const size_t n = sizeof(nad::nad_trace_buf) < bytes ? sizeof(nad::nad_trace_buf) : bytes;
   if (hipDeviceSynchronize() != hipSuccess) return -1;
   if (host && hipMemcpyFromSymbol(host, HIP_SYMBOL(nad::nad_trace_buf), n) != hipSuccess) return -1;
@@ -606,7 +646,6 @@ extern "C" int nad_trace_fetch(void* host, size_t bytes, int clear, int grid_fil
     void* p = nullptr;
     if (hipGetSymbolAddress(&p, HIP_SYMBOL(nad::nad_trace_buf)) != hipSuccess) return -1;
     if (hipMemset(p, 0, sizeof(nad::nad_trace_buf)) != hipSuccess) return -1;
-    if (hipMemcpyToSymbol(HIP_SYMBOL(nad::nad_trace_grid), &grid_filter, sizeof(int)) != hipSuccess) return -1;
     if (hipDeviceSynchronize() != hipSuccess) return -1;
   }
   return 0;

@@ -90,7 +90,8 @@ struct GemvArgs {
   float* aux;
   int ld_aux;
   int part_off;         // LDS byte offset of the partial-sum slots
-  int part_bytes;       // their size (the wave range table follows)
+  uint32_t dq_mask;     // 0x000F000F and 0x64006400: int4 dequant constants, passed in so they stay in registers
+  uint32_t dq_magic;
   SkinnyWeight w[3];
 };
 
@@ -100,7 +101,8 @@ hipError_t launch_skinny(const SkinnyArgs& a, int bits, int act_t, int waves_per
 hipError_t launch_gemm(const GemmArgs& a, int bits, int act_t, hipStream_t stream);
 // groups per K tile the GEMV handles (1, 2, 4, 8) for this geometry, 0 if unsupported; *tpg = tiles per group
 int gemv_groups_per_tile(int bits, int nt, int ng, int bs, int* tpg);
-size_t gemv_lds_bytes(const GemvArgs& a, int bits, int waves, int grid, int* part_off, int* part_bytes);
+size_t gemv_lds_layout(GemvArgs& a, int bits, int waves, int grid);
+int gemv_waves(int bits, int nt, int ng, int bs);
 hipError_t launch_gemv(const GemvArgs& a, int bits, int waves, int grid, size_t lds, hipStream_t stream);
 
 }  // namespace nad

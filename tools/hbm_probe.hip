@@ -106,6 +106,15 @@ int main(int argc, char** argv) {
   const double sizes_mb[] = {8.67, 26.0, 46.6, 23.3, 67.7};
   const int grids[][2] = {{256, 256}, {256, 512}, {256, 1024}, {512, 256}, {512, 512}, {1024, 256}, {2048, 256},
                           {4096, 256}};
+  if (argc > 1 && argv[1][0] == 'o') {  // one configuration (profiling): 8.67 MB, per-wave rows, 256 x 512
+    const size_t bytes = size_t(8.67e6) & ~size_t(1023);
+    const int copies = int(pool / bytes);
+    for (int r = 0; r < 64; r++)
+      hipLaunchKernelGGL(read_kernel<4>, dim3(256), dim3(512), 0, st,
+                         reinterpret_cast<const u4*>(buf + size_t(r % copies) * bytes), bytes / 16, out, 1);
+    CK(hipStreamSynchronize(st));
+    return 0;
+  }
   if (argc > 1) {  // instruction-footprint experiment only
     const size_t bytes = size_t(8.67e6) & ~size_t(1023);
     const int copies = int(pool / bytes);
