@@ -106,6 +106,60 @@ class Runner:
         st.lm_head.forward(self.x, out=self.logits)
 
 
+class ChainRunner:
+    """The decode step as ONE persistent launch (nad_chain_*): every WOQ matmul of the token with its real data
+    dependencies -- x -> RMSNorm -> QKV -> (attention at position 0 is the identity on V) -> O + x -> RMSNorm ->
+    gate/up + SiLU*mul -> down + h -> next layer, then RMSNorm -> lm_head.  RoPE at position 0 is the identity too;
+    only the attention over a KV history (out of scope) is not modelled."""
+
+    def __init__(self, stack, m, device):
+        import torch
+        from neural_amd import bestla
+        f = dict(dtype=torch.float32, device=device)
+        g = torch.Generator(device="cpu").manual_seed(7)
+        self.xs = [(torch.rand((m, HIDDEN), generator=g) - 0.5).to(device), torch.empty((m, HIDDEN), **f)]
+        self.q, self.k, self.v = (torch.empty((m, stack.nq), **f) for _ in range(3))
+        self.h = torch.empty((m, HIDDEN), **f)
+        self.t = torch.empty((m, stack.nf), **f)
+        self.logits = torch.empty((m, stack.nv), **f)
+        ops = []
+        for li, L in enumerate(stack.layers):
+            x, xn = self.xs[li % 2], self.xs[(li + 1) % 2]
+            ops.append(dict(kind=bestla.CHAIN_QKV, w=[L["wq"], L["wk"], L["wv"]], act=x, out=[self.q, self.k, self.v],
+                            norm=True))
+            ops.append(dict(kind=bestla.CHAIN_LINEAR, w=[L["wo"]], act=self.v, out=[self.h], epi=bestla.EPI_RES_ADD,
+                            res=x))
+            ops.append(dict(kind=bestla.CHAIN_GATE_UP, w=[L["w1"], L["w3"]], act=self.h, out=[self.t], norm=True))
+            ops.append(dict(kind=bestla.CHAIN_LINEAR, w=[L["w2"]], act=self.t, out=[xn], epi=bestla.EPI_RES_ADD,
+                            res=self.h))
+        ops.append(dict(kind=bestla.CHAIN_LINEAR, w=[stack.lm_head], act=self.xs[len(stack.layers) % 2],
+                        out=[self.logits], norm=True))
+        self.chain = bestla.Chain(ops, m)
+        self.n_ops = len(ops)
+
+    def step(self, stream=None):
+        self.chain.run(stream=stream)
+
+
+def time_chain(chain_runner, reps, torch):
+    """Average device time of one chain launch (= one decode token), graph-replayed, HIP events on its stream."""
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        chain_runner.step(stream=s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            chain_runner.step(stream=s)
+        g.replay()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        for _ in range(reps):
+            g.replay()
+        e1.record(s)
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps * 1e-3
+
+
 def time_launches(stack, m, reps, torch):
     """Average device time of each WOQ launch shape: `reps` launches cycling through the 32 layers' distinct weights
     (cold: 3.4 GB of weights defeat the 256 MB Infinity Cache) captured in one HIP graph, timed with HIP events on the
@@ -187,6 +241,7 @@ def main():
     ap.add_argument("--prefill-steps", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--per-op", action="store_true", help="headline from per-op launches instead of the decode chain")
     args = ap.parse_args()
 
     import torch
@@ -218,7 +273,7 @@ def main():
             torch.cuda.current_stream().wait_stream(s)
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
-                runner.step()
+                runner.step(**({"stream": torch.cuda.current_stream()} if isinstance(runner, ChainRunner) else {}))
             fn = g.replay
         for _ in range(warmup):
             fn()
@@ -234,10 +289,23 @@ def main():
             dt = float(t.item())
         return dt
 
-    # ---- decode (headline): M = 1
-    dec = Runner(stack, 1, dist, "cuda")
+    # ---- decode (headline): M = 1.  One GPU: the whole token as one persistent chain launch (nad_chain_*);
+    # tensor parallel: per-op launches with an RCCL all-reduce after O and down.
     use_graph = world == 1 and not args.no_graph
-    dt = timed(dec, args.steps, args.warmup, use_graph)
+    chain = None
+    chain_tok_s = None
+    if world == 1 and not args.per_op:
+        chain = ChainRunner(stack, 1, "cuda")
+        dt_chain = timed(chain, args.steps, args.warmup, use_graph)
+        assert chain.chain.status() == 0, "decode chain hand-off timed out"
+        chain_tok_s = args.steps / dt_chain
+    dec = Runner(stack, 1, dist, "cuda")
+    dt_op = timed(dec, args.steps, args.warmup, use_graph)
+    per_op_tok_s = args.steps / dt_op
+    # the headline is the faster of the two complete decode paths (both run every WOQ matmul of the token)
+    if chain is not None and dt_chain >= dt_op:
+        chain = None
+    dt = dt_chain if chain is not None else dt_op
     tok_s = args.steps / dt
 
     # ---- prefill: M = 2048 tokens
@@ -246,13 +314,22 @@ def main():
     pflops = sum(f * c for _, _, f, c in stack.launches(2048)) * world  # whole-job FLOPs
     prefill_tflops = pflops * args.prefill_steps / pdt / 1e12
 
-    # ---- roofline of the dominant kernel (decode GEMV, woq_skinny_kernel) on this rank's shards
+    # ---- roofline of the dominant kernel on this rank's shards.  Algorithmic bytes per SURVEY.md §8(d)
+    # (bestla_benchmark.cpp:817-823): packed weights + scales + activations in/out, for every WOQ matmul of the token.
     per = time_launches(stack, 1, 64, torch)
     L1 = stack.launches(1)
     tot_bytes = sum(b * c for _, b, _, c in L1)
-    tot_time = sum(per[n] * c for n, _, _, c in L1)
-    launches = sum(c for *_, c in L1)
-    achieved = tot_bytes / tot_time / 1e9
+    per_op_time = sum(per[n] * c for n, _, _, c in L1)
+    n_per_op_launches = sum(c for *_, c in L1)
+    if chain is not None:
+        # one woq_chain_kernel launch = one token: its average duration, HIP events on the stream it runs on
+        chain_us = time_chain(chain, 20, torch)
+        kernel, bytes_per_launch, launch_s = "woq_chain_kernel (whole decode step, one persistent launch)", tot_bytes, \
+            chain_us
+    else:
+        kernel, bytes_per_launch, launch_s = "woq_gemv_kernel (decode GEMV, one launch per matmul)", \
+            tot_bytes / n_per_op_launches, per_op_time / n_per_op_launches
+    achieved = bytes_per_launch / launch_s / 1e9
     traffic = None
     pmc = os.path.join(REPO, "profiles", "pmc_traffic.json")
     if os.path.exists(pmc):
@@ -276,17 +353,23 @@ def main():
             "vs_baseline": None,
             "dtype": "f16",
             "data": "synthetic: random int4 codes + fp16 group scales U[0.001,0.01] in Llama-2-7B shapes (no checkpoint)",
-            "config": {"workload": "Llama-2-7B int4-g128 sym decode linear stack, M=1 (32 x [QKV, O, gate/up+SiLU*mul, "
+            "config": {"workload": "Llama-2-7B int4-g128 sym decode step, M=1: 32 x [RMSNorm, fused QKV, O + residual, "
+                                   "RMSNorm, gate/up + SiLU*mul, down + residual] + RMSNorm + lm_head, fp32 activations "
+                                   "(attention at position 0 = V)" if chain is not None else
+                                   "Llama-2-7B int4-g128 sym decode linear stack, M=1 (32 x [QKV, O, gate/up+SiLU*mul, "
                                    "down] + lm_head), fp32 activations", "group_size": GROUP, "batch": 1,
-                       "tp": world, "parallelism": f"tp{world}", "cuda_graph": use_graph},
+                       "tp": world, "parallelism": f"tp{world}", "cuda_graph": use_graph,
+                       "decode_path": "chain (1 launch per token)" if chain is not None else "per-op launches"},
             "prefill_tflops": round(prefill_tflops, 2),
             "prefill_ms_per_2048_tokens": round(pdt / args.prefill_steps * 1e3, 3),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
-                         "kernel": "woq_gemv_kernel (decode GEMV, persistent stripe stream)",
-                         "bytes_per_launch": int(tot_bytes / launches),
-                         "avg_launch_us": round(tot_time / launches * 1e6, 3),
-                         "per_shape_us": {k: round(v * 1e6, 3) for k, v in per.items()}},
+                         "kernel": kernel, "bytes_per_launch": int(bytes_per_launch),
+                         "avg_launch_us": round(launch_s * 1e6, 3)},
+            "decode_chain_tokens_per_s": None if chain_tok_s is None else round(chain_tok_s, 2),
+            "per_op_launches": {"tokens_per_s": round(per_op_tok_s, 2),
+                                "gemv_achieved_GBps": round(tot_bytes / per_op_time / 1e9, 1),
+                                "per_shape_us": {k: round(v * 1e6, 3) for k, v in per.items()}},
             "prefill_roofline": {"bound": "mfma", "achieved": round(prefill_tflops / world, 2),
                                  "peak": MFMA_F16_PEAK_TFLOPS, "unit": "TFLOP/s",
                                  "frac": round(prefill_tflops / world / MFMA_F16_PEAK_TFLOPS, 4)},

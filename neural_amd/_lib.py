@@ -73,7 +73,18 @@ SIGNATURES = {
     "nad_synthetic_weight": (_i, [_p, _p, _sz, _i, _i, _i, _i, _i, _i, _u64, _p]),
     "nad_synthetic_weight_size": (_sz, [_i, _i, _i, _i, _i, _i]),
     "nad_device_unpack_fp32": (_i, [_p, _p, _p]),
+    "nad_chain_create": (_p, [_p, _i, _i]),
+    "nad_chain_run": (_i, [_p, _p]),
+    "nad_chain_status": (_i, [_p]),
+    "nad_chain_destroy": (None, [_p]),
 }
+
+
+class ChainOp(C.Structure):
+    """Mirror of include/neural_amd.h's nad_chain_op."""
+    _fields_ = [("kind", _i), ("w", _p * 3), ("act", _p), ("act_dtype", _i), ("lda", _i), ("out", _p * 3),
+                ("ldo", _i * 3), ("epi", _i), ("bias", _p), ("bias_ld", _i), ("res", _p), ("ld_res", _i),
+                ("aux", _p), ("ld_aux", _i), ("norm", _i), ("norm_eps", C.c_float), ("norm_w", _p)]
 
 
 class NativeLibraryMissing(RuntimeError):

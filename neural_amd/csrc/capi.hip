@@ -14,6 +14,7 @@
 
 #include "../../include/neural_amd.h"
 #include "btla_format.h"
+#include "woq_chain.h"
 #include "woq_kernels.h"
 
 using namespace nad;
@@ -295,10 +296,10 @@ static int device_cus() {
 // The persistent stripe-stream GEMV (woq_gemv.hip) when the launch fits it: M <= 16, the staged activations fit LDS,
 // the group size tiles the K tile, and all weights share one act-order LUT.  Returns 1 if launched, 0 if not eligible,
 // -1 on a launch error.
-static int try_gemv(const void* act, int act_t, int lda, int m, int k, int nw, const DeviceWeight* const* ws,
-                    float* const* outs, const int* ldos, int epi, const float* bias, int bias_ld, const float* res,
-                    int ld_res, float* aux, int ld_aux, hipStream_t st) {
-  if (env_int("NAD_GEMV_DISABLE", 0)) return 0;
+// Fill the GemvArgs of one decode op; returns 1 when the stripe-stream GEMV handles it, 0 when not eligible.
+static int prepare_gemv(GemvArgs& a, int& waves, int& grid, int& gpt_out, const void* act, int act_t, int lda, int m,
+                        int k, int nw, const DeviceWeight* const* ws, float* const* outs, const int* ldos, int epi,
+                        const float* bias, int bias_ld, const float* res, int ld_res, float* aux, int ld_aux) {
   const DeviceWeight& w0 = *ws[0];
   for (int i = 1; i < nw; i++)
     if (ws[i]->shuffle != w0.shuffle || ws[i]->nt != w0.nt || ws[i]->ng != w0.ng || ws[i]->bits != w0.bits ||
@@ -309,7 +310,7 @@ static int try_gemv(const void* act, int act_t, int lda, int m, int k, int nw, c
   int tpg = 0;
   const int gpt = gemv_groups_per_tile(w0.bits, w0.nt, w0.ng, w0.blocksize, &tpg);
   if (gpt == 0 || (gpt >= 4 && w0.asym)) return 0;
-  GemvArgs a{};
+  a = GemvArgs{};
   a.A = act;
   a.lda = lda;
   a.M = m;
@@ -340,9 +341,9 @@ static int try_gemv(const void* act, int act_t, int lda, int m, int k, int nw, c
   for (int i = nw; i < 3; i++) a.w[i] = a.w[0];
   a.units = a.dual ? ws[0]->ns : stripes;
   const int wpc = std::max(1, env_int("NAD_GEMV_WPC", 1));
-  int grid = std::max(1, std::min(a.units, device_cus() * wpc));
+  grid = std::max(1, std::min(a.units, device_cus() * wpc));
   if (env_int("NAD_GEMV_GRID", 0) > 0) grid = std::min(a.units, env_int("NAD_GEMV_GRID", 0));  // tests / tuning
-  int waves = gemv_waves(w0.bits, w0.nt, w0.ng, w0.blocksize);
+  waves = gemv_waves(w0.bits, w0.nt, w0.ng, w0.blocksize);
   if (env_int("NAD_GEMV_WAVES", 0) > 0) waves = std::min(gpt > 1 ? 8 : 16, env_int("NAD_GEMV_WAVES", 0));
   a.dq_mask = 0x000F000Fu;
   a.dq_magic = 0x64006400u;
@@ -353,7 +354,22 @@ static int try_gemv(const void* act, int act_t, int lda, int m, int k, int nw, c
   if (uint64_t(m) * lda * esz >= (1ull << 30)) return 0;
   for (int i = 0; i < nw; i++)
     if (uint64_t(ws[i]->ns) * ws[i]->nt * 1024 >= (1ull << 30)) return 0;
-  hipError_t e = launch_gemv(a, w0.bits, waves, grid, lds, st);
+  gpt_out = gpt;
+  (void)lds;
+  return 1;
+}
+
+static int try_gemv(const void* act, int act_t, int lda, int m, int k, int nw, const DeviceWeight* const* ws,
+                    float* const* outs, const int* ldos, int epi, const float* bias, int bias_ld, const float* res,
+                    int ld_res, float* aux, int ld_aux, hipStream_t st) {
+  if (env_int("NAD_GEMV_DISABLE", 0)) return 0;
+  GemvArgs a{};
+  int waves = 0, grid = 0, gpt = 0;
+  if (!prepare_gemv(a, waves, grid, gpt, act, act_t, lda, m, k, nw, ws, outs, ldos, epi, bias, bias_ld, res, ld_res,
+                    aux, ld_aux))
+    return 0;
+  const size_t lds = gemv_lds_layout(a, ws[0]->bits, waves, grid);
+  hipError_t e = launch_gemv(a, ws[0]->bits, waves, grid, lds, st);
   if (e != hipSuccess) {
     set_err("gemv kernel launch failed: %s", hipGetErrorString(e));
     return -1;
@@ -552,6 +568,132 @@ extern "C" int nad_device_ffn_forward(const void* act, int act_dtype, const void
                       st);
   }
   return run_gemm(tmp2, kActF32, fmid, m, fmid, *w2, out, fout, kEpiNone, nullptr, 0, nullptr, 0, nullptr, 0, st);
+}
+
+// ------------------------------------------------------------------------------------------------ decode chain
+// A decode step's WOQ matmuls as one persistent launch (woq_chain.hip).  Each op is what nad_device_forward /
+// nad_device_qkv_forward / nad_device_ffn_gate_up would run at M <= 16; ops execute in order and every op may read
+// any earlier op's output.  All ops must be int4, groups of >= 128 that tile K (one group per K tile or coarser),
+// no act-order shuffle, stripe-major layout, one activation dtype.
+struct NadChain {
+  GemvArgs* dev_ops = nullptr;
+  unsigned* ctl = nullptr;  // [0, grid) per-workgroup arrival flags, [1024] status
+  int n_ops = 0, waves = 0, grid = 0, hilo = 0, asym = 0;
+  size_t lds = 0;
+};
+
+extern "C" void* nad_chain_create(const nad_chain_op* ops, int n_ops, int m) {
+  if (!ops || n_ops <= 0 || m <= 0 || m > 8) {
+    set_err("nad_chain_create: need 1 <= m <= 8 and at least one op");
+    return nullptr;
+  }
+  std::vector<GemvArgs> host(static_cast<size_t>(n_ops));
+  const int grid = std::min(device_cus(), 256);  // the flag sweep covers 64 lanes x 4 flags
+  int waves = 0, act_t = ops[0].act_dtype, asym = -1;
+  for (int i = 0; i < n_ops; i++) {
+    const nad_chain_op& o = ops[i];
+    const int nw = o.kind == NAD_CHAIN_QKV ? 3 : (o.kind == NAD_CHAIN_GATE_UP ? 2 : 1);
+    const DeviceWeight* ws[3] = {nullptr, nullptr, nullptr};
+    for (int j = 0; j < nw; j++)
+      if (!(ws[j] = as_weight(o.w[j]))) return nullptr;
+    const DeviceWeight& w0 = *ws[0];
+    if (w0.bits != 4 || w0.has_shuffle || w0.kmajor || w0.blocksize % 128 != 0 || o.act_dtype != act_t ||
+        (asym >= 0 && asym != w0.asym)) {
+      set_err("nad_chain_create: op %d is not a chain op (int4, group >= 128, no shuffle, one act dtype/symmetry)", i);
+      return nullptr;
+    }
+    asym = w0.asym;
+    int epi = o.epi;
+    if (o.kind == NAD_CHAIN_GATE_UP && epi != kEpiSiluMul && epi != kEpiGeluMul) epi = kEpiSiluMul;
+    float* outs[3] = {o.out[0], o.out[1], o.out[2]};
+    int ldos[3] = {o.ldo[0], o.ldo[1], o.ldo[2]};
+    if (o.kind == NAD_CHAIN_GATE_UP) {
+      outs[1] = outs[0];
+      ldos[1] = ldos[0];
+    }
+    int wv = 0, gr = 0, gpt = 0;
+    GemvArgs& a = host[size_t(i)];
+    if (!prepare_gemv(a, wv, gr, gpt, o.act, o.act_dtype, o.lda, m, w0.k, nw, ws, outs, ldos, epi, o.bias,
+                      o.bias_ld, o.res, o.ld_res, o.aux, o.ld_aux) ||
+        gpt != 1) {
+      set_err("nad_chain_create: op %d not eligible for the stripe stream", i);
+      return nullptr;
+    }
+    a.nwa = wv;
+    a.norm = o.norm;
+    a.norm_eps = o.norm_eps;
+    a.norm_w = o.norm_w;
+    waves = std::max(waves, wv);
+  }
+  waves = std::max(waves, m);
+  if (waves > 12) {  // woq_chain_kernel is built for <= 768 threads (168 VGPRs, no spills)
+    set_err("nad_chain_create: %d waves per workgroup exceed the chain kernel's 12", waves);
+    return nullptr;
+  }
+  size_t lds = 80 * 1024 + 16;  // > half the LDS: exactly one workgroup per CU, all co-resident
+  for (int i = 0; i < n_ops; i++) {
+    GemvArgs& a = host[size_t(i)];
+    const int ku = a.nt * 128 / 8;
+    if (m * ku > 3 * waves * 64) {
+      set_err("nad_chain_create: op %d activations exceed the staging registers (m * K too large)", i);
+      return nullptr;
+    }
+    lds = std::max(lds, chain_lds_layout(a, waves, grid));
+  }
+  if (lds > 160 * 1024) {
+    set_err("nad_chain_create: LDS need %zu exceeds 160 KiB", lds);
+    return nullptr;
+  }
+  NadChain* c = new NadChain();
+  c->n_ops = n_ops;
+  c->waves = waves;
+  c->grid = grid;
+  c->lds = lds;
+  c->hilo = act_t == kActF16 ? 0 : 1;
+  c->asym = asym;
+  if (hipMalloc(&c->dev_ops, sizeof(GemvArgs) * size_t(n_ops)) != hipSuccess ||
+      hipMalloc(&c->ctl, 8192) != hipSuccess ||
+      hipMemcpy(c->dev_ops, host.data(), sizeof(GemvArgs) * size_t(n_ops), hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemset(c->ctl, 0, 8192) != hipSuccess) {
+    set_err("nad_chain_create: device allocation failed");
+    if (c->dev_ops) (void)hipFree(c->dev_ops);
+    if (c->ctl) (void)hipFree(c->ctl);
+    delete c;
+    return nullptr;
+  }
+  return c;
+}
+
+extern "C" int nad_chain_run(void* chain, void* queue) {
+  NadChain* c = static_cast<NadChain*>(chain);
+  if (!c) return -1;
+  hipStream_t st = static_cast<hipStream_t>(queue);
+  if (hipMemsetAsync(c->ctl, 0, sizeof(unsigned) * size_t(c->grid), st) != hipSuccess) {
+    set_err("nad_chain_run: flag reset failed");
+    return -1;
+  }
+  hipError_t e = launch_chain(c->dev_ops, c->n_ops, c->hilo, c->asym, c->waves, c->grid, c->lds, c->ctl, c->ctl + 1024, env_int("NAD_CHAIN_PRE", 1), st);
+  if (e != hipSuccess) {
+    set_err("nad_chain_run: launch failed: %s", hipGetErrorString(e));
+    return -1;
+  }
+  return 0;
+}
+
+extern "C" int nad_chain_status(void* chain) {
+  NadChain* c = static_cast<NadChain*>(chain);
+  if (!c) return -1;
+  unsigned s = 0;
+  if (hipMemcpy(&s, c->ctl + 1024, sizeof(unsigned), hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  return int(s);
+}
+
+extern "C" void nad_chain_destroy(void* chain) {
+  NadChain* c = static_cast<NadChain*>(chain);
+  if (!c) return;
+  (void)hipFree(c->dev_ops);
+  (void)hipFree(c->ctl);
+  delete c;
 }
 
 // ------------------------------------------------------------------------------------------------ synthetic weights
