@@ -417,6 +417,59 @@ static int run_skinny(const void* act, int act_t, int lda, int m, int k, int nw,
   return 0;
 }
 
+// Grow-only device scratch for the prefill GEMM's fp16 copy of the activations (never freed: one per process, sized
+// by the largest prefill).  Growing is refused while the stream is being captured into a graph.
+static void* scratch(size_t bytes, hipStream_t st) {
+  static std::mutex mu;
+  static void* buf = nullptr;
+  static size_t cap = 0;
+  std::lock_guard<std::mutex> lk(mu);
+  if (bytes <= cap) return buf;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+  if (hipStreamSynchronize(st) != hipSuccess) return nullptr;
+  if (buf) (void)hipFree(buf);
+  buf = nullptr;
+  cap = 0;
+  if (hipMalloc(&buf, bytes) != hipSuccess) {
+    buf = nullptr;
+    return nullptr;
+  }
+  cap = bytes;
+  return buf;
+}
+
+// The pipelined prefill GEMM (woq_gemm2.hip) when eligible: 1 launched, 0 not eligible, -1 launch error.
+static int try_gemm2(const GemmArgs& a, const void* act, int act_t, int lda, int m, int k, const DeviceWeight& w,
+                     hipStream_t st) {
+  if (env_int("NAD_GEMM2_DISABLE", 0)) return 0;
+  const int tpg = w.blocksize / 128;
+  if (w.bits != 4 || w.kmajor || w.blocksize % 128 != 0 || (tpg & (tpg - 1)) != 0 || m < 32) return 0;
+  const int kp = w.nt * 128;
+  const _Float16* a16 = nullptr;
+  int lda16 = kp;
+  if (act_t == kActF16 && !w.shuffle && k == kp && reinterpret_cast<uintptr_t>(act) % 16 == 0 &&
+      (size_t(lda) * 2) % 16 == 0) {
+    a16 = static_cast<const _Float16*>(act);
+    lda16 = lda;
+  } else {
+    _Float16* buf = static_cast<_Float16*>(scratch(size_t(m) * kp * 2, st));
+    if (!buf) return 0;
+    hipError_t e = launch_cvt_act(act, act_t, lda, m, k, kp, w.shuffle, buf, st);
+    if (e != hipSuccess) {
+      set_err("activation conversion launch failed: %s", hipGetErrorString(e));
+      return -1;
+    }
+    a16 = buf;
+  }
+  hipError_t e = launch_gemm2(a, a16, lda16, st);
+  if (e != hipSuccess) {
+    set_err("gemm2 kernel launch failed: %s", hipGetErrorString(e));
+    return -1;
+  }
+  return 1;
+}
+
 static int run_gemm(const void* act, int act_t, int lda, int m, int k, const DeviceWeight& w, float* out, int ldo,
                     int epi, const float* bias, int bias_ld, const float* res, int ld_res, const float* aux,
                     int ld_aux, hipStream_t st) {
@@ -433,6 +486,8 @@ static int run_gemm(const void* act, int act_t, int lda, int m, int k, const Dev
   a.aux = aux;
   a.ld_aux = ld_aux;
   a.w = view(w, out, ldo, bias, bias_ld);
+  const int g2 = try_gemm2(a, act, act_t, lda, m, k, w, st);
+  if (g2 != 0) return g2 < 0 ? -1 : 0;
   hipError_t e = launch_gemm(a, w.bits, act_t, st);
   if (e != hipSuccess) {
     set_err("gemm kernel launch failed: %s", hipGetErrorString(e));

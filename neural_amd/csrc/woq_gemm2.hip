@@ -1,0 +1,292 @@
+// woq_gemm2.hip -- the prefill (M > 16) weight-only-quantized GEMM for gfx950, int4, groups of 128 * 2^j.
+//
+// Replaces LauncherBase::gemm / run_block + WeightKBlockNInteger::getFpWeight + the AMX / AVX512 GEMM cores
+// (bestla/bestla/bestla_wrapper.h:481-542, bestla_prologue_b.h:732-838) for prefill-sized M.
+//
+// Structure (one workgroup per CU, 512 threads = 8 waves as 4 (M) x 2 (N), block tile 256 x 128, K step = one
+// 128-deep int4 tile):
+//   * A is fp16 [M][Kp] (a one-pass conversion of the fp32 / bf16 activations, nad_cvt_act_kernel, or the caller's
+//     fp16 rows) and streams global -> LDS by LDS-DMA (global_load_lds_dwordx4) into a double buffer, one K step
+//     ahead; the 16-B chunks of a 256-B row are XOR-swizzled by (row & 15) through the SOURCE address (the LDS image
+//     of a DMA is lane-linear) so the MFMA fragment reads (16 rows x one chunk) are bank-conflict free;
+//   * B needs no LDS: the tile layout (woq_layout.h) is already the v_mfma_f32_16x16x32_f16 B-fragment order, so each
+//     wave loads its 4 stripes' 1 KiB tiles of the NEXT K step straight into registers (with their scales / zero
+//     points) while it computes the current one, and dequantizes with the 0x6400 magic number into exact fp16
+//     integers (q - zp);
+//   * one fp32 group accumulator per output fragment is scaled into the result at every group end, so weights are
+//     applied exactly as w = (q - zp) * s (fp32 scale multiply), the only rounding being A -> fp16 (as the reference's
+//     own BF16/FP16 AMX cores round A);
+//   * workgroups are remapped so that the 8 M tiles of one N tile run on one XCD (B re-reads hit that XCD's L2).
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "woq_device.h"
+#include "woq_kernels.h"
+
+namespace nad {
+namespace g2 {
+
+constexpr int BM = 256, BN = 128, KT = 128, ROWB = KT * 2;  // ROWB: bytes of one A row slice in LDS
+constexpr int ABUF = BM * ROWB;                              // one A buffer: 64 KiB
+
+__device__ __forceinline__ uint32_t and_or(uint32_t x, uint32_t m, uint32_t c) {
+  uint32_t r;
+  asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "s"(m), "v"(c));
+  return r;
+}
+
+__device__ __forceinline__ h2_t splat(float v) {
+  h2_t r;
+  r[0] = _Float16(v);
+  r[1] = _Float16(v);
+  return r;
+}
+
+__device__ __forceinline__ h8_t dequant4(uint32_t w, uint32_t m0, uint32_t m1, uint32_t mag, h2_t s16, h2_t c0,
+                                         h2_t c1) {
+  const uint32_t w8 = w >> 8;
+  const h2_t p0 = as_h2(and_or(w, m0, mag)) + c0;
+  const h2_t p1 = as_h2(and_or(w, m1, mag)) * s16 + c1;
+  const h2_t p2 = as_h2(and_or(w8, m0, mag)) + c0;
+  const h2_t p3 = as_h2(and_or(w8, m1, mag)) * s16 + c1;
+  h8_t r;
+  r[0] = p0[0];
+  r[1] = p0[1];
+  r[2] = p1[0];
+  r[3] = p1[1];
+  r[4] = p2[0];
+  r[5] = p2[1];
+  r[6] = p3[0];
+  r[7] = p3[1];
+  return r;
+}
+
+// LDS-DMA of one K step of A: 256 rows x 256 B = 64 one-KiB pieces, 8 per wave; lane l of piece p fills LDS chunk
+// (l & 15) of row 4p + (l >> 4) with source chunk (l & 15) ^ (row & 15).  Rows past M re-read row M-1 (their
+// outputs are never stored).
+__device__ __forceinline__ void stage_a(const _Float16* A16, int lda16, int M, int m0, int t, char* lbuf, int wave,
+                                        int lane) {
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const int p = wave * 8 + i;
+    const int row = p * 4 + (lane >> 4);
+    const int grow = min(m0 + row, M - 1);
+    const int sch = (lane & 15) ^ (row & 15);
+    const _Float16* src = A16 + size_t(grow) * lda16 + size_t(t) * KT + sch * 8;
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                     (__attribute__((address_space(3))) void*)(lbuf + p * 1024), 16, 0, 0);
+  }
+}
+
+template <bool ASYM, bool TPG1>
+__global__ __launch_bounds__(512, 1) void woq_gemm2_kernel(GemmArgs a, const _Float16* __restrict__ A16, int lda16) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));
+  const int wm = wave >> 1, wn = wave & 1;
+  const SkinnyWeight& W = a.w;
+  const int M = a.M, nt = W.nt, ng = W.ng, ns = W.ns;
+  const int tpg = W.bs / KT;  // tiles per group (power of two, host-checked)
+
+  // XCD-aware remap: the nbm M tiles of one N tile are consecutive on one XCD
+  const int nbm = (M + BM - 1) / BM;
+  const int nbn = (ns + 7) / 8;
+  const int nwg = nbm * nbn;
+  int bid = blockIdx.x;
+  {
+    const int q = nwg / 8, r = nwg % 8, x = bid % 8, o = bid / 8;
+    bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + o;
+  }
+  const int bn = bid / nbm, bm = bid % nbm;
+  const int m0 = bm * BM;
+  const int s0 = bn * 8 + wn * 4;  // this wave's first stripe
+  const int nl = lane & 15;
+
+  // per-stripe bases (clamped stripes past N read stripe ns-1: their columns are never stored)
+  const u4_t* tl[4];
+  int srow[4];
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    const int s = min(s0 + j, ns - 1);
+    tl[j] = reinterpret_cast<const u4_t*>(W.tiles) + size_t(s) * nt * 64 + lane;
+    srow[j] = s * ng;
+  }
+  auto load_b = [&](int t, u4_t (&b)[4], float (&sc)[4], int (&zp)[4]) {
+    const int g = t / tpg;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      b[j] = __builtin_nontemporal_load(tl[j] + size_t(t) * 64);
+      const size_t si = size_t(srow[j] + g) * 16 + nl;
+      sc[j] = load_scale(W.scales, si, a.scale_t);
+      zp[j] = ASYM ? int(W.zps[si]) : 0;
+    }
+  };
+
+  f4_t acc[4][4], accg[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; i++)
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      acc[i][j] = f4_t{0.f, 0.f, 0.f, 0.f};
+      accg[i][j] = f4_t{0.f, 0.f, 0.f, 0.f};
+    }
+
+  u4_t bc[4], bx[4];
+  float scc[4], scx[4];
+  int zc[4], zx[4];
+  stage_a(A16, lda16, M, m0, 0, smem, wave, lane);
+  load_b(0, bc, scc, zc);
+  __syncthreads();
+
+  const uint32_t m0k = 0x000F000Fu, m1k = 0x00F000F0u, mag = 0x64006400u;
+  const h2_t s16 = splat(1.f / 16.f);
+  const h2_t zc0 = splat(-(1024.f + 8.f)), zc1 = splat(-(64.f + 8.f));
+  // this lane's A fragment rows (i = 0..3) and their XOR key
+  const int rbase = wm * 64 + nl;
+  const int kq = lane >> 4;
+  const f4_t zero = {0.f, 0.f, 0.f, 0.f};
+
+  for (int t = 0; t < nt; t++) {
+    char* cur = smem + (t & 1) * ABUF;
+    if (t + 1 < nt) {
+      stage_a(A16, lda16, M, m0, t + 1, smem + ((t + 1) & 1) * ABUF, wave, lane);
+      load_b(t + 1, bx, scx, zx);
+    }
+    const bool gstart = TPG1 || (t & (tpg - 1)) == 0;
+    const bool gend = TPG1 || ((t + 1) & (tpg - 1)) == 0 || t == nt - 1;
+#pragma unroll
+    for (int d = 0; d < 4; d++) {
+      h8_t bf[4];
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        if constexpr (ASYM) {
+          const float z = float(zc[j]);
+          bf[j] = dequant4(bc[j][d], m0k, m1k, mag, s16, zc0 - splat(z), zc1 - splat(z));
+        } else {
+          bf[j] = dequant4(bc[j][d], m0k, m1k, mag, s16, zc0, zc1);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        const int r = rbase + i * 16;
+        const int ch = (d * 4 + kq) ^ (r & 15);
+        const h8_t af = *reinterpret_cast<const h8_t*>(cur + r * ROWB + ch * 16);
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          if (d == 0 && gstart)
+            accg[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, bf[j], zero, 0, 0, 0);
+          else
+            accg[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, bf[j], accg[i][j], 0, 0, 0);
+        }
+      }
+    }
+    if (gend) {
+#pragma unroll
+      for (int j = 0; j < 4; j++)
+#pragma unroll
+        for (int i = 0; i < 4; i++) acc[i][j] += accg[i][j] * scc[j];
+    }
+    __syncthreads();  // next A buffer landed (vmcnt(0)), current buffer free for the step after
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      bc[j] = bx[j];
+      scc[j] = scx[j];
+      zc[j] = zx[j];
+    }
+  }
+
+  // epilogue: C fragment (i, j): row = m0 + wm*64 + i*16 + (lane>>4)*4 + rr, col = (s0+j)*16 + (lane&15)
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    const int n = (s0 + j) * 16 + nl;
+    if (s0 + j >= ns || n >= W.n) continue;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+#pragma unroll
+      for (int rr = 0; rr < 4; rr++) {
+        const int row = m0 + wm * 64 + i * 16 + kq * 4 + rr;
+        if (row >= M) continue;
+        float v = acc[i][j][rr];
+        switch (a.epi) {
+          case kEpiBias:
+            v += W.bias[size_t(row) * W.bias_ld + n];
+            break;
+          case kEpiAddGelu:
+            v = gelu_f(v + W.bias[size_t(row) * W.bias_ld + n]);
+            break;
+          case kEpiGelu:
+            v = gelu_f(v);
+            break;
+          case kEpiSilu:
+            v = silu_f(v);
+            break;
+          case kEpiResAdd:
+            v += a.res[size_t(row) * a.ld_res + n];
+            break;
+          case kEpiSiluMul:  // second pass of the FFN: out = silu(tmp1) * (x.w3), aux holds silu(x.w1)
+            v = a.aux[size_t(row) * a.ld_aux + n] * v;
+            break;
+          default:
+            break;
+        }
+        W.out[size_t(row) * W.ldo + n] = v;
+      }
+    }
+  }
+}
+
+// activations -> fp16 [M][Kp] (zero past K; act-order gather when shuffled): the A operand of woq_gemm2_kernel
+template <int AT>
+__global__ void nad_cvt_act_kernel(const void* A, int lda, int M, int K, int Kp, const int32_t* shuffle,
+                                   _Float16* out) {
+  const size_t total = size_t(M) * (Kp / 8);
+  for (size_t u = blockIdx.x * size_t(blockDim.x) + threadIdx.x; u < total; u += size_t(gridDim.x) * blockDim.x) {
+    const int row = int(u / (Kp / 8)), k0 = int(u % (Kp / 8)) * 8;
+    float v[8];
+    load_a8<AT>(A, lda, row, k0, K, shuffle, shuffle == nullptr && (reinterpret_cast<uintptr_t>(A) % 16 == 0) &&
+                                                 ((size_t(lda) * (AT == kActF32 ? 4 : 2)) % 16 == 0), v);
+    h8_t h;
+#pragma unroll
+    for (int j = 0; j < 8; j++) h[j] = _Float16(v[j]);
+    *reinterpret_cast<h8_t*>(out + size_t(row) * Kp + k0) = h;
+  }
+}
+
+}  // namespace g2
+
+hipError_t launch_cvt_act(const void* A, int act_t, int lda, int M, int K, int Kp, const int32_t* shuffle,
+                          _Float16* out, hipStream_t st) {
+  const size_t units = size_t(M) * (Kp / 8);
+  const int blocks = int(std::min<size_t>((units + 255) / 256, 4096));
+  if (act_t == kActF32)
+    hipLaunchKernelGGL(g2::nad_cvt_act_kernel<kActF32>, dim3(blocks), dim3(256), 0, st, A, lda, M, K, Kp, shuffle,
+                       out);
+  else if (act_t == kActF16)
+    hipLaunchKernelGGL(g2::nad_cvt_act_kernel<kActF16>, dim3(blocks), dim3(256), 0, st, A, lda, M, K, Kp, shuffle,
+                       out);
+  else
+    hipLaunchKernelGGL(g2::nad_cvt_act_kernel<kActBF16>, dim3(blocks), dim3(256), 0, st, A, lda, M, K, Kp, shuffle,
+                       out);
+  return hipGetLastError();
+}
+
+hipError_t launch_gemm2(const GemmArgs& a, const _Float16* A16, int lda16, hipStream_t st) {
+  const int nbm = (a.M + g2::BM - 1) / g2::BM, nbn = (a.w.ns + 7) / 8;
+  const size_t lds = 2 * size_t(g2::ABUF);
+  const bool tpg1 = a.w.bs == g2::KT;
+  auto go = [&](auto k) -> hipError_t {
+    static bool attr = false;  // per instantiation (distinct lambda argument types)
+    (void)attr;
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       int(lds));
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k, dim3(nbm * nbn), dim3(512), lds, st, a, A16, lda16);
+    return hipGetLastError();
+  };
+  const bool asym = a.w.zps != nullptr;
+  if (asym) return tpg1 ? go(g2::woq_gemm2_kernel<true, true>) : go(g2::woq_gemm2_kernel<true, false>);
+  return tpg1 ? go(g2::woq_gemm2_kernel<false, true>) : go(g2::woq_gemm2_kernel<false, false>);
+}
+
+}  // namespace nad

@@ -103,6 +103,11 @@ hipError_t launch_repack(const RepackArgs& a, hipStream_t stream);
 hipError_t launch_skinny(const SkinnyArgs& a, int bits, int act_t, int waves_per_wg, int stripes, int ch,
                          hipStream_t stream);
 hipError_t launch_gemm(const GemmArgs& a, int bits, int act_t, hipStream_t stream);
+// prefill GEMM v2 (woq_gemm2.hip): int4, group = 128 * 2^j, stripe-major; A as fp16 [M][lda16] with K padded to the
+// 128-deep tile (zeros), e.g. from launch_cvt_act
+hipError_t launch_gemm2(const GemmArgs& a, const _Float16* A16, int lda16, hipStream_t stream);
+hipError_t launch_cvt_act(const void* A, int act_t, int lda, int M, int K, int Kp, const int32_t* shuffle,
+                          _Float16* out, hipStream_t stream);
 // groups per K tile the GEMV handles (1, 2, 4, 8) for this geometry, 0 if unsupported; *tpg = tiles per group
 int gemv_groups_per_tile(int bits, int nt, int ng, int bs, int* tpg);
 size_t gemv_lds_layout(GemvArgs& a, int bits, int waves, int grid);
