@@ -330,11 +330,14 @@ def main():
         kernel, bytes_per_launch, launch_s = "woq_gemv_kernel (decode GEMV, one launch per matmul)", \
             tot_bytes / n_per_op_launches, per_op_time / n_per_op_launches
     achieved = bytes_per_launch / launch_s / 1e9
+    # HBM traffic per launch from the committed PMC pass (profiles/pmc_traffic.json: FETCH_SIZE x 2 + WRITE_SIZE, the
+    # gfx950 correction of MI355X_MICROARCH.md), scaled from its measured traffic / algorithmic-bytes ratio
     traffic = None
     pmc = os.path.join(REPO, "profiles", "pmc_traffic.json")
     if os.path.exists(pmc):
         try:
-            traffic = json.load(open(pmc)).get("bytes_per_launch")
+            rec = json.load(open(pmc))["woq_chain_kernel" if chain is not None else "woq_gemv_kernel"]
+            traffic = int(rec["traffic_over_algorithmic"] * bytes_per_launch)
         except Exception:
             traffic = None
 

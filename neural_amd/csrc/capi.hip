@@ -439,40 +439,47 @@ static void* scratch(size_t bytes, hipStream_t st) {
   return buf;
 }
 
-// The pipelined prefill GEMM (woq_gemm2.hip) when eligible: 1 launched, 0 not eligible, -1 launch error.
-static int try_gemm2(const GemmArgs& a, const void* act, int act_t, int lda, int m, int k, const DeviceWeight& w,
-                     hipStream_t st) {
-  if (env_int("NAD_GEMM2_DISABLE", 0)) return 0;
+// fp16 activations for the pipelined prefill GEMM (woq_gemm2.hip): the caller's rows when they already are fp16,
+// aligned, unshuffled and tile-padded, else one conversion pass into the scratch.  One conversion serves every GEMM
+// that reads the same activations (the QKV and gate/up fusions).
+struct A16 {
+  const _Float16* p = nullptr;
+  int ld = 0;
+  int kp = 0;
+};
+
+static bool gemm2_ok(const DeviceWeight& w, int m) {
   const int tpg = w.blocksize / 128;
-  if (w.bits != 4 || w.kmajor || w.blocksize % 128 != 0 || (tpg & (tpg - 1)) != 0 || m < 32) return 0;
+  return !env_int("NAD_GEMM2_DISABLE", 0) && w.bits == 4 && !w.kmajor && w.blocksize % 128 == 0 &&
+         (tpg & (tpg - 1)) == 0 && m >= 32 && uint64_t(m) * uint64_t(w.nt) * 256 < (1ull << 32);
+}
+
+// 1 ready, 0 unavailable (fall back to the register-staged GEMM), -1 launch error
+static int prepare_a16(A16& r, const void* act, int act_t, int lda, int m, int k, const DeviceWeight& w,
+                       hipStream_t st) {
   const int kp = w.nt * 128;
-  const _Float16* a16 = nullptr;
-  int lda16 = kp;
+  r.kp = kp;
   if (act_t == kActF16 && !w.shuffle && k == kp && reinterpret_cast<uintptr_t>(act) % 16 == 0 &&
       (size_t(lda) * 2) % 16 == 0) {
-    a16 = static_cast<const _Float16*>(act);
-    lda16 = lda;
-  } else {
-    _Float16* buf = static_cast<_Float16*>(scratch(size_t(m) * kp * 2, st));
-    if (!buf) return 0;
-    hipError_t e = launch_cvt_act(act, act_t, lda, m, k, kp, w.shuffle, buf, st);
-    if (e != hipSuccess) {
-      set_err("activation conversion launch failed: %s", hipGetErrorString(e));
-      return -1;
-    }
-    a16 = buf;
+    r.p = static_cast<const _Float16*>(act);
+    r.ld = lda;
+    return 1;
   }
-  hipError_t e = launch_gemm2(a, a16, lda16, st);
+  _Float16* buf = static_cast<_Float16*>(scratch(size_t(m) * kp * 2, st));
+  if (!buf) return 0;
+  hipError_t e = launch_cvt_act(act, act_t, lda, m, k, kp, w.shuffle, buf, st);
   if (e != hipSuccess) {
-    set_err("gemm2 kernel launch failed: %s", hipGetErrorString(e));
+    set_err("activation conversion launch failed: %s", hipGetErrorString(e));
     return -1;
   }
+  r.p = buf;
+  r.ld = kp;
   return 1;
 }
 
 static int run_gemm(const void* act, int act_t, int lda, int m, int k, const DeviceWeight& w, float* out, int ldo,
                     int epi, const float* bias, int bias_ld, const float* res, int ld_res, const float* aux,
-                    int ld_aux, hipStream_t st) {
+                    int ld_aux, hipStream_t st, const A16* pre = nullptr) {
   GemmArgs a{};
   a.A = act;
   a.lda = lda;
@@ -486,8 +493,23 @@ static int run_gemm(const void* act, int act_t, int lda, int m, int k, const Dev
   a.aux = aux;
   a.ld_aux = ld_aux;
   a.w = view(w, out, ldo, bias, bias_ld);
-  const int g2 = try_gemm2(a, act, act_t, lda, m, k, w, st);
-  if (g2 != 0) return g2 < 0 ? -1 : 0;
+  if (gemm2_ok(w, m)) {
+    A16 own;
+    int rc = 1;
+    if (!pre || pre->kp != w.nt * 128 || w.shuffle) {
+      rc = prepare_a16(own, act, act_t, lda, m, k, w, st);
+      pre = &own;
+    }
+    if (rc < 0) return -1;
+    if (rc > 0) {
+      hipError_t e = launch_gemm2(a, pre->p, pre->ld, st);
+      if (e != hipSuccess) {
+        set_err("gemm2 kernel launch failed: %s", hipGetErrorString(e));
+        return -1;
+      }
+      return 0;
+    }
+  }
   hipError_t e = launch_gemm(a, w.bits, act_t, st);
   if (e != hipSuccess) {
     set_err("gemm kernel launch failed: %s", hipGetErrorString(e));
@@ -559,9 +581,16 @@ extern "C" int nad_device_qkv_forward(const void* act, int act_dtype, const void
   int ldos[3] = {ldo_q, ldo_k, ldo_v};
   if (m <= kSkinnyMaxM)
     return run_skinny(act, act_dtype, lda, m, k, 3, ws, outs, ldos, kEpiNone, nullptr, 0, nullptr, 0, nullptr, 0, st);
+  A16 pre;
+  const A16* pp = nullptr;
+  if (gemm2_ok(*ws[0], m) && !ws[0]->shuffle) {
+    const int rc = prepare_a16(pre, act, act_dtype, lda, m, k, *ws[0], st);
+    if (rc < 0) return -1;
+    if (rc > 0) pp = &pre;
+  }
   for (int i = 0; i < 3; i++)
     if (run_gemm(act, act_dtype, lda, m, k, *ws[i], outs[i], ldos[i], kEpiNone, nullptr, 0, nullptr, 0, nullptr, 0,
-                 st))
+                 st, pp))
       return -1;
   return 0;
 }
@@ -593,8 +622,17 @@ extern "C" int nad_device_ffn_gate_up(const void* act, int act_dtype, const void
     return -1;
   }
   const int e1 = epi == kEpiSiluMul ? kEpiSilu : kEpiGelu;
-  if (run_gemm(act, act_dtype, lda, m, fin, *w1, tmp1, fmid, e1, nullptr, 0, nullptr, 0, nullptr, 0, st)) return -1;
-  return run_gemm(act, act_dtype, lda, m, fin, *w3, tmp2, fmid, kEpiSiluMul, nullptr, 0, nullptr, 0, tmp1, fmid, st);
+  A16 pre;
+  const A16* pp = nullptr;
+  if (gemm2_ok(*w1, m) && !w1->shuffle) {
+    const int rc = prepare_a16(pre, act, act_dtype, lda, m, fin, *w1, st);
+    if (rc < 0) return -1;
+    if (rc > 0) pp = &pre;
+  }
+  if (run_gemm(act, act_dtype, lda, m, fin, *w1, tmp1, fmid, e1, nullptr, 0, nullptr, 0, nullptr, 0, st, pp))
+    return -1;
+  return run_gemm(act, act_dtype, lda, m, fin, *w3, tmp2, fmid, kEpiSiluMul, nullptr, 0, nullptr, 0, tmp1, fmid, st,
+                  pp);
 }
 
 extern "C" int nad_device_ffn_forward(const void* act, int act_dtype, const void* w1p, const void* w2p,

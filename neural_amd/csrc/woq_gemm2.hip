@@ -16,7 +16,8 @@
 //   * one fp32 group accumulator per output fragment is scaled into the result at every group end, so weights are
 //     applied exactly as w = (q - zp) * s (fp32 scale multiply), the only rounding being A -> fp16 (as the reference's
 //     own BF16/FP16 AMX cores round A);
-//   * workgroups are remapped so that the 8 M tiles of one N tile run on one XCD (B re-reads hit that XCD's L2).
+//   * workgroups are remapped so that one XCD walks the N tiles of one M tile (the fp16 A rows, 8x the bytes of the
+//     int4 B tiles per K step, are re-read from that XCD's L2).
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -64,19 +65,14 @@ __device__ __forceinline__ h8_t dequant4(uint32_t w, uint32_t m0, uint32_t m1, u
 
 // LDS-DMA of one K step of A: 256 rows x 256 B = 64 one-KiB pieces, 8 per wave; lane l of piece p fills LDS chunk
 // (l & 15) of row 4p + (l >> 4) with source chunk (l & 15) ^ (row & 15).  Rows past M re-read row M-1 (their
-// outputs are never stored).
-__device__ __forceinline__ void stage_a(const _Float16* A16, int lda16, int M, int m0, int t, char* lbuf, int wave,
-                                        int lane) {
+// outputs are never stored).  The per-lane byte offsets are fixed for the whole K loop (aoff); each step only moves
+// the uniform base.
+__device__ __forceinline__ void stage_a(const char* base, const uint32_t (&aoff)[8], char* lbuf, int wave) {
 #pragma unroll
-  for (int i = 0; i < 8; i++) {
-    const int p = wave * 8 + i;
-    const int row = p * 4 + (lane >> 4);
-    const int grow = min(m0 + row, M - 1);
-    const int sch = (lane & 15) ^ (row & 15);
-    const _Float16* src = A16 + size_t(grow) * lda16 + size_t(t) * KT + sch * 8;
-    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                     (__attribute__((address_space(3))) void*)(lbuf + p * 1024), 16, 0, 0);
-  }
+  for (int i = 0; i < 8; i++)
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(base + aoff[i]),
+                                     (__attribute__((address_space(3))) void*)(lbuf + (wave * 8 + i) * 1024), 16, 0,
+                                     0);
 }
 
 template <bool ASYM, bool TPG1>
@@ -89,7 +85,9 @@ __global__ __launch_bounds__(512, 1) void woq_gemm2_kernel(GemmArgs a, const _Fl
   const int M = a.M, nt = W.nt, ng = W.ng, ns = W.ns;
   const int tpg = W.bs / KT;  // tiles per group (power of two, host-checked)
 
-  // XCD-aware remap: the nbm M tiles of one N tile are consecutive on one XCD
+  // XCD-aware remap: consecutive (remapped) ids share one XCD and walk the N tiles of ONE M tile, so the XCD's L2
+  // holds that M tile's fp16 A rows (64 KiB per K step, read by every workgroup) while the int4 B tiles (8 KiB per K
+  // step) stream from HBM / the Infinity Cache
   const int nbm = (M + BM - 1) / BM;
   const int nbn = (ns + 7) / 8;
   const int nwg = nbm * nbn;
@@ -98,7 +96,7 @@ __global__ __launch_bounds__(512, 1) void woq_gemm2_kernel(GemmArgs a, const _Fl
     const int q = nwg / 8, r = nwg % 8, x = bid % 8, o = bid / 8;
     bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + o;
   }
-  const int bn = bid / nbm, bm = bid % nbm;
+  const int bm = bid / nbn, bn = bid % nbn;
   const int m0 = bm * BM;
   const int s0 = bn * 8 + wn * 4;  // this wave's first stripe
   const int nl = lane & 15;
@@ -112,15 +110,27 @@ __global__ __launch_bounds__(512, 1) void woq_gemm2_kernel(GemmArgs a, const _Fl
     tl[j] = reinterpret_cast<const u4_t*>(W.tiles) + size_t(s) * nt * 64 + lane;
     srow[j] = s * ng;
   }
-  auto load_b = [&](int t, u4_t (&b)[4], float (&sc)[4], int (&zp)[4]) {
+  // branch-free scale fetch: the dword holding this lane's scale (f32, or a 16-bit pair), decoded at use.  A branch on
+  // the scale type here made hipcc drain vmcnt(0) right after the next step's loads were issued.
+  const int st = a.scale_t;
+  const int ssh = st == kScaleF32 ? 0 : (nl & 1) * 16;
+  const uint32_t* sbase = static_cast<const uint32_t*>(W.scales);
+  auto load_b = [&](int t, u4_t (&b)[4], uint32_t (&sc)[4], int (&zp)[4]) {
     const int g = t / tpg;
 #pragma unroll
     for (int j = 0; j < 4; j++) {
       b[j] = __builtin_nontemporal_load(tl[j] + size_t(t) * 64);
       const size_t si = size_t(srow[j] + g) * 16 + nl;
-      sc[j] = load_scale(W.scales, si, a.scale_t);
+      sc[j] = sbase[st == kScaleF32 ? si : (si >> 1)];
       zp[j] = ASYM ? int(W.zps[si]) : 0;
     }
+  };
+  auto scale_f32 = [&](uint32_t x) {
+    const uint32_t h = (x >> ssh) & 0xFFFFu;
+    const float fb = __uint_as_float(h << 16);
+    const float fh = f16_bits_to_f32(uint16_t(h));
+    const float f16or = st == kScaleBF16 ? fb : fh;
+    return st == kScaleF32 ? __uint_as_float(x) : f16or;
   };
 
   f4_t acc[4][4], accg[4][4];
@@ -133,9 +143,17 @@ __global__ __launch_bounds__(512, 1) void woq_gemm2_kernel(GemmArgs a, const _Fl
     }
 
   u4_t bc[4], bx[4];
-  float scc[4], scx[4];
+  uint32_t scc[4], scx[4];
   int zc[4], zx[4];
-  stage_a(A16, lda16, M, m0, 0, smem, wave, lane);
+  uint32_t aoff[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const int row = (wave * 8 + i) * 4 + (lane >> 4);
+    const int grow = min(m0 + row, M - 1);
+    aoff[i] = uint32_t(grow) * uint32_t(lda16) * 2u + uint32_t(((lane & 15) ^ (row & 15)) * 16);
+  }
+  const char* abase = reinterpret_cast<const char*>(A16);
+  stage_a(abase, aoff, smem, wave);
   load_b(0, bc, scc, zc);
   __syncthreads();
 
@@ -147,11 +165,13 @@ __global__ __launch_bounds__(512, 1) void woq_gemm2_kernel(GemmArgs a, const _Fl
   const int kq = lane >> 4;
   const f4_t zero = {0.f, 0.f, 0.f, 0.f};
 
-  for (int t = 0; t < nt; t++) {
+  // one K step on the registers (b, sc, z) while the next step's A and B land in (bn, scn, zn)
+  auto kstep = [&](int t, const u4_t (&b)[4], const uint32_t (&sc)[4], const int (&z)[4], u4_t (&bn)[4],
+                   uint32_t (&scn)[4], int (&zn)[4]) {
     char* cur = smem + (t & 1) * ABUF;
     if (t + 1 < nt) {
-      stage_a(A16, lda16, M, m0, t + 1, smem + ((t + 1) & 1) * ABUF, wave, lane);
-      load_b(t + 1, bx, scx, zx);
+      stage_a(abase + size_t(t + 1) * (KT * 2), aoff, smem + ((t + 1) & 1) * ABUF, wave);
+      load_b(t + 1, bn, scn, zn);
     }
     const bool gstart = TPG1 || (t & (tpg - 1)) == 0;
     const bool gend = TPG1 || ((t + 1) & (tpg - 1)) == 0 || t == nt - 1;
@@ -161,10 +181,10 @@ __global__ __launch_bounds__(512, 1) void woq_gemm2_kernel(GemmArgs a, const _Fl
 #pragma unroll
       for (int j = 0; j < 4; j++) {
         if constexpr (ASYM) {
-          const float z = float(zc[j]);
-          bf[j] = dequant4(bc[j][d], m0k, m1k, mag, s16, zc0 - splat(z), zc1 - splat(z));
+          const float zf = float(z[j]);
+          bf[j] = dequant4(b[j][d], m0k, m1k, mag, s16, zc0 - splat(zf), zc1 - splat(zf));
         } else {
-          bf[j] = dequant4(bc[j][d], m0k, m1k, mag, s16, zc0, zc1);
+          bf[j] = dequant4(b[j][d], m0k, m1k, mag, s16, zc0, zc1);
         }
       }
 #pragma unroll
@@ -183,13 +203,18 @@ __global__ __launch_bounds__(512, 1) void woq_gemm2_kernel(GemmArgs a, const _Fl
     }
     if (gend) {
 #pragma unroll
-      for (int j = 0; j < 4; j++)
+      for (int j = 0; j < 4; j++) {
+        const float sf = scale_f32(sc[j]);
 #pragma unroll
-        for (int i = 0; i < 4; i++) acc[i][j] += accg[i][j] * scc[j];
+        for (int i = 0; i < 4; i++) acc[i][j] += accg[i][j] * sf;
+      }
     }
     __syncthreads();  // next A buffer landed (vmcnt(0)), current buffer free for the step after
+  };
+  for (int t = 0; t < nt; t++) {
+    kstep(t, bc, scc, zc, bx, scx, zx);
 #pragma unroll
-    for (int j = 0; j < 4; j++) {
+    for (int j = 0; j < 4; j++) {  // (unrolling by two to swap the sets instead measured slower: 256 VGPRs)
       bc[j] = bx[j];
       scc[j] = scx[j];
       zc[j] = zx[j];

@@ -1,0 +1,22 @@
+"""Workload for the PMC traffic pass (development tool): a few decode tokens through the per-op launches and the
+decode chain, and a few prefill GEMMs, on the bench's synthetic Llama-2-7B stack (fewer layers: the per-launch
+counters do not depend on the layer count)."""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+
+bench.LAYERS = int(os.environ.get("PMC_LAYERS", "4"))
+stack = bench.Stack(0, 1)
+dec = bench.Runner(stack, 1, None, "cuda")
+for _ in range(3):
+    dec.step()
+ch = bench.ChainRunner(stack, 1, "cuda")
+for _ in range(2):
+    ch.step()
+pre = bench.Runner(stack, 2048, None, "cuda")
+pre.step()
+torch.cuda.synchronize()
