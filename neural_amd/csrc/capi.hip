@@ -347,6 +347,7 @@ static int prepare_gemv(GemvArgs& a, int& waves, int& grid, int& gpt_out, const 
   if (env_int("NAD_GEMV_WAVES", 0) > 0) waves = std::min(gpt > 1 ? 8 : 16, env_int("NAD_GEMV_WAVES", 0));
   a.dq_mask = 0x000F000Fu;
   a.dq_magic = 0x64006400u;
+  a.pre_stages = std::min(3, std::max(1, env_int("NAD_GEMV_PRE", 1)));
   const size_t lds = gemv_lds_layout(a, w0.bits, waves, grid);
   if (lds > 160 * 1024) return 0;
   // buffer-resource offsets are 32-bit: every tile array, scale array and the activations must stay below 2 GiB

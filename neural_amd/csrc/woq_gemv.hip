@@ -337,9 +337,11 @@ __global__ __launch_bounds__(gemv_max_threads<GPT>()) void woq_gemv_kernel(GemvA
   lc.rz = lc.rt;
   if (!idle && nv > 0) cursor_stripe(a, lc, v0);
   StageRegs<GPT> S0, S1, S2;
+  // Only `pre` stages go out before the activations are published: issuing all three first stalled the wave on
+  // memory back-pressure and delayed the (already landed) activation staging by ~1-2 us (phase trace).
   load_stage<GPT, ASYM>(a, S0, lc, nv, nsl, wave, NW, v0, lane, vs);
-  load_stage<GPT, ASYM>(a, S1, lc, nv, nsl, wave, NW, v0, lane, vs);
-  load_stage<GPT, ASYM>(a, S2, lc, nv, nsl, wave, NW, v0, lane, vs);
+  if (a.pre_stages > 1) load_stage<GPT, ASYM>(a, S1, lc, nv, nsl, wave, NW, v0, lane, vs);
+  if (a.pre_stages > 2) load_stage<GPT, ASYM>(a, S2, lc, nv, nsl, wave, NW, v0, lane, vs);
   NAD_TRACE(4);
 
   // 2) publish the activations (waits only for the loads issued before the weights)
@@ -371,6 +373,8 @@ __global__ __launch_bounds__(gemv_max_threads<GPT>()) void woq_gemv_kernel(GemvA
     for (int i = threadIdx.x; i < (Kp >> 3); i += bd) zr[i] = make_uint4(0u, 0u, 0u, 0u);
   }
   __syncthreads();
+  if (a.pre_stages <= 1) load_stage<GPT, ASYM>(a, S1, lc, nv, nsl, wave, NW, v0, lane, vs);
+  if (a.pre_stages <= 2) load_stage<GPT, ASYM>(a, S2, lc, nv, nsl, wave, NW, v0, lane, vs);
   NAD_TRACE(1);
 
   // 3) the stream

@@ -92,6 +92,7 @@ struct GemvArgs {
   int part_off;         // LDS byte offset of the partial-sum slots
   uint32_t dq_mask;     // 0x000F000F and 0x64006400: int4 dequant constants, passed in so they stay in registers
   uint32_t dq_magic;
+  int pre_stages;       // woq_gemv_kernel: weight stages issued before the activation staging (1..3)
   int nwa;              // woq_chain: waves that own K slices in this op (the single-op launch's wave count)
   int norm;             // woq_chain: RMS-normalise each activation row while staging (x / rms(x) * norm_w)
   float norm_eps;
