@@ -723,6 +723,54 @@ int orc_blob_gemv_ref(const float* A, const void* blob, float* C, int m, int lda
   return 0;
 }
 
+/* The same scalar GEMV, its independent NTILE column blocks spread over `threads` OpenMP threads (every output is
+ * computed by exactly the code and order of orc_blob_gemv_ref: bit-identical).  CPU-baseline timing only. */
+int orc_blob_gemv_par(const float* A, const void* blob, float* C, int m, int lda, int ldc, int threads) {
+  blob_t b;
+  int r = blob_parse(&b, blob);
+  if (r) return r;
+  int nt = orc_core_ntile(b.coreid);
+  if (orc_core_packrow(b.coreid) != 1 || m > 8 || b.has_shf) return -5;
+  int bits = dtype_bits(b.dtype);
+  if (bits != 4 && bits != 2) return -6;
+  const uint8_t* q = (const uint8_t*)((const int8_t*)blob + b.q_off);
+  const uint8_t* sp = (const uint8_t*)((const int8_t*)blob + b.s_off);
+  const int8_t* zp = b.asym ? (const int8_t*)blob + b.z_off : NULL;
+  int blks = b.k / b.bs;
+  int nblk = (b.n + nt - 1) / nt;
+#pragma omp parallel for schedule(static) num_threads(threads)
+  for (int blk = 0; blk < nblk; blk++) {
+    int n0 = blk * nt;
+    float acc[48 * 8];
+    memset(acc, 0, sizeof(float) * (size_t)nt * m);
+    const uint8_t* bp = q + (size_t)n0 * b.kpad * bits / 8;
+    for (int ib = 0; ib < blks; ib++) {
+      for (int ik = 0; ik < b.bs; ik++) {
+        int kk = ib * b.bs + ik;
+        for (int im = 0; im < m; im++) {
+          float aval = A[(size_t)im * lda + kk];
+          for (int in = 0; in < nt; in++) {
+            size_t ci = (size_t)ib * b.cstep + n0 + in;
+            int qv;
+            if (bits == 4)
+              qv = ((bp[(size_t)kk * nt / 2 + in / 2] >> (4 * (in & 1))) & 0xF) - 8;
+            else
+              qv = ((bp[((size_t)kk * nt + in) / 4] >> (2 * (in & 3))) & 3) - 2;
+            float z = zp ? (float)zp[ci] : 0.f;
+            if (bits == 4)
+              acc[im * nt + in] += aval * ((float)qv - z) * get_scale(sp, ci, b.scat);
+            else
+              acc[im * nt + in] += aval * (((float)qv - z) * get_scale(sp, ci, b.scat));
+          }
+        }
+      }
+    }
+    for (int im = 0; im < m; im++)
+      for (int in = 0; in < nt && n0 + in < b.n; in++) C[(size_t)im * ldc + n0 + in] = acc[im * nt + in];
+  }
+  return 0;
+}
+
 int orc_blob_gemv_timed(const float* A, const void* blob, float* C, int m, int lda, int ldc, int iters) {
   int r = 0;
   for (int it = 0; it < iters && r == 0; it++) r = orc_blob_gemv_ref(A, blob, C, m, lda, ldc);

@@ -94,6 +94,7 @@ int orc_blob_forward(const float* A, const void* blob, float* C, int m, int n, i
    float accumulation in the reference's order (MTILE = m <= 8) */
 int orc_blob_gemv_ref(const float* A, const void* blob, float* C, int m, int lda, int ldc);
 /* single-threaded CPU WOQ GEMV in the reference algorithm's float order, used as the timed cpu_baseline */
+int orc_blob_gemv_par(const float* A, const void* blob, float* C, int m, int lda, int ldc, int threads);
 int orc_blob_gemv_timed(const float* A, const void* blob, float* C, int m, int lda, int ldc, int iters);
 
 #ifdef __cplusplus

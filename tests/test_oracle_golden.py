@@ -187,3 +187,19 @@ def test_blob_roundtrip_and_layout(oracle):
                     np.testing.assert_array_equal(S, s)
                 if asym:
                     np.testing.assert_array_equal(Z, z)
+
+
+def test_parallel_gemv_matches_scalar(oracle):
+    """The OpenMP column-block GEMV used for bench.py's cpu_baseline is bit-identical to the scalar oracle GEMV."""
+    from tests.oracle_lib import S4, F16
+    rng = np.random.default_rng(11)
+    n, k = 200, 512
+    Q = rng.integers(-8, 8, size=(k, n), dtype=np.int8)
+    S = rng.uniform(0.001, 0.01, size=(k // 128, n)).astype(np.float32)
+    blob = oracle.pack_q(Q, S, None, n, k, 128, S4, F16, False, oracle.core("avx512f"))
+    A = rng.uniform(-0.5, 0.5, size=(2, k)).astype(np.float32)
+    c1 = np.zeros((2, n), np.float32)
+    c2 = np.zeros((2, n), np.float32)
+    assert oracle.lib.orc_blob_gemv_ref(A.ctypes.data, blob.ctypes.data, c1.ctypes.data, 2, k, n) == 0
+    assert oracle.lib.orc_blob_gemv_par(A.ctypes.data, blob.ctypes.data, c2.ctypes.data, 2, k, n, 4) == 0
+    np.testing.assert_array_equal(c1, c2)
