@@ -386,28 +386,25 @@ __global__ __launch_bounds__(768) void woq_chain_kernel(const GemvArgs* __restri
       if (cj >= nv) return;
       const int t0 = cq * KS;
       const char* ab = a_hi + t0 * KT * 2;
-      f4_t accg = {0.f, 0.f, 0.f, 0.f};
+      f4_t accg[KS];  // as woq_gemv.hip: KS independent chains, step-major, scaled per tile in tile order
 #pragma unroll
-      for (int i = 0; i < KS; i++) {
-        if (t0 + i < nt) {
+      for (int d = 0; d < SPT; d++) {
 #pragma unroll
-          for (int d = 0; d < SPT; d++) {
-            h8_t bf;
-            if constexpr (ASYM) {
-              const float z = float(S.zp[i]);
-              bf = dequant4(S.b[i][d], m0, m1, mag, s16, zc0 - splat(z), zc1 - splat(z));
-            } else {
-              bf = dequant4(S.b[i][d], m0, m1, mag, s16, zc0, zc1);
-            }
-            const h8_t af = *reinterpret_cast<const h8_t*>(ab + i * KT * 2 + d * 64);
-            accg = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, bf, accg, 0, 0, 0);
+        for (int i = 0; i < KS; i++) {
+          const int ti = min(t0 + i, nt - 1) - t0;
+          h8_t bf;
+          if constexpr (ASYM) {
+            const float z = float(S.zp[i]);
+            bf = dequant4(S.b[i][d], m0, m1, mag, s16, zc0 - splat(z), zc1 - splat(z));
+          } else {
+            bf = dequant4(S.b[i][d], m0, m1, mag, s16, zc0, zc1);
           }
-          if ((((t0 + i + 1) & a.tpg_mask) == 0) || i == KS - 1 || t0 + i == nt - 1) {
-            acc += accg * scale_bits_to_f32(S.sc[i], a.scale_t, ssh);
-            accg = f4_t{0.f, 0.f, 0.f, 0.f};
-          }
+          const h8_t af = *reinterpret_cast<const h8_t*>(ab + ti * KT * 2 + d * 64);
+          accg[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, bf, d == 0 ? f4_t{0.f, 0.f, 0.f, 0.f} : accg[i], 0, 0, 0);
         }
       }
+#pragma unroll
+      for (int i = 0; i < KS; i++) acc += accg[i] * scale_bits_to_f32(S.sc[i], a.scale_t, ssh);
       cq += NWa;
       if (cq >= nsl) {
         f4_t r = acc;

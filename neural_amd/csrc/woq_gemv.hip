@@ -403,44 +403,37 @@ __global__ __launch_bounds__(gemv_max_threads<GPT>()) void woq_gemv_kernel(GemvA
     const int t0 = cq * KS;
     const char* ab = a_hi + t0 * KT * 2;
     const char* abl = a_lo + t0 * KT * 2;
-    f4_t accg = {0.f, 0.f, 0.f, 0.f};
+    // KS independent MFMA chains (one per tile, step-major) so the scheduler can interleave them; tiles past the end
+    // of K carry out-of-range (zero) weights and a zero scale, and read a valid activation row (no NaN from LDS).
+    f4_t accg[KS];
 #pragma unroll
-    for (int i = 0; i < KS; i++) {
-      if (t0 + i < nt) {
+    for (int d = 0; d < SPT; d++) {
+      const int g = GPT == 1 ? 0 : d / SPG;
 #pragma unroll
-        for (int d = 0; d < SPT; d++) {
-          const int g = GPT == 1 ? 0 : d / SPG;
-          h8_t bf;
-          if constexpr (BITS == 4) {
-            if constexpr (ASYM) {
-              const float z = float(S.zp[i][g]);
-              bf = dequant4(S.b[i][d], dq, zc0 - splat(z), zc1 - splat(z));
-            } else {
-              bf = dequant4(S.b[i][d], dq, zc0, zc1);
-            }
+      for (int i = 0; i < KS; i++) {
+        const int ti = min(t0 + i, nt - 1) - t0;
+        h8_t bf;
+        if constexpr (BITS == 4) {
+          if constexpr (ASYM) {
+            const float z = float(S.zp[i][g]);
+            bf = dequant4(S.b[i][d], dq, zc0 - splat(z), zc1 - splat(z));
           } else {
-            bf = dequant_step<BITS>(S.b[i], d, zp_const(BIAS + S.zp[i][g]));
+            bf = dequant4(S.b[i][d], dq, zc0, zc1);
           }
-          const h8_t af = *reinterpret_cast<const h8_t*>(ab + i * KT * 2 + d * 64);
-          accg = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, bf, accg, 0, 0, 0);
-          if constexpr (HILO == 2) {
-            const h8_t afl = *reinterpret_cast<const h8_t*>(abl + i * KT * 2 + d * 64);
-            accg = __builtin_amdgcn_mfma_f32_16x16x32_f16(afl, bf, accg, 0, 0, 0);
-          }
-          if constexpr (GPT > 1) {
-            if ((d + 1) % SPG == 0) {
-              acc += accg * scale_bits_to_f32(S.sc[i][g], a.scale_t, ssh);
-              accg = f4_t{0.f, 0.f, 0.f, 0.f};
-            }
-          }
+        } else {
+          bf = dequant_step<BITS>(S.b[i], d, zp_const(BIAS + S.zp[i][g]));
         }
-        if constexpr (GPT == 1) {
-          // group end at this tile, or the slice ends inside the group (a linear partial of it)
-          if ((((t0 + i + 1) & a.tpg_mask) == 0) || i == KS - 1 || t0 + i == nt - 1) {
-            acc += accg * scale_bits_to_f32(S.sc[i][0], a.scale_t, ssh);
-            accg = f4_t{0.f, 0.f, 0.f, 0.f};
-          }
+        const h8_t af = *reinterpret_cast<const h8_t*>(ab + ti * KT * 2 + d * 64);
+        const bool first = d % SPG == 0;
+        accg[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, bf, first ? f4_t{0.f, 0.f, 0.f, 0.f} : accg[i], 0, 0, 0);
+        if constexpr (HILO == 2) {
+          const h8_t afl = *reinterpret_cast<const h8_t*>(abl + ti * KT * 2 + d * 64);
+          accg[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(afl, bf, accg[i], 0, 0, 0);
         }
+      }
+      if ((d + 1) % SPG == 0) {  // group end: scale each tile's group partial into the stripe sum, in tile order
+#pragma unroll
+        for (int i = 0; i < KS; i++) acc += accg[i] * scale_bits_to_f32(S.sc[i][g], a.scale_t, ssh);
       }
     }
     cq += NW;

@@ -66,6 +66,8 @@ def main():
         n, k, nw = SHAPES[name]
         per = nw * wbytes(n, k) + 4 * (k + nw * n)
         copies = max(2, math.ceil(600e6 / per))
+        if os.environ.get("SWEEP_COPIES"):  # e.g. 1-2: weights stay in the Infinity Cache (warm-MALL experiment)
+            copies = int(os.environ["SWEEP_COPIES"])
         ws = [[bestla.DeviceWeight.synthetic(4, n, k, G, "fp16", False, seed=1000 * i + j) for j in range(nw)]
               for i in range(copies)]
         xa = x[:, :k].contiguous()
