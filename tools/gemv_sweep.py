@@ -117,16 +117,14 @@ def main():
                 assert L.nad_trace_fetch(buf.ctypes.data, buf.nbytes, 0, 0) == 0
                 nz = buf[0] > 0
                 grid = int(nz.sum())
-                s0, s1, s2, s3, s4, s5, s6 = (buf[i, :grid].astype(np.int64) for i in range(7))
+                s0, s1, s2, s3, s4 = (buf[i, :grid].astype(np.int64) for i in range(5))
                 t0 = s0.min()
                 q = lambda v: "p10 %6.2f p50 %6.2f p90 %6.2f max %6.2f" % tuple(  # noqa: E731
                     np.percentile(v * tick_us, [10, 50, 90, 100]))
                 print(f"    traced span {(s3.max() - t0) * tick_us:7.2f} us, grid {grid}")
                 print(f"    wg start offset   {q(s0 - t0)}")
-                print(f"    A loads issued    {q(s4 - s0)}")
-                print(f"    S0,S1 issued      {q(s5 - s0)}")
-                print(f"    prologue (->bar)  {q(s1 - s0)}")
-                print(f"    first stage done  {q(s6 - s1)} (after barrier, max over waves)")
+                print(f"    A + stage0 issued {q(s4 - s0)}")
+                print(f"    A staged (->bar)  {q(s1 - s0)}")
                 print(f"    main loop         {q(s2 - s1)}")
                 print(f"    reduce+epilogue   {q(s3 - s2)}")
                 print(f"    wg end offset     {q(s3 - t0)}")
