@@ -503,7 +503,8 @@ static int run_gemm(const void* act, int act_t, int lda, int m, int k, const Dev
     }
     if (rc < 0) return -1;
     if (rc > 0) {
-      hipError_t e = launch_gemm2(a, pre->p, pre->ld, st);
+      hipError_t e = env_int("NAD_GEMM_KERNEL", 3) == 2 ? launch_gemm2(a, pre->p, pre->ld, st)
+                                                        : launch_gemm3(a, pre->p, pre->ld, st);
       if (e != hipSuccess) {
         set_err("gemm2 kernel launch failed: %s", hipGetErrorString(e));
         return -1;

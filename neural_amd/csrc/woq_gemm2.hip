@@ -21,6 +21,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <utility>
 
 #include "woq_device.h"
 #include "woq_kernels.h"
@@ -279,6 +280,329 @@ __global__ void nad_cvt_act_kernel(const void* A, int lda, int M, int K, int Kp,
 }
 
 }  // namespace g2
+
+// ------------------------------------------------------------------------------------------------------------------
+// gemm3: the same 256 x 128 block tile, pipelined across barriers.  In gemm2 the B tiles and scales are register loads
+// beside the A LDS-DMA, so hipcc waits vmcnt(0) at their first use and at the __syncthreads: every K step exposes the
+// full load latency (cdna_hip_programming.md §5 "Pipelining across barriers", trap (b)).  Here EVERY operand moves by
+// LDS-DMA into one __shared__ array and each barrier waits with a counted vmcnt for the buffer the next half step reads
+// only:
+//   * K advances in 64-deep half steps; A (256 rows x 128 B, 32 pieces of 1 KiB, 4 per wave) is staged three half
+//     steps ahead into a ring of four 32 KiB buffers;
+//   * the K tile of B (8 stripes x 1 KiB, one piece per wave) and its scale / zero-point dwords (one 256 B piece each,
+//     issued by every wave -- duplicate writes of identical bytes) go out with A on odd half steps into a ring of three;
+//   * waves are 2 (M) x 4 (N), 128 x 32 per wave: each wave dequantizes 2 stripes (half of gemm2's per-wave VALU) and
+//     reads 8 A fragments per 32-deep step;
+//   * LDS image of a half step: row r = 128 B = 8 chunks of 16 B, chunk c holds A[r][8 (c ^ f(r)) .. + 7] with
+//     f(r) = (r >> 1) & 7 (XOR through the DMA source address): a ds_read_b128 over 16 consecutive rows at one chunk
+//     hits 16 distinct 16-B bank slots.
+namespace g3 {
+
+constexpr int BM = 256, KT = 128, ROWB = 128;        // ROWB: bytes of one A row per 64-deep half step
+constexpr int HBUF = BM * ROWB;                       // one half step of A: 32 KiB
+constexpr int NA = 4;                                 // A ring: three half steps in flight
+constexpr int BTILES = 8 * 1024, BSC = 512, BZP = 512;
+constexpr int BBUF = BTILES + BSC + BZP;              // one K tile of B: 8 stripe tiles + scale and zero-point dwords
+constexpr int NBR = 3;                                // B ring
+constexpr int LDS_BYTES = NA * HBUF + NBR * BBUF;     // 155 KiB
+
+__device__ __forceinline__ void glds16(const void* g, char* l) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                   (__attribute__((address_space(3))) void*)l, 16, 0, 0);
+}
+__device__ __forceinline__ void glds4(const void* g, char* l) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                   (__attribute__((address_space(3))) void*)l, 4, 0, 0);
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// LDS reads in inline asm: hipcc puts a vmcnt(0) in front of every LDS read it can see while an LDS-DMA is in flight
+// (it cannot tell the buffers of one __shared__ array apart), which would drain the whole prefetch each half step.
+// Results are consumed only after an explicit lgkmcnt wait that names them (wait_lgk below).
+template <int OFF>
+__device__ __forceinline__ h8_t lds_b128(uint32_t addr) {
+  h8_t r;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "n"(OFF));
+  return r;
+}
+template <int OFF>
+__device__ __forceinline__ uint2 lds_b64(uint32_t addr) {
+  uint2 r;
+  asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "n"(OFF));
+  return r;
+}
+template <int OFF>
+__device__ __forceinline__ uint32_t lds_b32(uint32_t addr) {
+  uint32_t r;
+  asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "n"(OFF));
+  return r;
+}
+template <size_t... I>
+__device__ __forceinline__ void lds_frags(h8_t (&f)[8], uint32_t addr, std::index_sequence<I...>) {
+  ((f[I] = lds_b128<int(I) * 16 * ROWB>(addr)), ...);
+}
+template <class T>
+__device__ __forceinline__ void tie(T& r) {
+  asm volatile("" : "+v"(r));
+}
+template <int N, class... T>
+__device__ __forceinline__ void wait_lgk(T&... regs) {
+  asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(N));
+  (tie(regs), ...);  // each result is redefined after the wait: no use can be scheduled above it
+}
+__device__ __forceinline__ uint32_t lds_addr(const char* p) {
+  return uint32_t(reinterpret_cast<uintptr_t>((const __attribute__((address_space(3))) char*)p));
+}
+
+template <bool ASYM, bool TPG1>
+__global__ __launch_bounds__(512, 1) void woq_gemm3_kernel(GemmArgs a, const _Float16* __restrict__ A16, int lda16) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));
+  const int wm = wave >> 2, wn = wave & 3;
+  const SkinnyWeight& W = a.w;
+  const int M = a.M, nt = W.nt, ng = W.ng, ns = W.ns;
+  const int tpg = W.bs / KT;
+  const int tsh = __builtin_ctz(unsigned(tpg));
+  const int nh = 2 * nt;
+
+  // XCD-aware remap (as gemm2)
+  const int nbm = (M + BM - 1) / BM;
+  const int nbn = (ns + 7) / 8;
+  const int nwg = nbm * nbn;
+  int bid = blockIdx.x;
+  {
+    const int q = nwg / 8, r = nwg % 8, x = bid % 8, o = bid / 8;
+    bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + o;
+  }
+  const int bm = bid / nbn, bn = bid % nbn;
+  const int m0 = bm * BM;
+  const int nl = lane & 15, kq = lane >> 4;
+
+  // DMA sources of this lane.  A piece p = 4 wave + i: rows 8p .. 8p + 7, lane -> row 8p + (lane >> 3), chunk lane & 7
+  uint32_t aoff[4];
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const int row = (wave * 4 + i) * 8 + (lane >> 3);
+    const int grow = min(m0 + row, M - 1);  // rows past M re-read row M-1 (never stored)
+    aoff[i] = uint32_t(grow) * uint32_t(lda16) * 2u + uint32_t(((lane & 7) ^ ((row >> 1) & 7)) * 16);
+  }
+  const char* abase = reinterpret_cast<const char*>(A16);
+  // B: wave w copies stripe 8 bn + w (clamped: stripes past N are never stored); scale / zero-point piece w & 1 covers
+  // stripes 8 bn + 4 (w & 1) + (lane >> 4), column lane & 15
+  const char* btile = static_cast<const char*>(W.tiles) + (size_t(min(bn * 8 + wave, ns - 1)) * nt * 64 + lane) * 16;
+  const int sstripe = min(bn * 8 + (wave & 1) * 4 + (lane >> 4), ns - 1);
+  const size_t srow0 = size_t(sstripe) * ng * 16 + nl;
+  const int st = a.scale_t;
+  const uint32_t* sbase = static_cast<const uint32_t*>(W.scales);
+  const uint32_t* zbase = reinterpret_cast<const uint32_t*>(W.zps);
+
+  // batch(u): the DMAs issued at the start of half step u -- A(u + 3) and, on odd u, B tile (u + 3) / 2
+  auto issue = [&](auto Hc, int u) {
+    constexpr int H = decltype(Hc)::value;
+    if (u + 3 >= nh) return;
+    const int ua = u + 3;
+    char* ab = smem + (ua & 3) * HBUF;
+    const char* src = abase + size_t(ua) * ROWB;
+#pragma unroll
+    for (int i = 0; i < 4; i++) glds16(src + aoff[i], ab + (wave * 4 + i) * 1024);
+    if constexpr (H == 1) {
+      const int t = ua >> 1;
+      char* bb = smem + NA * HBUF + (t % NBR) * BBUF;
+      glds16(btile + size_t(t) * 1024, bb + wave * 1024);
+      const size_t si = srow0 + size_t(t >> tsh) * 16;
+      glds4(sbase + (st == kScaleF32 ? si : (si >> 1)), bb + BTILES + (wave & 1) * 256);
+      if constexpr (ASYM) glds4(zbase + (si >> 2), bb + BTILES + BSC + (wave & 1) * 256);
+    }
+  };
+  // VMEM instructions per odd batch besides the 4 A pieces
+  constexpr int NBW = ASYM ? 3 : 2;
+
+  f4_t acc[8][2], accg[8][2];
+#pragma unroll
+  for (int i = 0; i < 8; i++)
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+      acc[i][j] = f4_t{0.f, 0.f, 0.f, 0.f};
+      accg[i][j] = f4_t{0.f, 0.f, 0.f, 0.f};
+    }
+
+  // prologue: batches -3, -2, -1 (A0 + B0, A1, A2 + B1); wait for batch -3
+  issue(std::integral_constant<int, 1>{}, -3);
+  issue(std::integral_constant<int, 0>{}, -2);
+  issue(std::integral_constant<int, 1>{}, -1);
+  if (nh > 2)
+    wait_vm<8 + NBW>();
+  else
+    wait_vm<4>();
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+
+  const uint32_t m0k = 0x000F000Fu, m1k = 0x00F000F0u, mag = 0x64006400u;
+  const h2_t s16 = g2::splat(1.f / 16.f);
+  const h2_t zc0 = g2::splat(-(1024.f + 8.f)), zc1 = g2::splat(-(64.f + 8.f));
+  // fragment reads: A row wm*128 + i*16 + nl, chunk (dd*4 + kq) ^ f(row); B / scale / zp of stripe wn*2 + j
+  uint32_t roff[2];
+#pragma unroll
+  for (int dd = 0; dd < 2; dd++) roff[dd] = uint32_t((wm * 128 + nl) * ROWB + (((dd * 4 + kq) ^ ((nl >> 1) & 7)) * 16));
+  const int boff = (wn * 2) * 1024 + lane * 16;
+  const int soff = BTILES + ((wn * 2) * 16 + nl) * 4;
+  const int zoff = BTILES + BSC + ((wn * 2) * 16 + nl) * 4;
+  const int ssh = st == kScaleF32 ? 0 : (nl & 1) * 16;
+  const int zsh = (nl & 3) * 8;
+  const f4_t zero = {0.f, 0.f, 0.f, 0.f};
+  auto scale_f32 = [&](uint32_t x) {
+    const uint32_t h = (x >> ssh) & 0xFFFFu;
+    const float fb = __uint_as_float(h << 16);
+    const float fh = f16_bits_to_f32(uint16_t(h));
+    const float f16or = st == kScaleBF16 ? fb : fh;
+    return st == kScaleF32 ? __uint_as_float(x) : f16or;
+  };
+
+  auto half = [&](auto Hc, int u) {
+    constexpr int H = decltype(Hc)::value;  // which 64 of the B tile's 128
+    const int t = u >> 1;
+    const char* ab = smem + (u & 3) * HBUF;
+    const char* bb = smem + NA * HBUF + (t % NBR) * BBUF;
+    issue(Hc, u);
+    const uint32_t al = lds_addr(ab), bl = lds_addr(bb);
+    uint2 bv0 = lds_b64<H * 8>(bl + boff), bv1 = lds_b64<1024 + H * 8>(bl + boff);
+    uint32_t zw0 = 0, zw1 = 0;
+    if constexpr (ASYM) {
+      zw0 = lds_b32<0>(bl + zoff);
+      zw1 = lds_b32<64>(bl + zoff);
+    }
+    h8_t af0[8], af1[8];
+    lds_frags(af0, al + roff[0], std::make_index_sequence<8>{});
+    lds_frags(af1, al + roff[1], std::make_index_sequence<8>{});
+    wait_lgk<8>(bv0, bv1, zw0, zw1, af0[0], af0[1], af0[2], af0[3], af0[4], af0[5], af0[6], af0[7]);
+    const uint32_t bw[2][2] = {{bv0.x, bv0.y}, {bv1.x, bv1.y}};
+    int zp[2] = {0, 0};
+    if constexpr (ASYM) {
+      zp[0] = int(int8_t((zw0 >> zsh) & 0xFFu));
+      zp[1] = int(int8_t((zw1 >> zsh) & 0xFFu));
+    }
+    const bool gstart = H == 0 && (TPG1 || (t & (tpg - 1)) == 0);
+    const bool gend = H == 1 && (TPG1 || ((t + 1) & (tpg - 1)) == 0 || t == nt - 1);
+#pragma unroll
+    for (int dd = 0; dd < 2; dd++) {
+      if (dd == 1) wait_lgk<0>(af1[0], af1[1], af1[2], af1[3], af1[4], af1[5], af1[6], af1[7]);
+      h8_t bf[2];
+#pragma unroll
+      for (int j = 0; j < 2; j++) {
+        if constexpr (ASYM) {
+          const float zf = float(zp[j]);
+          bf[j] = g2::dequant4(bw[j][dd], m0k, m1k, mag, s16, zc0 - g2::splat(zf), zc1 - g2::splat(zf));
+        } else {
+          bf[j] = g2::dequant4(bw[j][dd], m0k, m1k, mag, s16, zc0, zc1);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 8; i++) {
+        const h8_t af = dd == 0 ? af0[i] : af1[i];
+#pragma unroll
+        for (int j = 0; j < 2; j++) {
+          if (dd == 0 && gstart)
+            accg[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, bf[j], zero, 0, 0, 0);
+          else
+            accg[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, bf[j], accg[i][j], 0, 0, 0);
+        }
+      }
+    }
+    if (gend) {
+      uint32_t sw0 = lds_b32<0>(bl + soff), sw1 = lds_b32<64>(bl + soff);
+      wait_lgk<0>(sw0, sw1);
+      const float sf[2] = {scale_f32(sw0), scale_f32(sw1)};
+#pragma unroll
+      for (int j = 0; j < 2; j++)
+#pragma unroll
+        for (int i = 0; i < 8; i++) acc[i][j] += accg[i][j] * sf[j];
+    }
+    // hand-over: batch(u - 2) (the buffers half step u + 1 reads) has landed for this wave; batches u - 1 and u
+    // (8 A pieces + one B batch, whatever the order inside a batch) stay in flight across the barrier
+    if constexpr (H == 0) {
+      if (u + 3 < nh)
+        wait_vm<8 + NBW>();
+      else
+        wait_vm<0>();
+    } else {
+      if (u + 3 < nh)
+        wait_vm<8 + NBW>();
+      else if (u + 3 == nh)
+        wait_vm<4>();
+      else
+        wait_vm<0>();
+    }
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+
+  for (int u = 0; u < nh; u += 2) {
+    half(std::integral_constant<int, 0>{}, u);
+    half(std::integral_constant<int, 1>{}, u + 1);
+  }
+
+  // epilogue: C fragment (i, j): row = m0 + wm*128 + i*16 + kq*4 + rr, col = (bn*8 + wn*2 + j)*16 + nl
+  const int s0 = bn * 8 + wn * 2;
+#pragma unroll
+  for (int j = 0; j < 2; j++) {
+    const int n = (s0 + j) * 16 + nl;
+    if (s0 + j >= ns || n >= W.n) continue;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+#pragma unroll
+      for (int rr = 0; rr < 4; rr++) {
+        const int row = m0 + wm * 128 + i * 16 + kq * 4 + rr;
+        if (row >= M) continue;
+        float v = acc[i][j][rr];
+        switch (a.epi) {
+          case kEpiBias:
+            v += W.bias[size_t(row) * W.bias_ld + n];
+            break;
+          case kEpiAddGelu:
+            v = gelu_f(v + W.bias[size_t(row) * W.bias_ld + n]);
+            break;
+          case kEpiGelu:
+            v = gelu_f(v);
+            break;
+          case kEpiSilu:
+            v = silu_f(v);
+            break;
+          case kEpiResAdd:
+            v += a.res[size_t(row) * a.ld_res + n];
+            break;
+          case kEpiSiluMul:
+            v = a.aux[size_t(row) * a.ld_aux + n] * v;
+            break;
+          default:
+            break;
+        }
+        W.out[size_t(row) * W.ldo + n] = v;
+      }
+    }
+  }
+}
+
+}  // namespace g3
+
+hipError_t launch_gemm3(const GemmArgs& a, const _Float16* A16, int lda16, hipStream_t st) {
+  const int nbm = (a.M + g3::BM - 1) / g3::BM, nbn = (a.w.ns + 7) / 8;
+  const bool tpg1 = a.w.bs == g3::KT;
+  auto go = [&](auto k) -> hipError_t {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       g3::LDS_BYTES);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k, dim3(nbm * nbn), dim3(512), g3::LDS_BYTES, st, a, A16, lda16);
+    return hipGetLastError();
+  };
+  const bool asym = a.w.zps != nullptr;
+  if (asym) return tpg1 ? go(g3::woq_gemm3_kernel<true, true>) : go(g3::woq_gemm3_kernel<true, false>);
+  return tpg1 ? go(g3::woq_gemm3_kernel<false, true>) : go(g3::woq_gemm3_kernel<false, false>);
+}
 
 hipError_t launch_cvt_act(const void* A, int act_t, int lda, int M, int K, int Kp, const int32_t* shuffle,
                           _Float16* out, hipStream_t st) {

@@ -107,6 +107,9 @@ hipError_t launch_gemm(const GemmArgs& a, int bits, int act_t, hipStream_t strea
 // prefill GEMM v2 (woq_gemm2.hip): int4, group = 128 * 2^j, stripe-major; A as fp16 [M][lda16] with K padded to the
 // 128-deep tile (zeros), e.g. from launch_cvt_act
 hipError_t launch_gemm2(const GemmArgs& a, const _Float16* A16, int lda16, hipStream_t stream);
+// prefill GEMM v3 (woq_gemm2.hip): same contract as launch_gemm2; every operand staged by LDS-DMA three 64-deep half
+// steps ahead with counted vmcnt (no drain at the barriers)
+hipError_t launch_gemm3(const GemmArgs& a, const _Float16* A16, int lda16, hipStream_t stream);
 hipError_t launch_cvt_act(const void* A, int act_t, int lda, int M, int K, int Kp, const int32_t* shuffle,
                           _Float16* out, hipStream_t stream);
 // groups per K tile the GEMV handles (1, 2, 4, 8) for this geometry, 0 if unsupported; *tpg = tiles per group

@@ -1,0 +1,130 @@
+"""Prefill GEMMs (woq_gemm2.hip): gemm3 (default: every operand by LDS-DMA, three 64-deep half steps in flight) and
+gemm2 (NAD_GEMM_KERNEL=2: A by LDS-DMA one K step ahead, B in registers).
+
+Both run for int4 weights with group size a power-of-two multiple of 128 and M >= 32 (capi.hip gemm2_ok); these
+cases pin them against the oracle (fp64 GEMM on the reference's dequantized weights) on ragged M/N, K tails, all
+scale dtypes, asymmetric zero points, per-channel scales and act-order shuffles.
+
+Tolerances (north_star: 1e-3 relative):
+  * fp32 activations (rounded to fp16 once by nad_cvt_act_kernel): max|y - ref| <= 1e-3 * max|ref|
+  * fp16 activations (exact inputs, fp32 MFMA accumulation):      max|y - ref| <= 2e-5 * max|ref|
+  * bf16 activations (exact in fp16 except below 2^-14):            max|y - ref| <= 1e-4 * max|ref|
+"""
+import numpy as np
+import pytest
+
+from tests.conftest import gpu_available
+from tests.oracle_lib import BF16, F16, F32, S4
+from tests.test_gpu_parity import _blob, _rel_err
+
+pytestmark = pytest.mark.gpu
+
+if gpu_available():
+    import torch
+    from neural_amd import bestla
+
+TOL = {"fp32": 1e-3, "fp16": 2e-5, "bf16": 1e-4}
+
+GEMM2_CASES = [
+    # m, n, k, bs, qtype, stype, asym, comp, act-order shuffle
+    (32, 64, 128, 128, S4, F16, False, 4, False),       # smallest eligible M, one K tile (two half steps)
+    (257, 300, 640, 128, S4, BF16, True, 4, False),     # ragged M (one row past a block), ragged N
+    (64, 128, 1024, 256, S4, F32, False, 1, False),     # 2 K tiles per group
+    (100, 96, 4096, 4096, S4, F32, True, 1, False),     # per-channel
+    (96, 130, 300, 128, S4, F16, False, 4, False),      # K tail (300 = 2 tiles + 44, zero padded)
+    (64, 80, 512, 128, S4, F16, True, 4, True),         # act-order shuffle gathered during conversion
+    (512, 384, 2048, 128, S4, F16, False, 4, False),    # several M and N blocks
+    (300, 200, 768, 256, S4, BF16, True, 4, False),     # 3 K tiles at 2 tiles per group: a group ends at the tail
+]
+
+
+@pytest.mark.parametrize("kernel", ["3", "2"])
+@pytest.mark.parametrize("cfg", GEMM2_CASES)
+@pytest.mark.parametrize("act", ["fp32", "fp16", "bf16"])
+def test_gemm_parity(oracle, monkeypatch, kernel, cfg, act):
+    monkeypatch.setenv("NAD_GEMM_KERNEL", kernel)
+    m, n, k, bs, qt, st, asym, comp, shuf = cfg
+    blob = _blob(oracle, n, k, bs, qt, st, asym, comp, seed=m + 3 * n + k, gidx=shuf)
+    w = bestla.DeviceWeight(blob)
+    assert bool(w.has_shuffle) == shuf
+    A = np.random.default_rng(m * 5 + n).uniform(-0.5, 0.5, size=(m, k)).astype(np.float32)
+    x = torch.from_numpy(A).cuda()
+    if act != "fp32":
+        x = x.to(torch.float16 if act == "fp16" else torch.bfloat16)
+    ref = oracle.forward(x.float().cpu().numpy(), blob, n, k)
+    y = w.forward(x).cpu().numpy()
+    assert _rel_err(y, ref) <= TOL[act], (_rel_err(y, ref), act)
+
+
+def test_gemm_kernels_agree(oracle, monkeypatch):
+    """gemm3, gemm2 and the register-staged fallback (NAD_GEMM2_DISABLE=1) on the same fp16 inputs: each within fp32
+    accumulation noise of the oracle and of each other; gemm3 repeatable bit for bit."""
+    m, n, k = 700, 272, 1536
+    blob = _blob(oracle, n, k, 128, S4, BF16, True, 4, seed=11)
+    w = bestla.DeviceWeight(blob)
+    x = (torch.rand((m, k), device="cuda") - 0.5).half()
+    ref = oracle.forward(x.float().cpu().numpy(), blob, n, k)
+    y3 = w.forward(x).cpu().numpy()
+    for _ in range(3):
+        assert np.array_equal(w.forward(x).cpu().numpy(), y3)
+    monkeypatch.setenv("NAD_GEMM_KERNEL", "2")
+    y2 = w.forward(x).cpu().numpy()
+    monkeypatch.setenv("NAD_GEMM2_DISABLE", "1")
+    y1 = w.forward(x).cpu().numpy()
+    for y in (y3, y2, y1):
+        assert _rel_err(y, ref) <= 2e-5
+    assert _rel_err(y3, y2.astype(np.float64)) <= 2e-5
+
+
+def test_gemm_full_size_rows(oracle):
+    """BASELINE synthetic GEMM shape K = N = 4096 at M = 4096 (gemm3): oracle on sampled rows."""
+    n = k = 4096
+    blob = _blob(oracle, n, k, 128, S4, F16, False, 4, seed=42)
+    w = bestla.DeviceWeight(blob)
+    x = (torch.rand((4096, k), device="cuda") - 0.5).half()
+    y = w.forward(x).cpu().numpy()
+    rows = np.random.default_rng(1).choice(4096, size=16, replace=False)
+    ref = oracle.forward(x[rows].float().cpu().numpy(), blob, n, k)
+    assert _rel_err(y[rows], ref) <= 2e-5
+
+
+def test_gemm_strided_epilogues(oracle):
+    """lda > k input view, ldc > n output view, bias and residual epilogues on the prefill path."""
+    m, n, k = 96, 200, 1024
+    blob = _blob(oracle, n, k, 128, S4, F16, False, 4, seed=12)
+    w = bestla.DeviceWeight(blob)
+    rng = np.random.default_rng(4)
+    big = rng.uniform(-0.5, 0.5, size=(m, k + 40)).astype(np.float32)
+    x = torch.from_numpy(big).cuda()[:, 8:8 + k]
+    A = np.ascontiguousarray(big[:, 8:8 + k])
+    ref = oracle.forward(A, blob, n, k).astype(np.float64)
+    out = torch.zeros((m, n + 7), device="cuda")[:, :n]
+    w.forward(x, out=out)
+    assert _rel_err(out.cpu().numpy(), ref) <= TOL["fp32"]
+    b = rng.uniform(-1, 1, size=(n,)).astype(np.float32)
+    r = rng.uniform(-1, 1, size=(m, n)).astype(np.float32)
+    y = w.forward(x, epilogue=bestla.EPI_BIAS, bias=torch.from_numpy(b).cuda()).cpu().numpy()
+    assert _rel_err(y, ref + b) <= TOL["fp32"]
+    y = w.forward(x, epilogue=bestla.EPI_RES_ADD, residual=torch.from_numpy(r).cuda()).cpu().numpy()
+    assert _rel_err(y, ref + r) <= TOL["fp32"]
+
+
+@pytest.mark.parametrize("m", [32, 200])
+def test_gemm_fused_qkv_and_ffn(oracle, m):
+    """Fused QKV and gate/up (SiLU*mul) prefill convert the activation once and run the GEMM per weight."""
+    k = 512
+    blobs = [_blob(oracle, n, k, 128, S4, F16, False, 4, seed=40 + i) for i, n in enumerate((256, 128, 128))]
+    ws = [bestla.DeviceWeight(b) for b in blobs]
+    A = np.random.default_rng(m).uniform(-1, 1, size=(m, k)).astype(np.float32)
+    for y, b, n in zip(bestla.qkv_forward(torch.from_numpy(A).cuda(), *ws), blobs, (256, 128, 128)):
+        assert _rel_err(y.cpu().numpy(), oracle.forward(A, b, n, k)) <= TOL["fp32"]
+    fin, fmid, fout = 512, 768, 512
+    b1 = _blob(oracle, fmid, fin, 128, S4, F16, False, 4, seed=51)
+    b3 = _blob(oracle, fmid, fin, 128, S4, F16, False, 4, seed=53)
+    b2 = _blob(oracle, fout, fmid, 128, S4, F16, False, 4, seed=52)
+    w1, w2, w3 = (bestla.DeviceWeight(b) for b in (b1, b2, b3))
+    y = bestla.ffn_forward(torch.from_numpy(A).cuda(), w1, w2, w3, act="silu").cpu().numpy()
+    h1 = oracle.forward(A, b1, fmid, fin).astype(np.float64)
+    h3 = oracle.forward(A, b3, fmid, fin).astype(np.float64)
+    ref = oracle.forward((h1 / (1 + np.exp(-h1)) * h3).astype(np.float32), b2, fout, fmid)
+    assert _rel_err(y, ref) <= 2 * TOL["fp32"]

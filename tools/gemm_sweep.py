@@ -1,0 +1,59 @@
+"""Prefill GEMM sweep (development tool): TFLOP/s of one WOQ linear per Llama-2-7B shape at prefill M.
+
+Usage: python tools/gemm_sweep.py [--m 2048,4096] [--act fp16,fp32] [--shapes o,gate,down,lm_head] [--reps 20]
+       [--kernels 3,2]
+Each line: shape, M, activation dtype, kernel, average device time per forward (HIP events on the launch stream, back
+to back launches) and TFLOP/s (2*M*N*K / time).  fp32 activations include the one-pass fp16 conversion kernel.
+"""
+import argparse
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+SHAPES = {"o": (4096, 4096), "gate": (11008, 4096), "down": (4096, 11008), "lm_head": (32000, 4096)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--m", default="2048,4096")
+    ap.add_argument("--act", default="fp16,fp32")
+    ap.add_argument("--shapes", default="o,gate,down,lm_head")
+    ap.add_argument("--kernels", default="3,2")
+    ap.add_argument("--reps", type=int, default=20)
+    args = ap.parse_args()
+    import torch
+    from neural_amd import bestla
+    dev = torch.device("cuda:0")
+    print(torch.cuda.get_device_name(0), flush=True)
+    for name in args.shapes.split(","):
+        n, k = SHAPES[name]
+        w = bestla.DeviceWeight.synthetic(4, n, k, 128, "fp16", False, seed=3)
+        for m in (int(x) for x in args.m.split(",")):
+            for act in args.act.split(","):
+                dt = {"fp16": torch.float16, "fp32": torch.float32, "bf16": torch.bfloat16}[act]
+                x = (torch.rand((m, k), device=dev) - 0.5).to(dt)
+                out = torch.empty((m, n), device=dev)
+                s = torch.cuda.current_stream()
+                for kern in args.kernels.split(","):
+                    os.environ["NAD_GEMM_KERNEL"] = kern
+                    for _ in range(3):
+                        w.forward(x, out=out)
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    torch.cuda.synchronize()
+                    e0.record(s)
+                    for _ in range(args.reps):
+                        w.forward(x, out=out)
+                    e1.record(s)
+                    torch.cuda.synchronize()
+                    us = e0.elapsed_time(e1) * 1e3 / args.reps
+                    tf = 2.0 * m * n * k / us / 1e6
+                    print(f"{name:8s} N={n:5d} K={k:5d} M={m:5d} {act} gemm{kern}: {us:9.1f} us  {tf:7.1f} TFLOP/s",
+                          flush=True)
+                del x, out
+        del w
+
+
+if __name__ == "__main__":
+    main()
