@@ -493,6 +493,7 @@ static int run_gemm(const void* act, int act_t, int lda, int m, int k, const Dev
   a.ld_res = ld_res;
   a.aux = aux;
   a.ld_aux = ld_aux;
+  a.prio = env_int("NAD_GEMM3_PRIO", 0);
   a.w = view(w, out, ldo, bias, bias_ld);
   if (gemm2_ok(w, m)) {
     A16 own;

@@ -541,6 +541,7 @@ __global__ __launch_bounds__(512, 1) void woq_gemm3_kernel(GemmArgs a, const _Fl
     asm volatile("" ::: "memory");
   };
 
+  if (a.prio && wave >= 4) __builtin_amdgcn_s_setprio(1);  // static priority for the younger half (wave-uniform)
   for (int u = 0; u < nh; u += 2) {
     half(std::integral_constant<int, 0>{}, u);
     half(std::integral_constant<int, 1>{}, u + 1);

@@ -65,6 +65,7 @@ struct GemmArgs {
   int ld_res;
   const float* aux;
   int ld_aux;
+  int prio;             // gemm3: waves 4-7 at s_setprio 1 for the whole loop (NAD_GEMM3_PRIO)
   SkinnyWeight w;
 };
 

@@ -37,7 +37,8 @@ def main():
                 out = torch.empty((m, n), device=dev)
                 s = torch.cuda.current_stream()
                 for kern in args.kernels.split(","):
-                    os.environ["NAD_GEMM_KERNEL"] = kern
+                    os.environ["NAD_GEMM_KERNEL"] = kern[0]
+                    os.environ["NAD_GEMM3_PRIO"] = "1" if kern.endswith("p") else "0"
                     for _ in range(3):
                         w.forward(x, out=out)
                     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
