@@ -547,43 +547,63 @@ __global__ __launch_bounds__(512, 1) void woq_gemm3_kernel(GemmArgs a, const _Fl
     half(std::integral_constant<int, 1>{}, u + 1);
   }
 
-  // epilogue: C fragment (i, j): row = m0 + wm*128 + i*16 + kq*4 + rr, col = (bn*8 + wn*2 + j)*16 + nl
+  // epilogue through LDS (free after the loop: the last barrier retired every read and DMA): each wave transposes its
+  // 128 x 32 fp32 tile into row-major LDS rows (stride 36 floats), then writes whole 16-B row chunks -- the C fragment
+  // (4 rows of one column per lane) would otherwise leave as 64 scattered dword stores per lane, an issue-bound tail
+  // that all workgroups reach at once.
+  float* tw = reinterpret_cast<float*>(smem) + wave * (128 * 36);
+#pragma unroll
+  for (int i = 0; i < 8; i++)
+#pragma unroll
+    for (int j = 0; j < 2; j++)
+#pragma unroll
+      for (int rr = 0; rr < 4; rr++) tw[(i * 16 + kq * 4 + rr) * 36 + j * 16 + nl] = acc[i][j][rr];
   const int s0 = bn * 8 + wn * 2;
+  const int col0 = s0 * 16;
+  const bool vec_out = (reinterpret_cast<uintptr_t>(W.out) % 16 == 0) && (W.ldo % 4 == 0);
+#pragma unroll 4
+  for (int q = 0; q < 16; q++) {
+    const int c = q * 64 + lane;
+    const int rl = c >> 3, c4 = c & 7;
+    const int row = m0 + wm * 128 + rl;
+    const int n0 = col0 + c4 * 4;
+    const float4 t = *reinterpret_cast<const float4*>(tw + rl * 36 + c4 * 4);
+    if (row >= M || n0 >= W.n) continue;
+    float v[4] = {t.x, t.y, t.z, t.w};
 #pragma unroll
-  for (int j = 0; j < 2; j++) {
-    const int n = (s0 + j) * 16 + nl;
-    if (s0 + j >= ns || n >= W.n) continue;
-#pragma unroll
-    for (int i = 0; i < 8; i++) {
-#pragma unroll
-      for (int rr = 0; rr < 4; rr++) {
-        const int row = m0 + wm * 128 + i * 16 + kq * 4 + rr;
-        if (row >= M) continue;
-        float v = acc[i][j][rr];
-        switch (a.epi) {
-          case kEpiBias:
-            v += W.bias[size_t(row) * W.bias_ld + n];
-            break;
-          case kEpiAddGelu:
-            v = gelu_f(v + W.bias[size_t(row) * W.bias_ld + n]);
-            break;
-          case kEpiGelu:
-            v = gelu_f(v);
-            break;
-          case kEpiSilu:
-            v = silu_f(v);
-            break;
-          case kEpiResAdd:
-            v += a.res[size_t(row) * a.ld_res + n];
-            break;
-          case kEpiSiluMul:
-            v = a.aux[size_t(row) * a.ld_aux + n] * v;
-            break;
-          default:
-            break;
-        }
-        W.out[size_t(row) * W.ldo + n] = v;
+    for (int e = 0; e < 4; e++) {
+      const int n = n0 + e;
+      if (n >= W.n) break;
+      switch (a.epi) {
+        case kEpiBias:
+          v[e] += W.bias[size_t(row) * W.bias_ld + n];
+          break;
+        case kEpiAddGelu:
+          v[e] = gelu_f(v[e] + W.bias[size_t(row) * W.bias_ld + n]);
+          break;
+        case kEpiGelu:
+          v[e] = gelu_f(v[e]);
+          break;
+        case kEpiSilu:
+          v[e] = silu_f(v[e]);
+          break;
+        case kEpiResAdd:
+          v[e] += a.res[size_t(row) * a.ld_res + n];
+          break;
+        case kEpiSiluMul:
+          v[e] = a.aux[size_t(row) * a.ld_aux + n] * v[e];
+          break;
+        default:
+          break;
       }
+    }
+    float* o = W.out + size_t(row) * W.ldo + n0;
+    if (vec_out && n0 + 3 < W.n) {
+      *reinterpret_cast<float4*>(o) = make_float4(v[0], v[1], v[2], v[3]);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; e++)
+        if (n0 + e < W.n) o[e] = v[e];
     }
   }
 }
