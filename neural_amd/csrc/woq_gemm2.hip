@@ -614,9 +614,14 @@ hipError_t launch_gemm3(const GemmArgs& a, const _Float16* A16, int lda16, hipSt
   const int nbm = (a.M + g3::BM - 1) / g3::BM, nbn = (a.w.ns + 7) / 8;
   const bool tpg1 = a.w.bs == g3::KT;
   auto go = [&](auto k) -> hipError_t {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       g3::LDS_BYTES);
-    if (e != hipSuccess) return e;
+    static bool attr[2][2] = {};  // opt in to 155 KiB of dynamic LDS once per instantiation
+    bool& done = attr[a.w.zps != nullptr][a.w.bs == g3::KT];
+    if (!done) {
+      hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                         g3::LDS_BYTES);
+      if (e != hipSuccess) return e;
+      done = true;
+    }
     hipLaunchKernelGGL(k, dim3(nbm * nbn), dim3(512), g3::LDS_BYTES, st, a, A16, lda16);
     return hipGetLastError();
   };
