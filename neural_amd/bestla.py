@@ -258,6 +258,21 @@ def qkv_forward(x, wq, wk, wv, out=None, stream=None):
     return oq, ok, ov
 
 
+def ffn_gate_up(x, w1, w3, act="silu", tmp1=None, tmp2=None, stream=None):
+    """Gate/up half of the fused FFN: tmp2 = act(x.W1^T) * (x.W3^T), tmp1 = act(x.W1^T) (ip_fusion_ffn.cpp:407-433).
+    tmp1 may be None at M <= 16 (decode: one dual-weight launch); the prefill path needs it."""
+    torch = _torch()
+    m, fin = x.shape
+    fmid = w1.n
+    if tmp1 is None and m > 16:
+        tmp1 = torch.empty((m, fmid), dtype=torch.float32, device=x.device)
+    tmp2 = torch.empty((m, fmid), dtype=torch.float32, device=x.device) if tmp2 is None else tmp2
+    epi = EPI_SILU_MUL if act == "silu" else EPI_GELU_MUL
+    check(lib().nad_device_ffn_gate_up(_ptr(x), _act_code(x), w1.desc, w3.desc, _ptr(tmp1), _ptr(tmp2), m, fin, fmid,
+                                       x.stride(0), epi, _stream(stream)), "nad_device_ffn_gate_up")
+    return tmp2
+
+
 def ffn_forward(x, w1, w2, w3, act="silu", tmp1=None, tmp2=None, out=None, stream=None):
     """Fused FFN: out = (act(x.W1^T) * (x.W3^T)) . W2^T  (ip_fusion_ffn.cpp:407-457)."""
     torch = _torch()

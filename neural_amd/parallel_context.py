@@ -14,7 +14,7 @@ import torch.distributed as dist
 class ParallelContext:
     """init_parallel_context() / get_tp_size / get_tp_rank / is_master / barrier / broadcast / alltoall / reduce_add"""
 
-    def __init__(self, backend=None, group=None):
+    def __init__(self, backend=None, group=None, device=None):
         if not dist.is_initialized():
             if backend is None:
                 backend = "nccl" if torch.cuda.is_available() else "gloo"
@@ -22,7 +22,8 @@ class ParallelContext:
             os.environ.setdefault("MASTER_PORT", "29517")
             os.environ.setdefault("RANK", "0")
             os.environ.setdefault("WORLD_SIZE", "1")
-            dist.init_process_group(backend)
+            kw = {"device_id": torch.device("cuda", device)} if (backend == "nccl" and device is not None) else {}
+            dist.init_process_group(backend, **kw)
         self.group = group
 
     def get_tp_size(self):
@@ -52,6 +53,16 @@ class ParallelContext:
             send = recv
         dist.all_reduce(send, op=dist.ReduceOp.SUM, group=self.group)
         return send
+
+    def max_over_ranks(self, value):
+        t = torch.tensor([float(value)], dtype=torch.float64,
+                         device="cuda" if dist.get_backend(self.group) == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+        return float(t.item())
+
+    def destroy(self):
+        if dist.is_initialized():
+            dist.destroy_process_group()
 
     def all_gather_cols(self, local, sizes):
         """concatenate column shards [M, n_r] of every rank into [M, sum n_r] (column-parallel output gather)."""
