@@ -107,6 +107,31 @@ bool BTLAGemmBatchDriver(const size_t M, const size_t N, const size_t K, const s
                          const BTLA_GEMM_DATA_PACKED_PARAMS* DataParams, int8_t* WorkSpace,
                          void* ThreadPool); /* bestla_gemm.h:54-55 */
 
+/* ===== tensor-parallel communicator: neural_speed/core/parallel_context.h:21-48 (oneCCL/MPI + SHM in the reference,
+ * parallel_context.cpp:19-159, shared_memory_ccl.hpp:100-139).  Implemented in csrc/parallel_context.hip: TCP
+ * rendezvous from RANK/WORLD_SIZE (or OMPI_/PMI_ env), RCCL on a context stream for device buffers, a one-shot IPC
+ * peer-buffer all-reduce for small device messages, host buffers staged through the device (or carried over the
+ * rendezvous sockets when no GPU is present).  `count` is an element count (the reference passes byte counts at
+ * ne_layers.c:5474 -- callers of this library pass elements). */
+typedef struct parallel_context parallel_context;
+parallel_context* init_parallel_context(void);   /* parallel_context.h:40 (process-wide singleton) */
+int get_tp_size(parallel_context* p);             /* :41 */
+int get_tp_rank(parallel_context* p);             /* :42 */
+bool is_master(parallel_context* p);              /* :43 */
+void barrier(parallel_context* p);                /* :44 (also drains this rank's device work) */
+void broadcast(parallel_context* p, float* buffer, size_t count);                           /* :45, root 0 */
+void alltoall(parallel_context* p, float* send_buffer, float* recv_buffer, size_t count);   /* :46, count per rank */
+void reduce_add(parallel_context* p, float* send_buffer, float* recv_buffer, size_t count); /* :47, sum */
+/* native: sum all-reduce of device buffers on `stream` (a hipStream_t; NULL = the null stream, as everywhere in this
+ * library), asynchronous, graph-capturable */
+int nad_pc_allreduce_f32(parallel_context* p, const float* send, float* recv, size_t count, void* stream);
+int nad_pc_set_stream(parallel_context* p, void* stream);   /* stream of the reference entry points (default NULL) */
+double nad_pc_max_f64(parallel_context* p, double v);        /* max over ranks (host value; bench timing) */
+int nad_pc_status(parallel_context* p);   /* 0 ok, 1 a one-shot all-reduce gave up waiting for a peer */
+int nad_pc_info(parallel_context* p);     /* bit0 GPU transport, bit1 one-shot IPC path, bit2 RCCL communicator */
+const char* nad_pc_last_error(parallel_context* p);
+void nad_pc_destroy(parallel_context* p);
+
 /* ===== native extensions (no reference counterpart) */
 #define NAD_ACT_F32 0
 #define NAD_ACT_F16 1

@@ -77,6 +77,21 @@ SIGNATURES = {
     "nad_chain_run": (_i, [_p, _p]),
     "nad_chain_status": (_i, [_p]),
     "nad_chain_destroy": (None, [_p]),
+    "init_parallel_context": (_p, []),
+    "get_tp_size": (_i, [_p]),
+    "get_tp_rank": (_i, [_p]),
+    "is_master": (_b, [_p]),
+    "barrier": (None, [_p]),
+    "broadcast": (None, [_p, _p, _sz]),
+    "alltoall": (None, [_p, _p, _p, _sz]),
+    "reduce_add": (None, [_p, _p, _p, _sz]),
+    "nad_pc_allreduce_f32": (_i, [_p, _p, _p, _sz, _p]),
+    "nad_pc_set_stream": (_i, [_p, _p]),
+    "nad_pc_max_f64": (C.c_double, [_p, C.c_double]),
+    "nad_pc_status": (_i, [_p]),
+    "nad_pc_info": (_i, [_p]),
+    "nad_pc_last_error": (C.c_char_p, [_p]),
+    "nad_pc_destroy": (None, [_p]),
 }
 
 

@@ -1,80 +1,110 @@
-"""Tensor-parallel communicator: the reference's parallel_context (neural_speed/core/parallel_context.h:28-52,
-parallel_context.cpp:19-137, oneCCL over MPI or a same-host SHM all-reduce) re-hosted on torch.distributed.
+"""Tensor-parallel communicator: Python face of the library's C-ABI parallel context (include/neural_amd.h,
+csrc/parallel_context.hip), which replaces the reference's neural_speed/core/parallel_context.{h,cpp}
+(init_parallel_context / get_tp_size / get_tp_rank / is_master / barrier / broadcast / alltoall / reduce_add).
 
-One process per GPU; backend "nccl" is RCCL on ROCm (point-to-point xGMI between the 8 MI355X of a node), "gloo"
-on CPU.  Counts are element counts of the tensors passed (the reference passes byte counts as element counts at
-ne_layers.c:5474 / llama.cpp:185 -- not replicated).
+One process per GPU.  Device tensors are reduced on the caller's current HIP stream (one-shot IPC all-reduce for small
+messages, RCCL over xGMI for large ones); host tensors go through the reference's synchronous entry points.  Without a
+GPU (transport="tcp") the rendezvous sockets carry host tensors, which is how the CPU tests run the N>1 logic.
+Element counts, not byte counts (the reference passes bytes as elements at ne_layers.c:5474 -- not replicated).
 """
+import ctypes as C
 import os
 
-import torch
-import torch.distributed as dist
+from ._lib import lib
 
 
 class ParallelContext:
-    """init_parallel_context() / get_tp_size / get_tp_rank / is_master / barrier / broadcast / alltoall / reduce_add"""
-
-    def __init__(self, backend=None, group=None, device=None):
-        if not dist.is_initialized():
-            if backend is None:
-                backend = "nccl" if torch.cuda.is_available() else "gloo"
-            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-            os.environ.setdefault("MASTER_PORT", "29517")
-            os.environ.setdefault("RANK", "0")
-            os.environ.setdefault("WORLD_SIZE", "1")
-            kw = {"device_id": torch.device("cuda", device)} if (backend == "nccl" and device is not None) else {}
-            dist.init_process_group(backend, **kw)
-        self.group = group
+    def __init__(self, transport=None, keep_device=True):
+        """transport: None (GPU when present) or "tcp" (host tensors over the rendezvous sockets, no GPU).
+        keep_device: use the HIP device the caller selected (torch.cuda.set_device) instead of LOCAL_RANK % devices."""
+        if transport:
+            os.environ["NAD_PC_TRANSPORT"] = transport
+        if keep_device:
+            os.environ["NAD_PC_KEEP_DEVICE"] = "1"
+        L = self.L = lib()
+        self.p = L.init_parallel_context()
+        if not self.p:
+            raise RuntimeError("init_parallel_context failed (see stderr)")
 
     def get_tp_size(self):
-        return dist.get_world_size(self.group)
+        return self.L.get_tp_size(self.p)
 
     def get_tp_rank(self):
-        return dist.get_rank(self.group)
+        return self.L.get_tp_rank(self.p)
 
     def is_master(self):
-        return self.get_tp_rank() == 0
+        return bool(self.L.is_master(self.p))
+
+    def info(self):
+        v = self.L.nad_pc_info(self.p)
+        return {"gpu": bool(v & 1), "oneshot": bool(v & 2), "rccl": bool(v & 4)}
+
+    def _err(self, what):
+        e = self.L.nad_pc_last_error(self.p)
+        return RuntimeError(f"{what} failed: {e.decode() if e else ''}")
+
+    @staticmethod
+    def _f32(t):
+        import torch
+        if t.dtype != torch.float32 or not t.is_contiguous():
+            raise TypeError("parallel_context buffers are contiguous float32 tensors")
+        return C.c_void_p(t.data_ptr())
 
     def barrier(self):
-        dist.barrier(self.group)
+        self.L.barrier(self.p)
 
     def broadcast(self, buffer, root=0):
-        dist.broadcast(buffer, root, group=self.group)
+        """from rank 0 (the reference always broadcasts from the master, parallel_context.cpp:58-61)"""
+        if root != 0:
+            raise ValueError("broadcast root must be 0 (reference semantics)")
+        self.L.broadcast(self.p, self._f32(buffer), buffer.numel())
         return buffer
 
     def alltoall(self, send, recv):
-        dist.all_to_all_single(recv, send, group=self.group)
+        """send/recv hold world blocks of send.numel() // world elements each"""
+        w = self.get_tp_size()
+        self.L.alltoall(self.p, self._f32(send), self._f32(recv), send.numel() // w)
+        if send.is_cuda:
+            import torch
+            torch.cuda.synchronize()
         return recv
 
-    def reduce_add(self, send, recv=None):
-        """sum over ranks (parallel_context.cpp:47-57); in place when recv is None or is send."""
-        if recv is not None and recv is not send:
-            recv.copy_(send)
-            send = recv
-        dist.all_reduce(send, op=dist.ReduceOp.SUM, group=self.group)
-        return send
+    def reduce_add(self, send, recv=None, stream=None):
+        """sum over ranks; in place when recv is None.  Device tensors: asynchronous on `stream` (default: torch's
+        current stream) -- graph-capturable; host tensors: synchronous (reference reduce_add)."""
+        recv = send if recv is None else recv
+        if send.is_cuda:
+            import torch
+            s = stream if stream is not None else torch.cuda.current_stream()
+            rc = self.L.nad_pc_allreduce_f32(self.p, self._f32(send), self._f32(recv), send.numel(),
+                                             C.c_void_p(s.cuda_stream))
+            if rc != 0:
+                raise self._err("nad_pc_allreduce_f32")
+        else:
+            self.L.reduce_add(self.p, self._f32(send), self._f32(recv), send.numel())
+        return recv
+
+    def status(self):
+        return self.L.nad_pc_status(self.p)
 
     def max_over_ranks(self, value):
-        t = torch.tensor([float(value)], dtype=torch.float64,
-                         device="cuda" if dist.get_backend(self.group) == "nccl" else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
-        return float(t.item())
-
-    def destroy(self):
-        if dist.is_initialized():
-            dist.destroy_process_group()
+        return float(self.L.nad_pc_max_f64(self.p, float(value)))
 
     def all_gather_cols(self, local, sizes):
-        """concatenate column shards [M, n_r] of every rank into [M, sum n_r] (column-parallel output gather)."""
-        world = self.get_tp_size()
-        parts = [torch.empty((local.shape[0], s), dtype=local.dtype, device=local.device) for s in sizes]
-        if len(set(sizes)) == 1:
-            dist.all_gather(parts, local.contiguous(), group=self.group)
-        else:  # uneven shards: pad to the max width
-            w = max(sizes)
-            pad = torch.zeros((local.shape[0], w), dtype=local.dtype, device=local.device)
-            pad[:, :local.shape[1]] = local
-            full = [torch.empty_like(pad) for _ in range(world)]
-            dist.all_gather(full, pad, group=self.group)
-            parts = [f[:, :s] for f, s in zip(full, sizes)]
-        return torch.cat(parts, dim=1)
+        """concatenate column shards [M, n_r] of every rank into [M, sum n_r] (column-parallel output gather), through
+        alltoall: every rank sends its (padded) shard to every rank."""
+        import torch
+        w = self.get_tp_size()
+        m, width = local.shape[0], max(sizes)
+        pad = torch.zeros((m, width), dtype=torch.float32, device=local.device)
+        pad[:, :local.shape[1]] = local
+        send = pad.reshape(1, -1).repeat(w, 1).contiguous()
+        recv = torch.empty_like(send)
+        self.alltoall(send, recv)
+        blocks = recv.reshape(w, m, width)
+        return torch.cat([blocks[r, :, :sizes[r]] for r in range(w)], dim=1)
+
+    def destroy(self):
+        if self.p:
+            self.L.nad_pc_destroy(self.p)
+            self.p = None

@@ -1,14 +1,14 @@
-"""Tensor-parallel composition on CPU: 2 (and 4) gloo ranks, exact blob shards, row/column-parallel linears,
-reduce_add.  The per-rank matmul is the oracle (this exercises the TP partition + communication logic that bench.py
-and neural_amd.tp run over RCCL on the GPUs); TP=W must reproduce TP=1 up to the all-reduce summation order.
-Pattern of the reference's TP test (tests/model-test/run_tp.sh: 2 ranks on one host vs 1 rank)."""
+"""Tensor-parallel composition on CPU: 2 (and 4) ranks through the library's C-ABI parallel context
+(init_parallel_context / reduce_add / broadcast / alltoall / barrier, csrc/parallel_context.hip) over its TCP transport,
+exact blob shards, row/column-parallel linears.  The per-rank matmul is the oracle here (no GPU in this container;
+tests/test_tp_gpu.py runs the same composition with the HIP kernels); TP=W must reproduce TP=1 up to the all-reduce
+summation order.  Pattern of the reference's TP test (tests/model-test/run_tp.sh: 2 ranks on one host vs 1 rank)."""
 import os
 import socket
 
 import numpy as np
 import pytest
 import torch
-import torch.distributed as dist
 import torch.multiprocessing as mp
 
 
@@ -54,14 +54,15 @@ def _block(x, wq, wo, w1, w3, w2, ctx, world):
 
 
 def _worker(rank, world, port, q):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    os.environ.update(MASTER_ADDR="127.0.0.1", NAD_TP_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
     torch.set_num_threads(1)
     try:
         from neural_amd.parallel_context import ParallelContext
         from neural_amd import tp
         from tests.oracle_lib import Oracle
         o = Oracle.get()
-        ctx = ParallelContext("gloo")
+        ctx = ParallelContext("tcp")
         assert ctx.get_tp_size() == world and ctx.get_tp_rank() == rank
         d, f, gs = 128, 320, 32  # hidden, ffn (10 groups of 32: uneven K shards at world 4)
         names = {"wq": (".attention.wq.weight", d, d), "wo": (".attention.wo.weight", d, d),
@@ -90,12 +91,14 @@ def _worker(rank, world, port, q):
         expect = torch.cat([torch.arange(2, dtype=torch.float32) + 2 * rank + 100 * r for r in range(world)])
         assert torch.equal(recv, expect)
         yq = layers["wq"](x)
-        sizes = [None] * world
-        dist.all_gather_object(sizes, yq.shape[1])
+        sizes = [hi - lo for lo, hi in (tp.shard_blob(_blob(100, d, d, gs), tp.TP_1D_ROW, r, world, unit=gs)[1]
+                                        for r in range(world))]
+        assert sizes[rank] == yq.shape[1]
         full_q = ctx.all_gather_cols(yq, sizes)
+        assert ctx.max_over_ranks(float(rank)) == world - 1
         ctx.barrier()
         q.put((rank, y.numpy(), full_q.numpy()))
-        dist.destroy_process_group()
+        ctx.destroy()
     except Exception as e:  # surface the failure to the parent
         import traceback
         q.put((rank, "ERR", traceback.format_exc() + str(e)))
