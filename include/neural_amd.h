@@ -183,6 +183,9 @@ int nad_synthetic_weight(void* devstor, void* deviceptr, size_t capacity, int bi
                          int scale_t, int asym, uint64_t seed, void* queue);
 /* device bytes of nad_synthetic_weight's layout */
 size_t nad_synthetic_weight_size(int bits, int n, int k, int blocksize, int scale_t, int asym);
+/* drop every device copy the host-pointer ABI cached (weights are keyed by blob address + content fingerprint and
+ * re-uploaded when a pack entry rewrites a blob) */
+void nad_host_cache_clear(void);
 /* host convenience: (re)pack one blob into fp32 dequantized [K][N] from the device tile layout (round-trip check) */
 int nad_device_unpack_fp32(const void* devstor, float* host_out, void* queue);
 

@@ -10,6 +10,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # NAD_LIB_PATH: development override (tools/trace_skinny.py loads the phase-trace build)
 LIB_PATH = os.environ.get("NAD_LIB_PATH") or os.path.join(_HERE, "libneural_amd.so")
 HEADER = os.path.join(os.path.dirname(_HERE), "include", "neural_amd.h")
+HEADERS = [HEADER, os.path.join(os.path.dirname(_HERE), "include", "neural_amd_ne.h")]
 
 _p = C.c_void_p
 _i = C.c_int
@@ -73,6 +74,7 @@ SIGNATURES = {
     "nad_synthetic_weight": (_i, [_p, _p, _sz, _i, _i, _i, _i, _i, _i, _u64, _p]),
     "nad_synthetic_weight_size": (_sz, [_i, _i, _i, _i, _i, _i]),
     "nad_device_unpack_fp32": (_i, [_p, _p, _p]),
+    "nad_host_cache_clear": (None, []),
     "nad_chain_create": (_p, [_p, _i, _i]),
     "nad_chain_run": (_i, [_p, _p]),
     "nad_chain_status": (_i, [_p]),
@@ -92,6 +94,23 @@ SIGNATURES = {
     "nad_pc_info": (_i, [_p]),
     "nad_pc_last_error": (C.c_char_p, [_p]),
     "nad_pc_destroy": (None, [_p]),
+    # include/neural_amd_ne.h
+    "bestla_timer": (None, [_b]),
+    "bestla_parallel_for": (None, [_p, _p, _p]),
+    "bestla_layernormalization": (None, [_i, _i, _b, C.c_float, _p, _p]),
+    "bestla_mul": (None, [_i, _i, _p, _p, _i, _p]),
+    "bestla_add": (None, [_i, _i, _p, _p, _i, _p]),
+    "bestla_backend_support": (_i, [_p, _p, _i]),
+    "bestla_support": (_b, [_p, _i, _p, _p]),
+    "bestla_device_mul_f32": (None, [_p, _p, _p, _p]),
+    "bestla_device_add_f32": (None, [_p, _p, _p, _p]),
+    "bestla_device_elewise_f32": (None, [_p, _p, _p]),
+    "bestla_device_rms_norm_f32": (None, [_p, _p, _p]),
+    "bestla_device_rope_f32": (None, [_p, _p, _p, _p]),
+    "bestla_device_dup_f32": (None, [_p, _p, _p]),
+    "bestla_device_mha_f32": (None, [_p, _p, _p, _p, _p]),
+    "nad_bind_workspace": (_i, [_p, _p, _sz]),
+    "nad_device_workspace_size": (_sz, [_i, _i]),
 }
 
 
@@ -127,11 +146,11 @@ def lib():
 
 
 def header_symbols():
-    """Function names declared in include/neural_amd.h."""
-    text = open(HEADER).read()
+    """Function names declared in the C headers include/neural_amd.h and include/neural_amd_ne.h."""
+    text = "\n".join(open(h).read() for h in HEADERS)
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
     names = re.findall(r"\b([A-Za-z_][A-Za-z0-9_]*)\s*\(", text)
-    skip = {"if", "defined", "sizeof", "extern"}
+    skip = {"if", "defined", "sizeof", "extern", "void"}
     return sorted({n for n in names if n not in skip and not n.isupper()})
 
 

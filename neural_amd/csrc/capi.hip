@@ -418,30 +418,68 @@ static int run_skinny(const void* act, int act_t, int lda, int m, int k, int nw,
   return 0;
 }
 
-// Grow-only device scratch for the prefill GEMM's fp16 copy of the activations (never freed: one per process, sized
-// by the largest prefill).  Growing is refused while the stream is being captured into a graph.
-static void* scratch(size_t bytes, hipStream_t st) {
-  static std::mutex mu;
-  static void* buf = nullptr;
-  static size_t cap = 0;
-  std::lock_guard<std::mutex> lk(mu);
-  if (bytes <= cap) return buf;
+// Device workspace for the prefill GEMM's fp16 copy of the activations, in order of preference:
+//   1. the caller's workspace of a reference entry point (bestla_device_f32f32_forward(..., workspace, queue): the
+//      graph's dev_work, sized by bestla_support -> nad_device_workspace_size, ne_layers.c:11947-11967);
+//   2. a workspace the caller bound to the stream (nad_bind_workspace; the nad_device_* entries take no argument);
+//   3. a per-stream grow-only scratch owned by the library.  It grows only outside graph capture and a buffer is never
+//      freed (a captured graph may reference it); a capture that would need growth fails loudly instead of switching
+//      kernels.
+namespace {
+struct WsRef {
+  void* ptr = nullptr;
+  size_t bytes = 0;
+};
+thread_local WsRef t_call_ws;  // set by the reference entry points for the duration of one call
+std::mutex g_ws_mu;
+std::unordered_map<hipStream_t, WsRef> g_bound_ws;
+std::unordered_map<hipStream_t, WsRef> g_scratch;
+std::vector<void*> g_scratch_all;  // every scratch buffer ever handed out (kept for captured graphs)
+
+struct CallWorkspace {  // RAII binding of a reference call's workspace argument
+  CallWorkspace(void* p, size_t b) { t_call_ws = WsRef{p, p ? b : 0}; }
+  ~CallWorkspace() { t_call_ws = WsRef{}; }
+};
+}  // namespace
+
+extern "C" size_t nad_device_workspace_size(int m, int k);
+
+extern "C" int nad_bind_workspace(void* queue, void* ptr, size_t bytes) {
+  std::lock_guard<std::mutex> lk(g_ws_mu);
+  hipStream_t st = static_cast<hipStream_t>(queue);
+  if (!ptr || !bytes)
+    g_bound_ws.erase(st);
+  else
+    g_bound_ws[st] = WsRef{ptr, bytes};
+  return 0;
+}
+
+static void* workspace_for(size_t bytes, hipStream_t st) {
+  if (t_call_ws.ptr && t_call_ws.bytes >= bytes) return t_call_ws.ptr;
+  std::lock_guard<std::mutex> lk(g_ws_mu);
+  auto b = g_bound_ws.find(st);
+  if (b != g_bound_ws.end() && b->second.bytes >= bytes) return b->second.ptr;
+  WsRef& sc = g_scratch[st];
+  if (sc.bytes >= bytes) return sc.ptr;
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-  if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
-  if (hipStreamSynchronize(st) != hipSuccess) return nullptr;
-  if (buf) (void)hipFree(buf);
-  buf = nullptr;
-  cap = 0;
-  if (hipMalloc(&buf, bytes) != hipSuccess) {
-    buf = nullptr;
+  if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) {
+    set_err("prefill under graph capture needs %zu bytes of device workspace: bind one with nad_bind_workspace (or run "
+            "the same shape once before capturing)", bytes);
     return nullptr;
   }
-  cap = bytes;
-  return buf;
+  void* p = nullptr;
+  const size_t want = std::max(bytes, sc.bytes * 2);
+  if (hipMalloc(&p, want) != hipSuccess) {
+    set_err("workspace allocation of %zu bytes failed", want);
+    return nullptr;
+  }
+  g_scratch_all.push_back(p);
+  sc = WsRef{p, want};
+  return p;
 }
 
 // fp16 activations for the pipelined prefill GEMM (woq_gemm2.hip): the caller's rows when they already are fp16,
-// aligned, unshuffled and tile-padded, else one conversion pass into the scratch.  One conversion serves every GEMM
+// aligned, unshuffled and tile-padded, else one conversion pass into the workspace.  One conversion serves every GEMM
 // that reads the same activations (the QKV and gate/up fusions).
 struct A16 {
   const _Float16* p = nullptr;
@@ -455,7 +493,7 @@ static bool gemm2_ok(const DeviceWeight& w, int m) {
          (tpg & (tpg - 1)) == 0 && m >= 32 && uint64_t(m) * uint64_t(w.nt) * 256 < (1ull << 32);
 }
 
-// 1 ready, 0 unavailable (fall back to the register-staged GEMM), -1 launch error
+// 1 ready, -1 error (no workspace under capture, launch error)
 static int prepare_a16(A16& r, const void* act, int act_t, int lda, int m, int k, const DeviceWeight& w,
                        hipStream_t st) {
   const int kp = w.nt * 128;
@@ -466,8 +504,8 @@ static int prepare_a16(A16& r, const void* act, int act_t, int lda, int m, int k
     r.ld = lda;
     return 1;
   }
-  _Float16* buf = static_cast<_Float16*>(scratch(size_t(m) * kp * 2, st));
-  if (!buf) return 0;
+  _Float16* buf = static_cast<_Float16*>(workspace_for(size_t(m) * kp * 2, st));
+  if (!buf) return -1;
   hipError_t e = launch_cvt_act(act, act_t, lda, m, k, kp, w.shuffle, buf, st);
   if (e != hipSuccess) {
     set_err("activation conversion launch failed: %s", hipGetErrorString(e));
@@ -497,21 +535,17 @@ static int run_gemm(const void* act, int act_t, int lda, int m, int k, const Dev
   a.w = view(w, out, ldo, bias, bias_ld);
   if (gemm2_ok(w, m)) {
     A16 own;
-    int rc = 1;
     if (!pre || pre->kp != w.nt * 128 || w.shuffle) {
-      rc = prepare_a16(own, act, act_t, lda, m, k, w, st);
+      if (prepare_a16(own, act, act_t, lda, m, k, w, st) < 0) return -1;
       pre = &own;
     }
-    if (rc < 0) return -1;
-    if (rc > 0) {
-      hipError_t e = env_int("NAD_GEMM_KERNEL", 3) == 2 ? launch_gemm2(a, pre->p, pre->ld, st)
-                                                        : launch_gemm3(a, pre->p, pre->ld, st);
-      if (e != hipSuccess) {
-        set_err("gemm2 kernel launch failed: %s", hipGetErrorString(e));
-        return -1;
-      }
-      return 0;
+    hipError_t e = env_int("NAD_GEMM_KERNEL", 3) == 2 ? launch_gemm2(a, pre->p, pre->ld, st)
+                                                      : launch_gemm3(a, pre->p, pre->ld, st);
+    if (e != hipSuccess) {
+      set_err("gemm2 kernel launch failed: %s", hipGetErrorString(e));
+      return -1;
     }
+    return 0;
   }
   hipError_t e = launch_gemm(a, w.bits, act_t, st);
   if (e != hipSuccess) {
@@ -560,6 +594,7 @@ extern "C" int nad_device_forward(const void* act, int act_dtype, const void* de
 
 extern "C" void bestla_device_f32f32_forward(float* activation, void* weiptr, float* output, int _m, int _n, int _k,
                                              int lda, int ldo, void* workspace, void* queue) {
+  CallWorkspace cw(workspace, nad_device_workspace_size(_m, _k));
   if (nad_device_forward(activation, kActF32, weiptr, output, _m, _n, _k, lda, ldo, kEpiNone, nullptr, 0, nullptr, 0,
                          queue) != 0)
     report("bestla_device_f32f32_forward");
@@ -587,9 +622,8 @@ extern "C" int nad_device_qkv_forward(const void* act, int act_dtype, const void
   A16 pre;
   const A16* pp = nullptr;
   if (gemm2_ok(*ws[0], m) && !ws[0]->shuffle) {
-    const int rc = prepare_a16(pre, act, act_dtype, lda, m, k, *ws[0], st);
-    if (rc < 0) return -1;
-    if (rc > 0) pp = &pre;
+    if (prepare_a16(pre, act, act_dtype, lda, m, k, *ws[0], st) < 0) return -1;
+    pp = &pre;
   }
   for (int i = 0; i < 3; i++)
     if (run_gemm(act, act_dtype, lda, m, k, *ws[i], outs[i], ldos[i], kEpiNone, nullptr, 0, nullptr, 0, nullptr, 0,
@@ -628,9 +662,8 @@ extern "C" int nad_device_ffn_gate_up(const void* act, int act_dtype, const void
   A16 pre;
   const A16* pp = nullptr;
   if (gemm2_ok(*w1, m) && !w1->shuffle) {
-    const int rc = prepare_a16(pre, act, act_dtype, lda, m, fin, *w1, st);
-    if (rc < 0) return -1;
-    if (rc > 0) pp = &pre;
+    if (prepare_a16(pre, act, act_dtype, lda, m, fin, *w1, st) < 0) return -1;
+    pp = &pre;
   }
   if (run_gemm(act, act_dtype, lda, m, fin, *w1, tmp1, fmid, e1, nullptr, 0, nullptr, 0, nullptr, 0, st, pp))
     return -1;
@@ -925,6 +958,7 @@ struct CachedWeight {
   DeviceWeight w;
   void* mem;
   uint64_t size;
+  uint64_t fingerprint;
 };
 struct HostCtx {
   std::mutex mu;
@@ -943,21 +977,41 @@ NadDevice* host_device() {
   if (!c.dev) c.dev = static_cast<NadDevice*>(bestla_create_device(false));
   return c.dev;
 }
-// device copy of a host blob, created on first use (a blob's bytes are immutable once packed)
-const DeviceWeight* cached_weight(void* blob) {
+// FNV-1a over the blob header, the whole correction section (scales / zero points: 1/32 of an int4 blob) and every
+// 4 KiB-th dword of the packed codes: a re-pack into the same buffer changes the scales, so it changes the key
+uint64_t blob_fingerprint(const Blob& b, const uint8_t* base) {
+  uint64_t h = 1469598103934665603ull;
+  auto mix = [&](const uint8_t* p, size_t n) {
+    for (size_t i = 0; i < n; i++) h = (h ^ p[i]) * 1099511628211ull;
+  };
+  mix(base, 64);
+  mix(base + b.s_off, b.s_size);
+  if (b.asym) mix(base + b.z_off, b.z_size);
+  for (uint64_t o = 0; o + 4 <= b.q_size; o += 4096) mix(base + b.q_off + o, 4);
+  mix(reinterpret_cast<const uint8_t*>(&b.size), sizeof(b.size));
+  return h;
+}
+void drop_cached(const void* blob) {
   HostCtx& c = hctx();
   auto it = c.cache.find(blob);
+  if (it == c.cache.end()) return;
+  if (c.dev) (void)hipStreamSynchronize(c.dev->stream);
+  (void)hipFree(it->second.mem);
+  c.cache.erase(it);
+}
+// device copy of a host blob, created on first use and refreshed when the blob's bytes change
+const DeviceWeight* cached_weight(void* blob) {
+  HostCtx& c = hctx();
   Blob b;
   std::string err;
   if (!b.parse(blob, &err)) {
     set_err("%s", err.c_str());
     return nullptr;
   }
-  if (it != c.cache.end() && it->second.size == b.size) return &it->second.w;
-  if (it != c.cache.end()) {
-    (void)hipFree(it->second.mem);
-    c.cache.erase(it);
-  }
+  const uint64_t fp = blob_fingerprint(b, static_cast<const uint8_t*>(blob));
+  auto it = c.cache.find(blob);
+  if (it != c.cache.end() && it->second.size == b.size && it->second.fingerprint == fp) return &it->second.w;
+  drop_cached(blob);
   NadDevice* d = host_device();
   if (!d) return nullptr;
   size_t need = nad_device_weight_size(blob);
@@ -974,6 +1028,7 @@ const DeviceWeight* cached_weight(void* blob) {
   }
   cw.mem = mem;
   cw.size = b.size;
+  cw.fingerprint = fp;
   auto res = c.cache.emplace(blob, cw);
   return &res.first->second.w;
 }
@@ -1261,6 +1316,21 @@ extern "C" void bestla_fusion_FFN_Add_GeLu_f32f32_forward(float* activation, voi
             "bestla_fusion_FFN_Add_GeLu_f32f32_forward");
 }
 
+// a pack entry is about to (re)write `blob`: forget its device copy
+static void invalidate_host_weight(const void* blob) {
+  std::lock_guard<std::mutex> lk(hctx().mu);
+  drop_cached(blob);
+}
+
+// release every cached device weight of the host-pointer ABI (e.g. before freeing host blobs)
+extern "C" void nad_host_cache_clear(void) {
+  HostCtx& c = hctx();
+  std::lock_guard<std::mutex> lk(c.mu);
+  if (c.dev) (void)hipStreamSynchronize(c.dev->stream);
+  for (auto& kv : c.cache) (void)hipFree(kv.second.mem);
+  c.cache.clear();
+}
+
 // ------------------------------------------------------------------------------------------------ pack API
 extern "C" size_t BTLAGemmPackBSize(size_t N, size_t K, size_t BlkSize, uint32_t QuantType, uint32_t ScaleDtype,
                                     bool isAsym, int CompType, int* shuffle_indice) {
@@ -1281,6 +1351,7 @@ extern "C" bool BTLAGemmQuantPackB(void* PackedBuf, const float* FpData, size_t 
   uint64_t core = select_core(CompType, QuantType, int(BlkSize), isAsym, host_isa_profile());
   if (!core) return false;
   Blob b = Blob::describe(int(N), int(K), int(BlkSize), QuantType, ScaleDtype, isAsym, core, false);
+  invalidate_host_weight(PackedBuf);
   b.write_header(static_cast<int8_t*>(PackedBuf));
   // quantizeWeight works on [K][N]; packTransposeWeight first transposes a torch-layout [N][ldb] matrix
   std::vector<float> kn;
@@ -1315,6 +1386,7 @@ extern "C" bool BTLAGemmPackB(void* PackedBuf, const int8_t* QData, const float*
   if (!core) return false;
   Blob b = Blob::describe(int(N), int(K), int(BlkSize), QuantType, ScaleDtype, isAsym, core,
                           shuffle_indice != nullptr);
+  invalidate_host_weight(PackedBuf);
   b.write_header(static_cast<int8_t*>(PackedBuf));
   std::string err;
   if (!pack_quantized(b, static_cast<int8_t*>(PackedBuf), QData, int(ldb), Scales, isAsym ? Zp : nullptr,
@@ -1369,6 +1441,7 @@ extern "C" void bestla_packweight_copyattr(const float* f32ptr, void* dstpr, int
     return;
   }
   Blob b = Blob::describe(n, k, s.blocksize >= s.kpad ? -1 : s.blocksize, s.qtype, s.scale_t, s.asym, s.core_id, false);
+  invalidate_host_weight(dstpr);
   b.write_header(static_cast<int8_t*>(dstpr));
   std::vector<float> kn(size_t(k) * n);
   for (int kk = 0; kk < k; kk++)

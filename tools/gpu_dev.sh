@@ -6,7 +6,7 @@ mkdir -p gpurun_out
 TAG=${TAG:-dev}
 ok() { local rc=$1; [ "$rc" -eq 0 ] || [ "$rc" -eq 1 ]; }
 echo "== pytest ${PYTEST_FILES:-tests} -m gpu ${PYTEST_K:+-k $PYTEST_K}"; date
-timeout -k 10 ${PYTEST_TIMEOUT:-900} python -u -m pytest ${PYTEST_FILES:-tests} -m gpu -q ${PYTEST_X:--x} --timeout 300 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} > gpurun_out/pytest_$TAG.log 2>&1; rc=$?
+timeout -k 10 ${PYTEST_TIMEOUT:-900} python -u -m pytest ${PYTEST_FILES:-tests} -m gpu -q ${PYTEST_X--x} --timeout 300 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} > gpurun_out/pytest_$TAG.log 2>&1; rc=$?
 tail -30 gpurun_out/pytest_$TAG.log; echo "pytest rc=$rc"; ok $rc || exit $rc
 if [ "${BENCH:-0}" = 1 ]; then
   echo "== bench"; date
