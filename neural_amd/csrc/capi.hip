@@ -487,16 +487,23 @@ struct A16 {
   int kp = 0;
 };
 
-static bool gemm2_ok(const DeviceWeight& w, int m) {
+// 3: gemm3 (int4, groups of 128 * 2^j); 4: gemm4 (int4 g32 / g64, int2 groups >= 64); 0: register-staged fallback
+static int pipelined_gemm(const DeviceWeight& w, int m) {
+  if (env_int("NAD_GEMM2_DISABLE", 0) || w.kmajor || m < 32 || uint64_t(m) * uint64_t(w.nt) * 512 >= (1ull << 32))
+    return 0;
   const int tpg = w.blocksize / 128;
-  return !env_int("NAD_GEMM2_DISABLE", 0) && w.bits == 4 && !w.kmajor && w.blocksize % 128 == 0 &&
-         (tpg & (tpg - 1)) == 0 && m >= 32 && uint64_t(m) * uint64_t(w.nt) * 256 < (1ull << 32);
+  if (w.bits == 4 && w.blocksize % 128 == 0 && (tpg & (tpg - 1)) == 0 && !env_int("NAD_GEMM4_ALL", 0)) return 3;
+  const int kt = w.bits == 4 ? 128 : 256;
+  if (!env_int("NAD_GEMM4_DISABLE", 0) && gemm4_mode(w.bits, w.blocksize, w.ng, w.nt * kt, w.asym)) return 4;
+  return 0;
 }
+static bool gemm2_ok(const DeviceWeight& w, int m) { return pipelined_gemm(w, m) != 0; }
+static int k_tile(const DeviceWeight& w) { return w.bits == 4 ? 128 : (w.bits == 2 ? 256 : 64); }
 
 // 1 ready, -1 error (no workspace under capture, launch error)
 static int prepare_a16(A16& r, const void* act, int act_t, int lda, int m, int k, const DeviceWeight& w,
                        hipStream_t st) {
-  const int kp = w.nt * 128;
+  const int kp = w.nt * k_tile(w);
   r.kp = kp;
   if (act_t == kActF16 && !w.shuffle && k == kp && reinterpret_cast<uintptr_t>(act) % 16 == 0 &&
       (size_t(lda) * 2) % 16 == 0) {
@@ -533,14 +540,16 @@ static int run_gemm(const void* act, int act_t, int lda, int m, int k, const Dev
   a.ld_aux = ld_aux;
   a.prio = env_int("NAD_GEMM3_PRIO", 0);
   a.w = view(w, out, ldo, bias, bias_ld);
-  if (gemm2_ok(w, m)) {
+  const int pg = pipelined_gemm(w, m);
+  if (pg) {
     A16 own;
-    if (!pre || pre->kp != w.nt * 128 || w.shuffle) {
+    if (!pre || pre->kp != w.nt * k_tile(w) || w.shuffle) {
       if (prepare_a16(own, act, act_t, lda, m, k, w, st) < 0) return -1;
       pre = &own;
     }
-    hipError_t e = env_int("NAD_GEMM_KERNEL", 3) == 2 ? launch_gemm2(a, pre->p, pre->ld, st)
-                                                      : launch_gemm3(a, pre->p, pre->ld, st);
+    hipError_t e = pg == 4                                ? launch_gemm4(a, w.bits, pre->p, pre->ld, st)
+                   : env_int("NAD_GEMM_KERNEL", 3) == 2 ? launch_gemm2(a, pre->p, pre->ld, st)
+                                                        : launch_gemm3(a, pre->p, pre->ld, st);
     if (e != hipSuccess) {
       set_err("gemm2 kernel launch failed: %s", hipGetErrorString(e));
       return -1;

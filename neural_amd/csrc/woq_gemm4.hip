@@ -1,0 +1,512 @@
+// woq_gemm4.hip -- the pipelined prefill GEMM (gemm3's structure) generalised to the configurations gemm3 leaves to
+// the register-staged fallback: int4 with groups of 32 / 64 (the reference Python default is g32,
+// neural_speed/__init__.py:150) and int2 with groups of >= 64 (Mistral int2 g64, BASELINE config 5).
+//
+// Replaces LauncherBase::gemm / run_block + WeightKBlockNInteger::getFpWeight (bestla/bestla/bestla_wrapper.h:481-542,
+// bestla_prologue_b.h:732-838) for these weights.
+//
+// Same skeleton as woq_gemm3_kernel (woq_gemm2.hip): 256 x 128 block tile, 8 waves as 2 (M) x 4 (N), K in 64-deep
+// half steps, A (fp16) three half steps ahead in a ring of four 32 KiB LDS buffers, every operand by LDS-DMA, counted
+// vmcnt + raw s_barrier at each half step, inline-asm LDS reads.  What changes with the weight format:
+//   * a 1 KiB B tile spans HPT = 2 (int4, 128 k) or 4 (int2, 256 k) half steps; it is DMA'd when the A of its first
+//     half step goes out, into a ring of NBR tiles, so batch sizes follow the half step's phase in the tile and every
+//     wait count is a compile-time constant of that phase;
+//   * a tile carries up to GSLOTS groups: scale (and zero-point) dword pieces for all of them go out with the tile,
+//     one 256 B piece per wave (slot = wave >> 1, stripe half = wave & 1; spare waves re-copy a slot: identical bytes);
+//   * groups end every 2^gh_log2 half steps (>= 64 k) or after every 32-deep MFMA step (G32); at a group end the
+//     group accumulators are scaled into the result (exact weights, w = (q - zp) * s in fp32);
+//   * int2 crumbs dequantise like woq_device.h dequant_step<2> (0x6400 magic, 2-bit fields), one LDS dword per stripe
+//     per half step.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <utility>
+
+#include "woq_device.h"
+#include "woq_kernels.h"
+
+namespace nad {
+namespace g4 {
+
+constexpr int BM = 256, ROWB = 128;        // ROWB: bytes of one A row per 64-deep half step
+constexpr int HBUF = BM * ROWB;            // one half step of A: 32 KiB
+constexpr int NA = 4;                      // A ring: three half steps in flight
+constexpr int BTILES = 8 * 1024;           // one B tile of the block's 8 stripes
+constexpr int LDS_BUDGET = 160 * 1024;
+
+template <int BITS>
+constexpr int hpt() {
+  return BITS == 4 ? 2 : 4;
+}
+template <int BITS, bool G32>
+constexpr int gslots() {
+  return G32 ? 4 : hpt<BITS>();
+}
+template <int BITS, bool G32, bool ASYM>
+constexpr int bbuf() {
+  return BTILES + gslots<BITS, G32>() * 512 * (ASYM ? 2 : 1);
+}
+template <int BITS, bool G32, bool ASYM>
+constexpr int nbr() {
+  return (LDS_BUDGET - NA * HBUF) / bbuf<BITS, G32, ASYM>() >= 3 ? 3 : 2;
+}
+template <int BITS, bool G32, bool ASYM>
+constexpr int lds_bytes() {
+  // a 2-deep ring is only safe when a tile spans more than two half steps (int2)
+  static_assert(hpt<BITS>() > 2 || nbr<BITS, G32, ASYM>() == 3, "int4 needs a 3-deep B ring");
+  return NA * HBUF + nbr<BITS, G32, ASYM>() * bbuf<BITS, G32, ASYM>();
+}
+
+__device__ __forceinline__ uint32_t and_or(uint32_t x, uint32_t m, uint32_t c) {
+  uint32_t r;
+  asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "s"(m), "v"(c));
+  return r;
+}
+__device__ __forceinline__ h2_t splat(float v) {
+  h2_t r;
+  r[0] = _Float16(v);
+  r[1] = _Float16(v);
+  return r;
+}
+// int4: 8 nibbles of one dword -> 8 exact fp16 (q - 8 - zp), 0x6400 magic (as woq_gemm2.hip)
+__device__ __forceinline__ h8_t dq4(uint32_t w, h2_t s16, h2_t c0, h2_t c1) {
+  const uint32_t m0 = 0x000F000Fu, m1 = 0x00F000F0u, mag = 0x64006400u;
+  const uint32_t w8 = w >> 8;
+  const h2_t p0 = as_h2(and_or(w, m0, mag)) + c0;
+  const h2_t p1 = as_h2(and_or(w, m1, mag)) * s16 + c1;
+  const h2_t p2 = as_h2(and_or(w8, m0, mag)) + c0;
+  const h2_t p3 = as_h2(and_or(w8, m1, mag)) * s16 + c1;
+  h8_t r;
+  r[0] = p0[0];
+  r[1] = p0[1];
+  r[2] = p1[0];
+  r[3] = p1[1];
+  r[4] = p2[0];
+  r[5] = p2[1];
+  r[6] = p3[0];
+  r[7] = p3[1];
+  return r;
+}
+// int2: the 16-bit half `sh` (0 or 8) of a dword -> 8 exact fp16 (q - 2 - zp); field order of dequant_step<2>
+__device__ __forceinline__ h8_t dq2(uint32_t w, int sh, h2_t c) {
+  const uint32_t m = 0x00030003u, mag = 0x64006400u;
+  const uint32_t x = w >> sh;
+  const h2_t p0 = as_h2(and_or(x, m, mag)) + c;
+  const h2_t p1 = as_h2(and_or(x >> 2, m, mag)) + c;
+  const h2_t p2 = as_h2(and_or(x >> 4, m, mag)) + c;
+  const h2_t p3 = as_h2(and_or(x >> 6, m, mag)) + c;
+  h8_t r;
+  r[0] = p0[0];
+  r[1] = p0[1];
+  r[2] = p1[0];
+  r[3] = p1[1];
+  r[4] = p2[0];
+  r[5] = p2[1];
+  r[6] = p3[0];
+  r[7] = p3[1];
+  return r;
+}
+
+__device__ __forceinline__ void glds16(const void* g, char* l) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                   (__attribute__((address_space(3))) void*)l, 16, 0, 0);
+}
+__device__ __forceinline__ void glds4(const void* g, char* l) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                   (__attribute__((address_space(3))) void*)l, 4, 0, 0);
+}
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+// LDS reads in inline asm (hipcc would put a vmcnt(0) before every LDS read it can see while an LDS-DMA is in flight)
+template <int OFF>
+__device__ __forceinline__ h8_t lds_b128(uint32_t addr) {
+  h8_t r;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "n"(OFF));
+  return r;
+}
+template <int OFF>
+__device__ __forceinline__ uint2 lds_b64(uint32_t addr) {
+  uint2 r;
+  asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "n"(OFF));
+  return r;
+}
+template <int OFF>
+__device__ __forceinline__ uint32_t lds_b32(uint32_t addr) {
+  uint32_t r;
+  asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "n"(OFF));
+  return r;
+}
+__device__ __forceinline__ uint32_t lds_b32v(uint32_t addr) {  // runtime offset folded into the address
+  uint32_t r;
+  asm volatile("ds_read_b32 %0, %1" : "=v"(r) : "v"(addr));
+  return r;
+}
+template <size_t... I>
+__device__ __forceinline__ void lds_frags(h8_t (&f)[8], uint32_t addr, std::index_sequence<I...>) {
+  ((f[I] = lds_b128<int(I) * 16 * ROWB>(addr)), ...);
+}
+template <class T>
+__device__ __forceinline__ void tie(T& r) {
+  asm volatile("" : "+v"(r));
+}
+template <int N, class... T>
+__device__ __forceinline__ void wait_lgk(T&... regs) {
+  asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(N));
+  (tie(regs), ...);
+}
+__device__ __forceinline__ uint32_t lds_addr(const char* p) {
+  return uint32_t(reinterpret_cast<uintptr_t>((const __attribute__((address_space(3))) char*)p));
+}
+
+template <int BITS, bool G32, bool ASYM>
+__global__ __launch_bounds__(512, 1) void woq_gemm4_kernel(GemmArgs a, const _Float16* __restrict__ A16, int lda16,
+                                                           int gh_log2) {
+  constexpr int HPT = hpt<BITS>();
+  constexpr int GS = gslots<BITS, G32>();
+  constexpr int BSC = GS * 512;
+  constexpr int BBUF = bbuf<BITS, G32, ASYM>();
+  constexpr int NBR = nbr<BITS, G32, ASYM>();
+  constexpr int NBW = ASYM ? 3 : 2;  // B-side VMEM instructions of a tile batch, per wave
+  constexpr int BIAS = BITS == 4 ? 8 : 2;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));
+  const int wm = wave >> 2, wn = wave & 3;
+  const SkinnyWeight& W = a.w;
+  const int M = a.M, nt = W.nt, ng = W.ng, ns = W.ns;
+  const int nh = HPT * nt;  // half steps
+  const int gh = 1 << gh_log2;
+
+  // XCD-aware remap (as gemm2 / gemm3)
+  const int nbm = (M + BM - 1) / BM;
+  const int nbn = (ns + 7) / 8;
+  const int nwg = nbm * nbn;
+  int bid = blockIdx.x;
+  {
+    const int q = nwg / 8, r = nwg % 8, x = bid % 8, o = bid / 8;
+    bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + o;
+  }
+  const int bm = bid / nbn, bn = bid % nbn;
+  const int m0 = bm * BM;
+  const int nl = lane & 15, kq = lane >> 4;
+
+  uint32_t aoff[4];
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const int row = (wave * 4 + i) * 8 + (lane >> 3);
+    const int grow = min(m0 + row, M - 1);
+    aoff[i] = uint32_t(grow) * uint32_t(lda16) * 2u + uint32_t(((lane & 7) ^ ((row >> 1) & 7)) * 16);
+  }
+  const char* abase = reinterpret_cast<const char*>(A16);
+  const char* btile = static_cast<const char*>(W.tiles) + (size_t(min(bn * 8 + wave, ns - 1)) * nt * 64 + lane) * 16;
+  const int sstripe = min(bn * 8 + (wave & 1) * 4 + (lane >> 4), ns - 1);
+  const size_t srow0 = size_t(sstripe) * ng * 16 + nl;
+  const int slot_w = (wave >> 1) % GS;  // this wave's scale / zero-point slot
+  const int st = a.scale_t;
+  const uint32_t* sbase = static_cast<const uint32_t*>(W.scales);
+  const uint32_t* zbase = reinterpret_cast<const uint32_t*>(W.zps);
+
+  // group of tile t's slot s
+  auto slot_group = [&](int t, int s) {
+    int g;
+    if constexpr (G32)
+      g = t * 4 + s;
+    else
+      g = ((t * HPT) >> gh_log2) + (gh_log2 < 30 ? min(s, max(HPT >> gh_log2, 1) - 1) : 0);
+    return min(g, ng - 1);
+  };
+
+  // batch(u): A(u + 3) and, when u + 3 starts a tile, that tile + its scale (+ zero-point) pieces
+  auto issue = [&](auto Pc, int u) {
+    constexpr int P = decltype(Pc)::value;  // (u + 3) % HPT
+    if (u + 3 >= nh) return;
+    const int ua = u + 3;
+    char* ab = smem + (ua & 3) * HBUF;
+    const char* src = abase + size_t(ua) * ROWB;
+#pragma unroll
+    for (int i = 0; i < 4; i++) glds16(src + aoff[i], ab + (wave * 4 + i) * 1024);
+    if constexpr (P == 0) {
+      const int t = ua / HPT;
+      char* bb = smem + NA * HBUF + (t % NBR) * BBUF;
+      glds16(btile + size_t(t) * 1024, bb + wave * 1024);
+      const size_t si = srow0 + size_t(slot_group(t, slot_w)) * 16;
+      glds4(sbase + (st == kScaleF32 ? si : (si >> 1)), bb + BTILES + slot_w * 512 + (wave & 1) * 256);
+      if constexpr (ASYM) glds4(zbase + (si >> 2), bb + BTILES + BSC + slot_w * 512 + (wave & 1) * 256);
+    }
+  };
+
+  f4_t acc[8][2], accg[8][2];
+#pragma unroll
+  for (int i = 0; i < 8; i++)
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+      acc[i][j] = f4_t{0.f, 0.f, 0.f, 0.f};
+      accg[i][j] = f4_t{0.f, 0.f, 0.f, 0.f};
+    }
+
+  // prologue: batches -3, -2, -1 (A0 + tile 0, A1, A2; the tile of half 2 goes with A2 when HPT == 2)
+  issue(std::integral_constant<int, 0>{}, -3);
+  issue(std::integral_constant<int, 1 % HPT>{}, -2);
+  issue(std::integral_constant<int, 2 % HPT>{}, -1);
+  // wait for batch -3: batches -2 and -1 may stay in flight
+  {
+    constexpr int b2 = 4 + ((1 % HPT) == 0 ? NBW : 0), b1 = 4 + ((2 % HPT) == 0 ? NBW : 0);
+    if (nh > 2)
+      wait_vm<b2 + b1>();
+    else if (nh > 1)
+      wait_vm<b2>();
+    else
+      wait_vm<0>();
+  }
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+
+  const h2_t s16 = splat(1.f / 16.f);
+  const h2_t zc0 = splat(-(1024.f + BIAS)), zc1 = splat(-(64.f + BIAS));
+  uint32_t roff[2];
+#pragma unroll
+  for (int dd = 0; dd < 2; dd++) roff[dd] = uint32_t((wm * 128 + nl) * ROWB + (((dd * 4 + kq) ^ ((nl >> 1) & 7)) * 16));
+  const int boff = (wn * 2) * 1024 + lane * 16;
+  const int soff = BTILES + ((wn * 2) * 16 + nl) * 4;
+  const int zoff = BTILES + BSC + ((wn * 2) * 16 + nl) * 4;
+  const int ssh = st == kScaleF32 ? 0 : (nl & 1) * 16;
+  const int zsh = (nl & 3) * 8;
+  const f4_t zero = {0.f, 0.f, 0.f, 0.f};
+  auto scale_f32 = [&](uint32_t x) {
+    const uint32_t h = (x >> ssh) & 0xFFFFu;
+    const float fb = __uint_as_float(h << 16);
+    const float fh = f16_bits_to_f32(uint16_t(h));
+    const float f16or = st == kScaleBF16 ? fb : fh;
+    return st == kScaleF32 ? __uint_as_float(x) : f16or;
+  };
+
+  auto half = [&](auto Hc, int u) {
+    constexpr int H = decltype(Hc)::value;  // phase of half step u in its tile
+    const int t = u / HPT;
+    const char* ab = smem + (u & 3) * HBUF;
+    const char* bb = smem + NA * HBUF + (t % NBR) * BBUF;
+    issue(std::integral_constant<int, (H + 3) % HPT>{}, u);
+    const uint32_t al = lds_addr(ab), bl = lds_addr(bb);
+    // B words of this half step for the wave's two stripes: int4 two dwords (one per 32-deep step), int2 one dword
+    uint32_t bw[2][2];
+    if constexpr (BITS == 4) {
+      const uint2 v0 = lds_b64<H * 8>(bl + boff), v1 = lds_b64<1024 + H * 8>(bl + boff);
+      bw[0][0] = v0.x;
+      bw[0][1] = v0.y;
+      bw[1][0] = v1.x;
+      bw[1][1] = v1.y;
+    } else {
+      // one dword serves both 32-deep steps.  No copy into bw[j][1]: a register copy of an inline-asm LDS result would
+      // be scheduled before the lgkmcnt wait and read the register before the data lands
+      bw[0][0] = lds_b32<H * 4>(bl + boff);
+      bw[1][0] = lds_b32<1024 + H * 4>(bl + boff);
+      bw[0][1] = bw[1][1] = 0u;
+    }
+    // group slot(s) of this half step
+    const int slot = G32 ? 2 * H : (gh_log2 >= 30 ? 0 : (H >> gh_log2) % GS);
+    uint32_t zw[2][2] = {{0u, 0u}, {0u, 0u}};
+    if constexpr (ASYM) {
+      const uint32_t za = bl + zoff + slot * 512;
+      zw[0][0] = lds_b32v(za);
+      zw[1][0] = lds_b32v(za + 64);
+      if constexpr (G32) {
+        zw[0][1] = lds_b32v(za + 512);
+        zw[1][1] = lds_b32v(za + 512 + 64);
+      }
+    }
+    // G32: both groups' scales up front, so each 32-deep step's products scale straight into the result
+    uint32_t sg[2][2] = {{0u, 0u}, {0u, 0u}};
+    if constexpr (G32) {
+      const uint32_t sa = bl + soff + slot * 512;
+      sg[0][0] = lds_b32v(sa);
+      sg[0][1] = lds_b32v(sa + 64);
+      sg[1][0] = lds_b32v(sa + 512);
+      sg[1][1] = lds_b32v(sa + 512 + 64);
+    }
+    h8_t af0[8], af1[8];
+    lds_frags(af0, al + roff[0], std::make_index_sequence<8>{});
+    lds_frags(af1, al + roff[1], std::make_index_sequence<8>{});
+    wait_lgk<8>(bw[0][0], bw[0][1], bw[1][0], bw[1][1], zw[0][0], zw[0][1], zw[1][0], zw[1][1], sg[0][0], sg[0][1],
+                sg[1][0], sg[1][1], af0[0], af0[1], af0[2], af0[3], af0[4], af0[5], af0[6], af0[7]);
+    const bool gstart = G32 || (u & (gh - 1)) == 0;
+    const bool gend = G32 || ((u + 1) & (gh - 1)) == 0 || u == nh - 1;
+#pragma unroll
+    for (int dd = 0; dd < 2; dd++) {
+      if (dd == 1) wait_lgk<0>(af1[0], af1[1], af1[2], af1[3], af1[4], af1[5], af1[6], af1[7]);
+      const int zi = G32 ? dd : 0;
+      h8_t bf[2];
+#pragma unroll
+      for (int j = 0; j < 2; j++) {
+        const float zf = ASYM ? float(int(int8_t((zw[j][zi] >> zsh) & 0xFFu))) : 0.f;
+        if constexpr (BITS == 4)
+          bf[j] = dq4(bw[j][dd], s16, zc0 - splat(zf), zc1 - splat(zf));
+        else
+          bf[j] = dq2(bw[j][0], dd * 8, zc0 - splat(zf));
+      }
+      if constexpr (G32) {
+        const float sf[2] = {scale_f32(sg[dd][0]), scale_f32(sg[dd][1])};
+        // software-pipelined by one row block: the products of block i are scaled in while block i + 1 multiplies,
+        // so only two blocks of products are ever live
+        f4_t p[2][2];
+#pragma unroll
+        for (int i = 0; i <= 8; i++) {
+          if (i < 8) {
+            const h8_t af = dd == 0 ? af0[i] : af1[i];
+#pragma unroll
+            for (int j = 0; j < 2; j++) p[i & 1][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, bf[j], zero, 0, 0, 0);
+          }
+          if (i > 0) {
+#pragma unroll
+            for (int j = 0; j < 2; j++) {
+              acc[i - 1][j] += p[(i - 1) & 1][j] * sf[j];
+              tie(acc[i - 1][j]);  // pin the update here: left alone, the compiler sinks it past the hand-over
+            }                      // branches and keeps every product of the half step live (spills)
+          }
+        }
+        continue;
+      }
+#pragma unroll
+      for (int i = 0; i < 8; i++) {
+        const h8_t af = dd == 0 ? af0[i] : af1[i];
+#pragma unroll
+        for (int j = 0; j < 2; j++) {
+          const bool fresh = dd == 0 && gstart;
+          accg[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, bf[j], fresh ? zero : accg[i][j], 0, 0, 0);
+        }
+      }
+      if (dd == 1 && gend) {  // group end: scale the group partials into the result
+        const uint32_t sa = bl + soff + slot * 512;
+        uint32_t sw0 = lds_b32v(sa), sw1 = lds_b32v(sa + 64);
+        wait_lgk<0>(sw0, sw1);
+        const float sf[2] = {scale_f32(sw0), scale_f32(sw1)};
+#pragma unroll
+        for (int j = 0; j < 2; j++)
+#pragma unroll
+          for (int i = 0; i < 8; i++) {
+            acc[i][j] += accg[i][j] * sf[j];
+            tie(acc[i][j]);
+          }
+      }
+    }
+    // hand-over: batch u - 2 has landed; batches u - 1 and u stay in flight
+    constexpr int bu = 4 + (((H + 3) % HPT) == 0 ? NBW : 0);       // |batch u| (when issued)
+    constexpr int bu1 = 4 + (((H + 2) % HPT) == 0 ? NBW : 0);      // |batch u - 1|
+    if (u + 3 < nh)
+      wait_vm<bu + bu1>();
+    else if (u + 2 < nh)
+      wait_vm<bu1>();
+    else
+      wait_vm<0>();
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+
+  for (int u = 0; u < nh; u += HPT) {
+    half(std::integral_constant<int, 0>{}, u);
+    half(std::integral_constant<int, 1>{}, u + 1);
+    if constexpr (HPT == 4) {
+      half(std::integral_constant<int, 2>{}, u + 2);
+      half(std::integral_constant<int, 3>{}, u + 3);
+    }
+  }
+
+  // epilogue through LDS (as gemm3)
+  float* tw = reinterpret_cast<float*>(smem) + wave * (128 * 36);
+#pragma unroll
+  for (int i = 0; i < 8; i++)
+#pragma unroll
+    for (int j = 0; j < 2; j++)
+#pragma unroll
+      for (int rr = 0; rr < 4; rr++) tw[(i * 16 + kq * 4 + rr) * 36 + j * 16 + nl] = acc[i][j][rr];
+  const int s0 = bn * 8 + wn * 2;
+  const int col0 = s0 * 16;
+  const bool vec_out = (reinterpret_cast<uintptr_t>(W.out) % 16 == 0) && (W.ldo % 4 == 0);
+#pragma unroll 4
+  for (int q = 0; q < 16; q++) {
+    const int c = q * 64 + lane;
+    const int rl = c >> 3, c4 = c & 7;
+    const int row = m0 + wm * 128 + rl;
+    const int n0 = col0 + c4 * 4;
+    const float4 tv = *reinterpret_cast<const float4*>(tw + rl * 36 + c4 * 4);
+    if (row >= M || n0 >= W.n) continue;
+    float v[4] = {tv.x, tv.y, tv.z, tv.w};
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+      const int n = n0 + e;
+      if (n >= W.n) break;
+      switch (a.epi) {
+        case kEpiBias:
+          v[e] += W.bias[size_t(row) * W.bias_ld + n];
+          break;
+        case kEpiAddGelu:
+          v[e] = gelu_f(v[e] + W.bias[size_t(row) * W.bias_ld + n]);
+          break;
+        case kEpiGelu:
+          v[e] = gelu_f(v[e]);
+          break;
+        case kEpiSilu:
+          v[e] = silu_f(v[e]);
+          break;
+        case kEpiResAdd:
+          v[e] += a.res[size_t(row) * a.ld_res + n];
+          break;
+        case kEpiSiluMul:
+          v[e] = a.aux[size_t(row) * a.ld_aux + n] * v[e];
+          break;
+        default:
+          break;
+      }
+    }
+    float* o = W.out + size_t(row) * W.ldo + n0;
+    if (vec_out && n0 + 3 < W.n) {
+      *reinterpret_cast<float4*>(o) = make_float4(v[0], v[1], v[2], v[3]);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; e++)
+        if (n0 + e < W.n) o[e] = v[e];
+    }
+  }
+}
+
+}  // namespace g4
+
+// 0 if gemm4 does not take this weight; kG32Mode for int4 groups of 32; else gh_log2 + 1 (gh_log2: log2 of half steps
+// per group, 30 = one group over all of K)
+constexpr int kG32Mode = 100;
+int gemm4_mode(int bits, int blocksize, int ng, int kpad, bool asym) {
+  if (bits != 4 && bits != 2) return 0;
+  if (ng == 1) return 30 + 1;  // per-channel
+  if (bits == 4 && blocksize == 32) return asym ? 0 : kG32Mode;  // G32 + zero points: no room for a 3-deep B ring
+  if (blocksize < 64 || blocksize % 64) return 0;
+  const int gh = blocksize / 64;
+  if (gh & (gh - 1)) return 0;
+  (void)kpad;
+  return __builtin_ctz(unsigned(gh)) + 1;
+}
+
+hipError_t launch_gemm4(const GemmArgs& a, int bits, const _Float16* A16, int lda16, hipStream_t st) {
+  const int mode = gemm4_mode(bits, a.w.bs, a.w.ng, a.w.nt * (bits == 4 ? 128 : 256), a.w.zps != nullptr);
+  if (!mode) return hipErrorInvalidValue;
+  const bool g32 = mode == kG32Mode;
+  const int gh_log2 = g32 ? 0 : mode - 1;
+  const int nbm = (a.M + g4::BM - 1) / g4::BM, nbn = (a.w.ns + 7) / 8;
+  const bool asym = a.w.zps != nullptr;
+  auto go = [&](auto k, int lds) -> hipError_t {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       lds);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k, dim3(nbm * nbn), dim3(512), lds, st, a, A16, lda16, gh_log2);
+    return hipGetLastError();
+  };
+#define NAD_G4(B, G, A) go(g4::woq_gemm4_kernel<B, G, A>, g4::lds_bytes<B, G, A>())
+  if (bits == 4) {
+    if (g32) return NAD_G4(4, true, false);
+    return asym ? NAD_G4(4, false, true) : NAD_G4(4, false, false);
+  }
+  return asym ? NAD_G4(2, false, true) : NAD_G4(2, false, false);
+#undef NAD_G4
+}
+
+}  // namespace nad

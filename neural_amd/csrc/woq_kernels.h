@@ -111,6 +111,10 @@ hipError_t launch_gemm2(const GemmArgs& a, const _Float16* A16, int lda16, hipSt
 // prefill GEMM v3 (woq_gemm2.hip): same contract as launch_gemm2; every operand staged by LDS-DMA three 64-deep half
 // steps ahead with counted vmcnt (no drain at the barriers)
 hipError_t launch_gemm3(const GemmArgs& a, const _Float16* A16, int lda16, hipStream_t stream);
+// prefill GEMM v4 (woq_gemm4.hip): gemm3's pipeline for int4 groups of 32 / 64 and int2 groups >= 64.
+// gemm4_mode: 0 = not taken, else the group mode; A as for gemm3 with K padded to the weight's K tile (128 / 256)
+int gemm4_mode(int bits, int blocksize, int ng, int kpad, bool asym);
+hipError_t launch_gemm4(const GemmArgs& a, int bits, const _Float16* A16, int lda16, hipStream_t stream);
 hipError_t launch_cvt_act(const void* A, int act_t, int lda, int M, int K, int Kp, const int32_t* shuffle,
                           _Float16* out, hipStream_t stream);
 // groups per K tile the GEMV handles (1, 2, 4, 8) for this geometry, 0 if unsupported; *tpg = tiles per group

@@ -14,7 +14,7 @@ import numpy as np
 import pytest
 
 from tests.conftest import gpu_available
-from tests.oracle_lib import BF16, F16, F32, S4
+from tests.oracle_lib import BF16, F16, F32, S2, S4
 from tests.test_gpu_parity import _blob, _rel_err
 
 pytestmark = pytest.mark.gpu
@@ -128,3 +128,46 @@ def test_gemm_fused_qkv_and_ffn(oracle, m):
     h3 = oracle.forward(A, b3, fmid, fin).astype(np.float64)
     ref = oracle.forward((h1 / (1 + np.exp(-h1)) * h3).astype(np.float32), b2, fout, fmid)
     assert _rel_err(y, ref) <= 2 * TOL["fp32"]
+
+
+GEMM4_CASES = [
+    # m, n, k, bs, qtype, stype, asym, comp  -- gemm4 (woq_gemm4.hip): int4 g32 / g64, int2 groups >= 64
+    (64, 128, 512, 32, S4, F16, False, 4),        # int4 g32 (the reference Python default group)
+    (257, 300, 640, 32, S4, BF16, False, 4),      # ragged M / N, 5 K tiles
+    (96, 130, 300, 64, S4, F16, False, 4),        # int4 g64, K tail (zero padded)
+    (300, 200, 768, 64, S4, BF16, True, 4),       # int4 g64 asym
+    (128, 256, 1024, 64, S2, F16, False, 1),      # int2 g64 (Mistral config 5)
+    (200, 96, 640, 64, S2, F32, True, 1),         # int2 g64 asym, K tail inside a 256-deep tile
+    (64, 160, 1024, 128, S2, BF16, False, 4),     # int2 g128
+    (100, 64, 2048, 256, S2, F16, True, 4),       # int2 g256 asym (one group per tile)
+    (48, 80, 1024, 1024, S2, F32, False, 1),      # int2 per-channel
+]
+
+
+@pytest.mark.parametrize("cfg", GEMM4_CASES)
+@pytest.mark.parametrize("act", ["fp32", "fp16", "bf16"])
+def test_gemm4_parity(oracle, cfg, act):
+    """gemm4 against the oracle, and against the register-staged fallback (NAD_GEMM4_DISABLE=1) on the same inputs."""
+    m, n, k, bs, qt, st, asym, comp = cfg
+    blob = _blob(oracle, n, k, bs, qt, st, asym, comp, seed=m + 7 * n + k)
+    w = bestla.DeviceWeight(blob)
+    A = np.random.default_rng(m * 3 + n).uniform(-0.5, 0.5, size=(m, k)).astype(np.float32)
+    x = torch.from_numpy(A).cuda()
+    if act != "fp32":
+        x = x.to(torch.float16 if act == "fp16" else torch.bfloat16)
+    ref = oracle.forward(x.float().cpu().numpy(), blob, n, k)
+    y = w.forward(x).cpu().numpy()
+    assert _rel_err(y, ref) <= TOL[act], (_rel_err(y, ref), act)
+
+
+def test_gemm4_takes_the_fallback_configs(oracle, monkeypatch):
+    """With gemm4 disabled the same inputs run the register-staged kernel: both agree within fp32 accumulation noise
+    (they see identical fp16 A and exact weights)."""
+    m, n, k = 200, 256, 1024
+    blob = _blob(oracle, n, k, 64, S2, F16, True, 1, seed=5)
+    w = bestla.DeviceWeight(blob)
+    x = (torch.rand((m, k), device="cuda") - 0.5).half()
+    y4 = w.forward(x).cpu().numpy()
+    monkeypatch.setenv("NAD_GEMM4_DISABLE", "1")
+    y1 = w.forward(x).cpu().numpy()
+    assert _rel_err(y4, y1.astype(np.float64)) <= 2e-5

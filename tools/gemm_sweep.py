@@ -1,7 +1,8 @@
 """Prefill GEMM sweep (development tool): TFLOP/s of one WOQ linear per Llama-2-7B shape at prefill M.
 
 Usage: python tools/gemm_sweep.py [--m 2048,4096] [--act fp16,fp32] [--shapes o,gate,down,lm_head] [--reps 20]
-       [--kernels 3,2]
+       [--kernels 3,2] [--bits 4] [--group 128] [--asym]
+Kernels: 3 / 2 = the int4 pipelined kernels, 4 = gemm4 (int4 g32/g64, int2), 0 = generic tiled fallback.
 Each line: shape, M, activation dtype, kernel, average device time per forward (HIP events on the launch stream, back
 to back launches) and TFLOP/s (2*M*N*K / time).  fp32 activations include the one-pass fp16 conversion kernel.
 """
@@ -22,6 +23,9 @@ def main():
     ap.add_argument("--shapes", default="o,gate,down,lm_head")
     ap.add_argument("--kernels", default="3,2")
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--bits", type=int, default=4)
+    ap.add_argument("--group", type=int, default=128)
+    ap.add_argument("--asym", action="store_true")
     args = ap.parse_args()
     import torch
     from neural_amd import bestla
@@ -29,7 +33,7 @@ def main():
     print(torch.cuda.get_device_name(0), flush=True)
     for name in args.shapes.split(","):
         n, k = SHAPES[name]
-        w = bestla.DeviceWeight.synthetic(4, n, k, 128, "fp16", False, seed=3)
+        w = bestla.DeviceWeight.synthetic(args.bits, n, k, args.group, "fp16", args.asym, seed=3)
         for m in (int(x) for x in args.m.split(",")):
             for act in args.act.split(","):
                 dt = {"fp16": torch.float16, "fp32": torch.float32, "bf16": torch.bfloat16}[act]
@@ -38,6 +42,8 @@ def main():
                 s = torch.cuda.current_stream()
                 for kern in args.kernels.split(","):
                     os.environ["NAD_GEMM_KERNEL"] = kern[0]
+                    os.environ["NAD_GEMM2_DISABLE"] = "1" if kern[0] == "0" else "0"
+                    os.environ["NAD_GEMM4_DISABLE"] = "1" if kern[0] != "4" else "0"
                     os.environ["NAD_GEMM3_PRIO"] = "1" if kern.endswith("p") else "0"
                     for _ in range(3):
                         w.forward(x, out=out)
@@ -50,7 +56,7 @@ def main():
                     torch.cuda.synchronize()
                     us = e0.elapsed_time(e1) * 1e3 / args.reps
                     tf = 2.0 * m * n * k / us / 1e6
-                    print(f"{name:8s} N={n:5d} K={k:5d} M={m:5d} {act} gemm{kern}: {us:9.1f} us  {tf:7.1f} TFLOP/s",
+                    print(f"{name:8s} b{args.bits} g{args.group}{'a' if args.asym else 's'} N={n:5d} K={k:5d} M={m:5d} {act} gemm{kern}: {us:9.1f} us  {tf:7.1f} TFLOP/s",
                           flush=True)
                 del x, out
         del w
