@@ -186,6 +186,17 @@ size_t nad_synthetic_weight_size(int bits, int n, int k, int blocksize, int scal
 /* drop every device copy the host-pointer ABI cached (weights are keyed by blob address + content fingerprint and
  * re-uploaded when a pack entry rewrites a blob) */
 void nad_host_cache_clear(void);
+/* ===== int8-compute mode: the reference's comp_int8 arithmetic for weights packed for an integer core (blobs that
+ * carry the bf16 reduce).  0 (default): fp16 MFMA on the exact weights.  1: activations quantized to u8 per (row,
+ * weight block) as kernel_ref.h:1824-1883, s32 block dot products, the kblock core's fp32 combine
+ * (bestla_wrapper.h:768-831, bestla_gemm.h:2983-3050).  Initial value from NAD_COMPUTE_INT8.  Weights without a
+ * reduce keep the fp path; a fused call mixing the two kinds fails. */
+int nad_set_compute_mode(int mode);
+int nad_get_compute_mode(void);
+/* kernel::wrapper::QuantizeU8ColBlock::forward (kernel_wrapper.h:571-590) on device pointers: act [m][lda] in
+ * act_dtype, q [m][ldq] u8, scales / zps [m][ld_scale] per block, blkreduce (may be NULL) = sum(round(x/s)) * s. */
+int nad_quant_u8_colblock(const void* act, int act_dtype, int m, int k, int lda, int blocksize, uint8_t* q, int ldq,
+                          float* scales, uint8_t* zps, int ld_scale, float* blkreduce, void* queue);
 /* host convenience: (re)pack one blob into fp32 dequantized [K][N] from the device tile layout (round-trip check) */
 int nad_device_unpack_fp32(const void* devstor, float* host_out, void* queue);
 

@@ -75,6 +75,9 @@ SIGNATURES = {
     "nad_synthetic_weight_size": (_sz, [_i, _i, _i, _i, _i, _i]),
     "nad_device_unpack_fp32": (_i, [_p, _p, _p]),
     "nad_host_cache_clear": (None, []),
+    "nad_set_compute_mode": (_i, [_i]),
+    "nad_get_compute_mode": (_i, []),
+    "nad_quant_u8_colblock": (_i, [_p, _i, _i, _i, _i, _i, _p, _i, _p, _p, _i, _p, _p]),
     "nad_chain_create": (_p, [_p, _i, _i]),
     "nad_chain_run": (_i, [_p, _p]),
     "nad_chain_status": (_i, [_p]),

@@ -230,6 +230,37 @@ class DeviceWeight:
         return out
 
 
+COMPUTE_FP, COMPUTE_INT8 = 0, 1
+
+
+def set_compute_mode(mode):
+    """0 (fp16 MFMA on exact weights, default) or 1: the reference's comp_int8 arithmetic for weights packed for an
+    integer core (u8 activations per (row, block), s32 block dots, kblock fp32 combine).  Returns the previous mode."""
+    L = lib()
+    prev = L.nad_get_compute_mode()
+    check(L.nad_set_compute_mode(int(mode)), "nad_set_compute_mode")
+    return prev
+
+
+def get_compute_mode():
+    return lib().nad_get_compute_mode()
+
+
+def quant_u8_colblock(x, blocksize, stream=None):
+    """kernel::wrapper::QuantizeU8ColBlock (kernel_wrapper.h:571-590) on the GPU: x cuda [M][K] fp32/fp16/bf16 ->
+    (q u8 [M][K], scales f32 [M][nblk], zero points u8 [M][nblk], block reduce f32 [M][nblk])."""
+    torch = _torch()
+    m, k = x.shape
+    nblk = -(-k // blocksize)
+    q = torch.empty((m, k), dtype=torch.uint8, device=x.device)
+    s = torch.empty((m, nblk), dtype=torch.float32, device=x.device)
+    z = torch.empty((m, nblk), dtype=torch.uint8, device=x.device)
+    red = torch.empty((m, nblk), dtype=torch.float32, device=x.device)
+    check(lib().nad_quant_u8_colblock(_ptr(x), _act_code(x), m, k, x.stride(0), blocksize, _ptr(q), k, _ptr(s),
+                                      _ptr(z), nblk, _ptr(red), _stream(stream)), "nad_quant_u8_colblock")
+    return q, s, z, red
+
+
 def f32f32_forward(activation, weight, output, m, n, k, lda, ldo, stream=None):
     """bestla_device_f32f32_forward with raw device tensors (void result; errors via last_error)."""
     L = lib()

@@ -123,7 +123,8 @@ extern "C" size_t nad_device_weight_size(const void* hostblob) {
   }
   DeviceWeight w{};
   int bs = b.blocksize >= b.k ? b.kpad : b.blocksize;
-  return layout_geometry(w, dtype_bits(b.qtype), b.n, b.k, bs, scale_code(b.scale_t), b.asym, b.has_shuffle);
+  return layout_geometry(w, dtype_bits(b.qtype), b.n, b.k, bs, scale_code(b.scale_t), b.asym, b.has_shuffle, 0,
+                         b.has_reduce);
 }
 
 extern "C" int nad_device_load(const void* hostblob, void* devstor, void* deviceptr, size_t capacity, void* queue) {
@@ -143,7 +144,7 @@ extern "C" int nad_device_load(const void* hostblob, void* devstor, void* device
   const int bs = b.blocksize >= b.k ? b.kpad : b.blocksize;
   const char* km = getenv("NAD_TILE_KMAJOR");  // layout A/B switch (development); default K-major
   const uint64_t need = layout_geometry(w, dtype_bits(b.qtype), b.n, b.k, bs, scale_code(b.scale_t), b.asym,
-                                        b.has_shuffle, (km && *km) ? atoi(km) : 0);
+                                        b.has_shuffle, (km && *km) ? atoi(km) : 0, b.has_reduce);
   if (need > capacity) {
     set_err("device buffer too small for the tile layout: need %llu bytes, have %zu (see nad_device_weight_size)",
             (unsigned long long)need, capacity);
@@ -152,6 +153,7 @@ extern "C" int nad_device_load(const void* hostblob, void* devstor, void* device
   layout_assign(w, deviceptr);
   w.src_core_id = b.core_id;
   w.owner = nullptr;
+  w.blob_bs = b.blocksize;
   // stage the raw blob buffers on the device, repack there
   const uint8_t* base = static_cast<const uint8_t*>(hostblob);
   uint8_t* stage = nullptr;
@@ -164,6 +166,11 @@ extern "C" int nad_device_load(const void* hostblob, void* devstor, void* device
   HIP_OK(hipMemcpyAsync(ds, base + b.s_off, sz, hipMemcpyHostToDevice, st));
   if (zz) HIP_OK(hipMemcpyAsync(dz, base + b.z_off, zz, hipMemcpyHostToDevice, st));
   if (b.has_shuffle) HIP_OK(hipMemcpyAsync(w.shuffle, base + b.shf_off, size_t(b.k) * 4, hipMemcpyHostToDevice, st));
+  if (w.reduce) {  // bf16 rows [block][cstep] -> [block][red_ld], zero padded columns
+    HIP_OK(hipMemsetAsync(w.reduce, 0, size_t(w.ng) * w.red_ld * 2, st));
+    HIP_OK(hipMemcpy2DAsync(w.reduce, size_t(w.red_ld) * 2, base + b.r_off, size_t(b.cstep) * 2, size_t(b.n) * 2,
+                            size_t(w.ng), hipMemcpyHostToDevice, st));
+  }
   CoreInfo ci = core_info(b.core_id);
   RepackArgs ra{};
   ra.src_q = dq;
@@ -378,9 +385,17 @@ static int try_gemv(const void* act, int act_t, int lda, int m, int k, int nw, c
   return 1;
 }
 
+static bool int8_compute(const DeviceWeight& w);
+static int run_i8(const void* act, int act_t, int lda, int m, int k, int nw, const DeviceWeight* const* ws,
+                  float* const* outs, const int* ldos, bool dual, int epi, const float* bias, int bias_ld,
+                  const float* res, int ld_res, const float* aux, int ld_aux, hipStream_t st);
+
 static int run_skinny(const void* act, int act_t, int lda, int m, int k, int nw, const DeviceWeight* const* ws,
                       float* const* outs, const int* ldos, int epi, const float* bias, int bias_ld, const float* res,
                       int ld_res, float* aux, int ld_aux, hipStream_t st) {
+  if (int8_compute(*ws[0]))
+    return run_i8(act, act_t, lda, m, k, nw, ws, outs, ldos, nw == 2 && (epi == kEpiSiluMul || epi == kEpiGeluMul),
+                  epi, bias, bias_ld, res, ld_res, aux, ld_aux, st);
   const int g = try_gemv(act, act_t, lda, m, k, nw, ws, outs, ldos, epi, bias, bias_ld, res, ld_res, aux, ld_aux, st);
   if (g != 0) return g < 0 ? -1 : 0;
   SkinnyArgs a{};
@@ -478,6 +493,149 @@ static void* workspace_for(size_t bytes, hipStream_t st) {
   return p;
 }
 
+// ------------------------------------------------------------------------------------------------ int8 compute
+// The reference's comp_int8 arithmetic (woq_i8.hip) for weights packed for an integer core (the blob carries the bf16
+// reduce).  Off by default: the fp16-MFMA path on exact weights is the more accurate one.  Mode 1 (nad_set_compute_mode
+// or NAD_COMPUTE_INT8=1) reproduces the reference: u8 activations per (row, block), s32 block dots, the kblock core's
+// fp32 combine.
+static int g_compute_mode = -1;
+static int compute_mode() {
+  if (g_compute_mode < 0) g_compute_mode = env_int("NAD_COMPUTE_INT8", 0) ? 1 : 0;
+  return g_compute_mode;
+}
+static bool int8_compute(const DeviceWeight& w) { return compute_mode() == 1 && w.reduce != nullptr; }
+
+extern "C" int nad_set_compute_mode(int mode) {
+  if (mode != 0 && mode != 1) {
+    set_err("compute mode must be 0 (fp) or 1 (int8 for integer-core weights), got %d", mode);
+    return -1;
+  }
+  g_compute_mode = mode;
+  return 0;
+}
+extern "C" int nad_get_compute_mode(void) { return compute_mode(); }
+
+struct I8Act {
+  const int8_t* aq = nullptr;
+  int ldq = 0;
+  const float2* sa = nullptr;
+};
+
+static size_t i8_act_bytes(int m, const DeviceWeight& w) {
+  return align256(size_t(m) * w.nt * tile_k(w.bits)) + align256(size_t(m) * w.ng * sizeof(float2));
+}
+
+static int i8_quantize(I8Act& r, char* ws, const void* act, int act_t, int lda, int m, int k, const DeviceWeight& w,
+                       hipStream_t st) {
+  const int kp = w.nt * tile_k(w.bits);
+  QuantU8Args q{};
+  q.A = act;
+  q.lda = lda;
+  q.M = m;
+  q.K = k;
+  q.bs = w.blob_bs;
+  q.ng = w.ng;
+  q.shuffle = w.shuffle;
+  q.aq = reinterpret_cast<int8_t*>(ws);
+  q.ldq = kp;
+  q.kp = kp;
+  q.sa = reinterpret_cast<float2*>(ws + align256(size_t(m) * kp));
+  hipError_t e = launch_quant_u8(q, act_t, st);
+  if (e != hipSuccess) {
+    set_err("activation quantization launch failed: %s", hipGetErrorString(e));
+    return -1;
+  }
+  r.aq = q.aq;
+  r.ldq = kp;
+  r.sa = q.sa;
+  return 0;
+}
+
+static int i8_gemm(const I8Act& x, int m, int k, const DeviceWeight& w, float* out, int ldo, int epi,
+                   const float* bias, int bias_ld, const float* res, int ld_res, const float* aux, int ld_aux,
+                   hipStream_t st) {
+  I8Args a{};
+  a.aq = x.aq;
+  a.ldq = x.ldq;
+  a.sa = x.sa;
+  a.M = m;
+  a.K = k;
+  a.red = static_cast<const uint16_t*>(w.reduce);
+  a.red_ld = w.red_ld;
+  a.scale_t = w.scale_t;
+  a.epi = epi;
+  a.res = res;
+  a.ld_res = ld_res;
+  a.aux = aux;
+  a.ld_aux = ld_aux;
+  a.w = view(w, out, ldo, bias, bias_ld);
+  hipError_t e = launch_i8(a, w.bits, st);
+  if (e != hipSuccess) {
+    set_err("int8-compute kernel launch failed: %s", hipGetErrorString(e));
+    return -1;
+  }
+  return 0;
+}
+
+// nw weights on one activation.  dual: the FFN gate/up pair (outs[1] = act(x.w0) * (x.w1); aux, if given, receives
+// act(x.w0)), run as the prefill FFN does: two passes, the second multiplying by the first's output.
+static int run_i8(const void* act, int act_t, int lda, int m, int k, int nw, const DeviceWeight* const* ws,
+                  float* const* outs, const int* ldos, bool dual, int epi, const float* bias, int bias_ld,
+                  const float* res, int ld_res, const float* aux, int ld_aux, hipStream_t st) {
+  for (int i = 0; i < nw; i++)
+    if (!int8_compute(*ws[i])) {
+      set_err("int8 compute: every weight of a fused call needs an integer-core blob (with reduce)");
+      return -1;
+    }
+  const size_t abytes = i8_act_bytes(m, *ws[0]);
+  const bool own_t1 = dual && !aux;
+  const size_t t1bytes = own_t1 ? size_t(m) * ws[0]->n * sizeof(float) : 0;
+  char* wsp = static_cast<char*>(workspace_for(abytes + t1bytes, st));
+  if (!wsp) return -1;
+  I8Act x;
+  if (i8_quantize(x, wsp, act, act_t, lda, m, k, *ws[0], st)) return -1;
+  if (dual) {
+    float* t1 = own_t1 ? reinterpret_cast<float*>(wsp + abytes) : const_cast<float*>(aux);
+    const int ld1 = own_t1 ? ws[0]->n : ld_aux;
+    const int e1 = epi == kEpiSiluMul ? kEpiSilu : kEpiGelu;
+    if (i8_gemm(x, m, k, *ws[0], t1, ld1, e1, nullptr, 0, nullptr, 0, nullptr, 0, st)) return -1;
+    return i8_gemm(x, m, k, *ws[1], outs[1], ldos[1], kEpiSiluMul, nullptr, 0, nullptr, 0, t1, ld1, st);
+  }
+  for (int i = 0; i < nw; i++)
+    if (i8_gemm(x, m, k, *ws[i], outs[i], ldos[i], epi, bias, bias_ld, res, ld_res, aux, ld_aux, st)) return -1;
+  return 0;
+}
+
+extern "C" int nad_quant_u8_colblock(const void* act, int act_dtype, int m, int k, int lda, int blocksize,
+                                     uint8_t* q, int ldq, float* scales, uint8_t* zps, int ld_scale, float* blkreduce,
+                                     void* queue) {
+  if (m <= 0 || k <= 0 || blocksize <= 0 || lda < k || ldq < k || !q || !scales || !zps ||
+      ld_scale < (k + blocksize - 1) / blocksize) {
+    set_err("nad_quant_u8_colblock: bad arguments (m=%d k=%d lda=%d ldq=%d blocksize=%d ld_scale=%d)", m, k, lda, ldq,
+            blocksize, ld_scale);
+    return -1;
+  }
+  QuantU8Args a{};
+  a.A = act;
+  a.lda = lda;
+  a.M = m;
+  a.K = k;
+  a.bs = blocksize;
+  a.ng = (k + blocksize - 1) / blocksize;
+  a.q_u8 = q;
+  a.ldu = ldq;
+  a.s_out = scales;
+  a.z_out = zps;
+  a.red_out = blkreduce;
+  a.ld_scale = ld_scale;
+  hipError_t e = launch_quant_u8(a, act_dtype, static_cast<hipStream_t>(queue));
+  if (e != hipSuccess) {
+    set_err("activation quantization launch failed: %s", hipGetErrorString(e));
+    return -1;
+  }
+  return 0;
+}
+
 // fp16 activations for the pipelined prefill GEMM (woq_gemm2.hip): the caller's rows when they already are fp16,
 // aligned, unshuffled and tile-padded, else one conversion pass into the workspace.  One conversion serves every GEMM
 // that reads the same activations (the QKV and gate/up fusions).
@@ -493,8 +651,7 @@ static int pipelined_gemm(const DeviceWeight& w, int m) {
     return 0;
   const int tpg = w.blocksize / 128;
   if (w.bits == 4 && w.blocksize % 128 == 0 && (tpg & (tpg - 1)) == 0 && !env_int("NAD_GEMM4_ALL", 0)) return 3;
-  const int kt = w.bits == 4 ? 128 : 256;
-  if (!env_int("NAD_GEMM4_DISABLE", 0) && gemm4_mode(w.bits, w.blocksize, w.ng, w.nt * kt, w.asym)) return 4;
+  if (!env_int("NAD_GEMM4_DISABLE", 0) && gemm4_mode(w.bits, w.blocksize, w.ng, w.nt * tile_k(w.bits), w.asym)) return 4;
   return 0;
 }
 static bool gemm2_ok(const DeviceWeight& w, int m) { return pipelined_gemm(w, m) != 0; }
@@ -526,6 +683,12 @@ static int prepare_a16(A16& r, const void* act, int act_t, int lda, int m, int k
 static int run_gemm(const void* act, int act_t, int lda, int m, int k, const DeviceWeight& w, float* out, int ldo,
                     int epi, const float* bias, int bias_ld, const float* res, int ld_res, const float* aux,
                     int ld_aux, hipStream_t st, const A16* pre = nullptr) {
+  if (int8_compute(w)) {
+    const DeviceWeight* ws[1] = {&w};
+    float* outs[1] = {out};
+    const int ldos[1] = {ldo};
+    return run_i8(act, act_t, lda, m, k, 1, ws, outs, ldos, false, epi, bias, bias_ld, res, ld_res, aux, ld_aux, st);
+  }
   GemmArgs a{};
   a.A = act;
   a.lda = lda;
@@ -630,7 +793,7 @@ extern "C" int nad_device_qkv_forward(const void* act, int act_dtype, const void
     return run_skinny(act, act_dtype, lda, m, k, 3, ws, outs, ldos, kEpiNone, nullptr, 0, nullptr, 0, nullptr, 0, st);
   A16 pre;
   const A16* pp = nullptr;
-  if (gemm2_ok(*ws[0], m) && !ws[0]->shuffle) {
+  if (gemm2_ok(*ws[0], m) && !ws[0]->shuffle && !int8_compute(*ws[0])) {
     if (prepare_a16(pre, act, act_dtype, lda, m, k, *ws[0], st) < 0) return -1;
     pp = &pre;
   }
@@ -670,7 +833,7 @@ extern "C" int nad_device_ffn_gate_up(const void* act, int act_dtype, const void
   const int e1 = epi == kEpiSiluMul ? kEpiSilu : kEpiGelu;
   A16 pre;
   const A16* pp = nullptr;
-  if (gemm2_ok(*w1, m) && !w1->shuffle) {
+  if (gemm2_ok(*w1, m) && !w1->shuffle && !int8_compute(*w1)) {
     if (prepare_a16(pre, act, act_dtype, lda, m, fin, *w1, st) < 0) return -1;
     pp = &pre;
   }
@@ -735,6 +898,11 @@ extern "C" void* nad_chain_create(const nad_chain_op* ops, int n_ops, int m) {
     for (int j = 0; j < nw; j++)
       if (!(ws[j] = as_weight(o.w[j]))) return nullptr;
     const DeviceWeight& w0 = *ws[0];
+    for (int j = 0; j < nw; j++)
+      if (int8_compute(*ws[j])) {
+        set_err("nad_chain_create: op %d runs in the int8-compute mode, which the chain does not implement", i);
+        return nullptr;
+      }
     if (w0.bits != 4 || w0.has_shuffle || w0.kmajor || w0.blocksize % 128 != 0 || o.act_dtype != act_t ||
         (asym >= 0 && asym != w0.asym)) {
       set_err("nad_chain_create: op %d is not a chain op (int4, group >= 128, no shuffle, one act dtype/symmetry)", i);

@@ -36,15 +36,20 @@ constexpr int LDS_BUDGET = 160 * 1024;
 
 template <int BITS>
 constexpr int hpt() {
-  return BITS == 4 ? 2 : 4;
+  return BITS == 4 ? 2 : (BITS == 2 ? 4 : 1);
 }
 template <int BITS, bool G32>
 constexpr int gslots() {
-  return G32 ? 4 : hpt<BITS>();
+  return G32 ? 2 * hpt<BITS>() : hpt<BITS>();
+}
+// zero points: one byte per column per group, [slot][stripe][16] -- 128 B a slot, filled 256 B (two slots) per wave load
+template <int BITS, bool G32>
+constexpr int zpbytes() {
+  return (gslots<BITS, G32>() < 2 ? 2 : gslots<BITS, G32>()) * 128;
 }
 template <int BITS, bool G32, bool ASYM>
 constexpr int bbuf() {
-  return BTILES + gslots<BITS, G32>() * 512 * (ASYM ? 2 : 1);
+  return BTILES + gslots<BITS, G32>() * 512 + (ASYM ? zpbytes<BITS, G32>() : 0);
 }
 template <int BITS, bool G32, bool ASYM>
 constexpr int nbr() {
@@ -53,7 +58,7 @@ constexpr int nbr() {
 template <int BITS, bool G32, bool ASYM>
 constexpr int lds_bytes() {
   // a 2-deep ring is only safe when a tile spans more than two half steps (int2)
-  static_assert(hpt<BITS>() > 2 || nbr<BITS, G32, ASYM>() == 3, "int4 needs a 3-deep B ring");
+  static_assert(hpt<BITS>() > 2 || nbr<BITS, G32, ASYM>() == 3, "int4 / int8 need a 3-deep B ring");
   return NA * HBUF + nbr<BITS, G32, ASYM>() * bbuf<BITS, G32, ASYM>();
 }
 
@@ -107,6 +112,24 @@ __device__ __forceinline__ h8_t dq2(uint32_t w, int sh, h2_t c) {
   return r;
 }
 
+// int8: 8 bytes (two dwords) -> 8 exact fp16 (q - 128 - zp): byte b becomes the fp16 1024 + b by a byte permute
+__device__ __forceinline__ h8_t dq8(uint32_t w0, uint32_t w1, h2_t c) {
+  const h2_t p0 = as_h2(__builtin_amdgcn_perm(0x64646464u, w0, 0x04010400u)) + c;
+  const h2_t p1 = as_h2(__builtin_amdgcn_perm(0x64646464u, w0, 0x04030402u)) + c;
+  const h2_t p2 = as_h2(__builtin_amdgcn_perm(0x64646464u, w1, 0x04010400u)) + c;
+  const h2_t p3 = as_h2(__builtin_amdgcn_perm(0x64646464u, w1, 0x04030402u)) + c;
+  h8_t r;
+  r[0] = p0[0];
+  r[1] = p0[1];
+  r[2] = p1[0];
+  r[3] = p1[1];
+  r[4] = p2[0];
+  r[5] = p2[1];
+  r[6] = p3[0];
+  r[7] = p3[1];
+  return r;
+}
+
 __device__ __forceinline__ void glds16(const void* g, char* l) {
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
                                    (__attribute__((address_space(3))) void*)l, 16, 0, 0);
@@ -123,6 +146,12 @@ __device__ __forceinline__ void wait_vm() {
 template <int OFF>
 __device__ __forceinline__ h8_t lds_b128(uint32_t addr) {
   h8_t r;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "n"(OFF));
+  return r;
+}
+template <int OFF>
+__device__ __forceinline__ u4_t lds_u128(uint32_t addr) {
+  u4_t r;
   asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "n"(OFF));
   return r;
 }
@@ -169,7 +198,11 @@ __global__ __launch_bounds__(512, 1) void woq_gemm4_kernel(GemmArgs a, const _Fl
   constexpr int BBUF = bbuf<BITS, G32, ASYM>();
   constexpr int NBR = nbr<BITS, G32, ASYM>();
   constexpr int NBW = ASYM ? 3 : 2;  // B-side VMEM instructions of a tile batch, per wave
-  constexpr int BIAS = BITS == 4 ? 8 : 2;
+  constexpr int ZPB = zpbytes<BITS, G32>();
+  constexpr int BIAS = BITS == 4 ? 8 : (BITS == 2 ? 2 : 128);
+  // int8: a tile is one half step, so the tile rides two half steps ahead (not three, as A does): a 4-deep tile ring
+  // would not fit beside the A ring.  Its batch is [tile (u + 2), A (u + 3)], tile first.
+  constexpr bool B2 = BITS == 8;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));
@@ -203,7 +236,11 @@ __global__ __launch_bounds__(512, 1) void woq_gemm4_kernel(GemmArgs a, const _Fl
   const char* btile = static_cast<const char*>(W.tiles) + (size_t(min(bn * 8 + wave, ns - 1)) * nt * 64 + lane) * 16;
   const int sstripe = min(bn * 8 + (wave & 1) * 4 + (lane >> 4), ns - 1);
   const size_t srow0 = size_t(sstripe) * ng * 16 + nl;
-  const int slot_w = (wave >> 1) % GS;  // this wave's scale / zero-point slot
+  const int slot_w = (wave >> 1) % GS;  // this wave's scale slot
+  // zero-point piece of this wave: slots 2 zq, 2 zq + 1 (lanes 0-31 / 32-63), stripe (lane >> 2) & 7, 4 columns a lane
+  const int zq = wave % (ZPB / 256);
+  const int zslot = min(2 * zq + (lane >> 5), GS - 1);
+  const size_t zrow0 = size_t(min(bn * 8 + ((lane >> 2) & 7), ns - 1)) * ng * 16 + (lane & 3) * 4;
   const int st = a.scale_t;
   const uint32_t* sbase = static_cast<const uint32_t*>(W.scales);
   const uint32_t* zbase = reinterpret_cast<const uint32_t*>(W.zps);
@@ -212,29 +249,32 @@ __global__ __launch_bounds__(512, 1) void woq_gemm4_kernel(GemmArgs a, const _Fl
   auto slot_group = [&](int t, int s) {
     int g;
     if constexpr (G32)
-      g = t * 4 + s;
+      g = t * (2 * HPT) + s;
     else
       g = ((t * HPT) >> gh_log2) + (gh_log2 < 30 ? min(s, max(HPT >> gh_log2, 1) - 1) : 0);
     return min(g, ng - 1);
   };
 
   // batch(u): A(u + 3) and, when u + 3 starts a tile, that tile + its scale (+ zero-point) pieces
+  auto issue_tile = [&](int t) {
+    char* bb = smem + NA * HBUF + (t % NBR) * BBUF;
+    glds16(btile + size_t(t) * 1024, bb + wave * 1024);
+    const size_t si = srow0 + size_t(slot_group(t, slot_w)) * 16;
+    glds4(sbase + (st == kScaleF32 ? si : (si >> 1)), bb + BTILES + slot_w * 512 + (wave & 1) * 256);
+    if constexpr (ASYM) glds4(zbase + ((zrow0 + size_t(slot_group(t, zslot)) * 16) >> 2), bb + BTILES + BSC + zq * 256);
+  };
   auto issue = [&](auto Pc, int u) {
     constexpr int P = decltype(Pc)::value;  // (u + 3) % HPT
+    if constexpr (B2) {
+      if (u + 2 >= 0 && u + 2 < nh) issue_tile(u + 2);
+    }
     if (u + 3 >= nh) return;
     const int ua = u + 3;
     char* ab = smem + (ua & 3) * HBUF;
     const char* src = abase + size_t(ua) * ROWB;
 #pragma unroll
     for (int i = 0; i < 4; i++) glds16(src + aoff[i], ab + (wave * 4 + i) * 1024);
-    if constexpr (P == 0) {
-      const int t = ua / HPT;
-      char* bb = smem + NA * HBUF + (t % NBR) * BBUF;
-      glds16(btile + size_t(t) * 1024, bb + wave * 1024);
-      const size_t si = srow0 + size_t(slot_group(t, slot_w)) * 16;
-      glds4(sbase + (st == kScaleF32 ? si : (si >> 1)), bb + BTILES + slot_w * 512 + (wave & 1) * 256);
-      if constexpr (ASYM) glds4(zbase + (si >> 2), bb + BTILES + BSC + slot_w * 512 + (wave & 1) * 256);
-    }
+    if constexpr (!B2 && P == 0) issue_tile(ua / HPT);
   };
 
   f4_t acc[8][2], accg[8][2];
@@ -251,7 +291,14 @@ __global__ __launch_bounds__(512, 1) void woq_gemm4_kernel(GemmArgs a, const _Fl
   issue(std::integral_constant<int, 1 % HPT>{}, -2);
   issue(std::integral_constant<int, 2 % HPT>{}, -1);
   // wait for batch -3: batches -2 and -1 may stay in flight
-  {
+  if constexpr (B2) {  // batch -2 = [tile 0, A1], batch -1 = [tile 1, A2]: tile 0 landed, A1 + batch -1 in flight
+    if (nh > 2)
+      wait_vm<8 + NBW>();
+    else if (nh > 1)
+      wait_vm<4 + NBW>();
+    else
+      wait_vm<0>();
+  } else {
     constexpr int b2 = 4 + ((1 % HPT) == 0 ? NBW : 0), b1 = 4 + ((2 % HPT) == 0 ? NBW : 0);
     if (nh > 2)
       wait_vm<b2 + b1>();
@@ -270,7 +317,7 @@ __global__ __launch_bounds__(512, 1) void woq_gemm4_kernel(GemmArgs a, const _Fl
   for (int dd = 0; dd < 2; dd++) roff[dd] = uint32_t((wm * 128 + nl) * ROWB + (((dd * 4 + kq) ^ ((nl >> 1) & 7)) * 16));
   const int boff = (wn * 2) * 1024 + lane * 16;
   const int soff = BTILES + ((wn * 2) * 16 + nl) * 4;
-  const int zoff = BTILES + BSC + ((wn * 2) * 16 + nl) * 4;
+  const int zoff = BTILES + BSC + (wn * 2) * 16 + (nl & ~3);
   const int ssh = st == kScaleF32 ? 0 : (nl & 1) * 16;
   const int zsh = (nl & 3) * 8;
   const f4_t zero = {0.f, 0.f, 0.f, 0.f};
@@ -291,7 +338,12 @@ __global__ __launch_bounds__(512, 1) void woq_gemm4_kernel(GemmArgs a, const _Fl
     const uint32_t al = lds_addr(ab), bl = lds_addr(bb);
     // B words of this half step for the wave's two stripes: int4 two dwords (one per 32-deep step), int2 one dword
     uint32_t bw[2][2];
-    if constexpr (BITS == 4) {
+    u4_t b8[2];
+    if constexpr (BITS == 8) {
+      b8[0] = lds_u128<0>(bl + boff);
+      b8[1] = lds_u128<1024>(bl + boff);
+      bw[0][0] = bw[0][1] = bw[1][0] = bw[1][1] = 0u;
+    } else if constexpr (BITS == 4) {
       const uint2 v0 = lds_b64<H * 8>(bl + boff), v1 = lds_b64<1024 + H * 8>(bl + boff);
       bw[0][0] = v0.x;
       bw[0][1] = v0.y;
@@ -308,12 +360,12 @@ __global__ __launch_bounds__(512, 1) void woq_gemm4_kernel(GemmArgs a, const _Fl
     const int slot = G32 ? 2 * H : (gh_log2 >= 30 ? 0 : (H >> gh_log2) % GS);
     uint32_t zw[2][2] = {{0u, 0u}, {0u, 0u}};
     if constexpr (ASYM) {
-      const uint32_t za = bl + zoff + slot * 512;
+      const uint32_t za = bl + zoff + slot * 128;
       zw[0][0] = lds_b32v(za);
-      zw[1][0] = lds_b32v(za + 64);
+      zw[1][0] = lds_b32v(za + 16);
       if constexpr (G32) {
-        zw[0][1] = lds_b32v(za + 512);
-        zw[1][1] = lds_b32v(za + 512 + 64);
+        zw[0][1] = lds_b32v(za + 128);
+        zw[1][1] = lds_b32v(za + 128 + 16);
       }
     }
     // G32: both groups' scales up front, so each 32-deep step's products scale straight into the result
@@ -328,7 +380,7 @@ __global__ __launch_bounds__(512, 1) void woq_gemm4_kernel(GemmArgs a, const _Fl
     h8_t af0[8], af1[8];
     lds_frags(af0, al + roff[0], std::make_index_sequence<8>{});
     lds_frags(af1, al + roff[1], std::make_index_sequence<8>{});
-    wait_lgk<8>(bw[0][0], bw[0][1], bw[1][0], bw[1][1], zw[0][0], zw[0][1], zw[1][0], zw[1][1], sg[0][0], sg[0][1],
+    wait_lgk<8>(b8[0], b8[1], bw[0][0], bw[0][1], bw[1][0], bw[1][1], zw[0][0], zw[0][1], zw[1][0], zw[1][1], sg[0][0], sg[0][1],
                 sg[1][0], sg[1][1], af0[0], af0[1], af0[2], af0[3], af0[4], af0[5], af0[6], af0[7]);
     const bool gstart = G32 || (u & (gh - 1)) == 0;
     const bool gend = G32 || ((u + 1) & (gh - 1)) == 0 || u == nh - 1;
@@ -340,7 +392,9 @@ __global__ __launch_bounds__(512, 1) void woq_gemm4_kernel(GemmArgs a, const _Fl
 #pragma unroll
       for (int j = 0; j < 2; j++) {
         const float zf = ASYM ? float(int(int8_t((zw[j][zi] >> zsh) & 0xFFu))) : 0.f;
-        if constexpr (BITS == 4)
+        if constexpr (BITS == 8)
+          bf[j] = dq8(b8[j][2 * dd], b8[j][2 * dd + 1], zc0 - splat(zf));
+        else if constexpr (BITS == 4)
           bf[j] = dq4(bw[j][dd], s16, zc0 - splat(zf), zc1 - splat(zf));
         else
           bf[j] = dq2(bw[j][0], dd * 8, zc0 - splat(zf));
@@ -391,21 +445,30 @@ __global__ __launch_bounds__(512, 1) void woq_gemm4_kernel(GemmArgs a, const _Fl
       }
     }
     // hand-over: batch u - 2 has landed; batches u - 1 and u stay in flight
-    constexpr int bu = 4 + (((H + 3) % HPT) == 0 ? NBW : 0);       // |batch u| (when issued)
-    constexpr int bu1 = 4 + (((H + 2) % HPT) == 0 ? NBW : 0);      // |batch u - 1|
-    if (u + 3 < nh)
-      wait_vm<bu + bu1>();
-    else if (u + 2 < nh)
-      wait_vm<bu1>();
-    else
-      wait_vm<0>();
+    if constexpr (B2) {  // tile u + 1 (head of batch u - 1) and A(u + 1) landed; A(u + 2) and batch u in flight
+      if (u + 3 < nh)
+        wait_vm<8 + NBW>();
+      else if (u + 2 < nh)
+        wait_vm<4 + NBW>();
+      else
+        wait_vm<0>();
+    } else {
+      constexpr int bu = 4 + (((H + 3) % HPT) == 0 ? NBW : 0);   // |batch u| (when issued)
+      constexpr int bu1 = 4 + (((H + 2) % HPT) == 0 ? NBW : 0);  // |batch u - 1|
+      if (u + 3 < nh)
+        wait_vm<bu + bu1>();
+      else if (u + 2 < nh)
+        wait_vm<bu1>();
+      else
+        wait_vm<0>();
+    }
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
   };
 
   for (int u = 0; u < nh; u += HPT) {
     half(std::integral_constant<int, 0>{}, u);
-    half(std::integral_constant<int, 1>{}, u + 1);
+    if constexpr (HPT >= 2) half(std::integral_constant<int, 1>{}, u + 1);
     if constexpr (HPT == 4) {
       half(std::integral_constant<int, 2>{}, u + 2);
       half(std::integral_constant<int, 3>{}, u + 3);
@@ -476,9 +539,10 @@ __global__ __launch_bounds__(512, 1) void woq_gemm4_kernel(GemmArgs a, const _Fl
 // per group, 30 = one group over all of K)
 constexpr int kG32Mode = 100;
 int gemm4_mode(int bits, int blocksize, int ng, int kpad, bool asym) {
-  if (bits != 4 && bits != 2) return 0;
+  if (bits != 4 && bits != 2 && bits != 8) return 0;
+  (void)asym;
   if (ng == 1) return 30 + 1;  // per-channel
-  if (bits == 4 && blocksize == 32) return asym ? 0 : kG32Mode;  // G32 + zero points: no room for a 3-deep B ring
+  if (blocksize == 32) return bits == 2 ? 0 : kG32Mode;
   if (blocksize < 64 || blocksize % 64) return 0;
   const int gh = blocksize / 64;
   if (gh & (gh - 1)) return 0;
@@ -487,7 +551,7 @@ int gemm4_mode(int bits, int blocksize, int ng, int kpad, bool asym) {
 }
 
 hipError_t launch_gemm4(const GemmArgs& a, int bits, const _Float16* A16, int lda16, hipStream_t st) {
-  const int mode = gemm4_mode(bits, a.w.bs, a.w.ng, a.w.nt * (bits == 4 ? 128 : 256), a.w.zps != nullptr);
+  const int mode = gemm4_mode(bits, a.w.bs, a.w.ng, a.w.nt * (bits == 4 ? 128 : (bits == 2 ? 256 : 64)), a.w.zps != nullptr);
   if (!mode) return hipErrorInvalidValue;
   const bool g32 = mode == kG32Mode;
   const int gh_log2 = g32 ? 0 : mode - 1;
@@ -502,8 +566,12 @@ hipError_t launch_gemm4(const GemmArgs& a, int bits, const _Float16* A16, int ld
   };
 #define NAD_G4(B, G, A) go(g4::woq_gemm4_kernel<B, G, A>, g4::lds_bytes<B, G, A>())
   if (bits == 4) {
-    if (g32) return NAD_G4(4, true, false);
+    if (g32) return asym ? NAD_G4(4, true, true) : NAD_G4(4, true, false);
     return asym ? NAD_G4(4, false, true) : NAD_G4(4, false, false);
+  }
+  if (bits == 8) {
+    if (g32) return asym ? NAD_G4(8, true, true) : NAD_G4(8, true, false);
+    return asym ? NAD_G4(8, false, true) : NAD_G4(8, false, false);
   }
   return asym ? NAD_G4(2, false, true) : NAD_G4(2, false, false);
 #undef NAD_G4

@@ -114,6 +114,39 @@ hipError_t launch_gemm3(const GemmArgs& a, const _Float16* A16, int lda16, hipSt
 // prefill GEMM v4 (woq_gemm4.hip): gemm3's pipeline for int4 groups of 32 / 64 and int2 groups >= 64.
 // gemm4_mode: 0 = not taken, else the group mode; A as for gemm3 with K padded to the weight's K tile (128 / 256)
 int gemm4_mode(int bits, int blocksize, int ng, int kpad, bool asym);
+
+// int8-compute mode (woq_i8.hip).  Activation quantizer: one thread per (row, block); any output may be null.
+struct QuantU8Args {
+  const void* A;
+  int lda, M, K, bs, ng;
+  const int32_t* shuffle;
+  int8_t* aq;           // [M][ldq] s8 = u8 - 128, zero in [K, kp)
+  int ldq, kp;
+  float2* sa;           // [M][ng] {scale, float(zp) * scale}
+  uint8_t* q_u8;        // [M][ldu] the reference's u8 codes
+  int ldu;
+  float* s_out;         // [M][ld_scale]
+  uint8_t* z_out;
+  float* red_out;       // sum(q - zp... as kernel_ref: sum of round(x / s)) * s
+  int ld_scale;
+};
+struct I8Args {
+  const int8_t* aq;
+  int ldq;
+  const float2* sa;     // [M][ng]
+  int M, K;
+  const uint16_t* red;  // bf16 reduce [ng][red_ld]
+  int red_ld;
+  int scale_t;
+  int epi;
+  const float* res;
+  int ld_res;
+  const float* aux;
+  int ld_aux;
+  SkinnyWeight w;
+};
+hipError_t launch_quant_u8(const QuantU8Args& a, int act_t, hipStream_t stream);
+hipError_t launch_i8(const I8Args& a, int bits, hipStream_t stream);
 hipError_t launch_gemm4(const GemmArgs& a, int bits, const _Float16* A16, int lda16, hipStream_t stream);
 hipError_t launch_cvt_act(const void* A, int act_t, int lda, int M, int K, int Kp, const int32_t* shuffle,
                           _Float16* out, hipStream_t stream);

@@ -17,6 +17,7 @@
 //   scales : [ns][ngroups][16] (or K-major [ngroups][ns][16]) in the blob's scale dtype (f32 / bf16 / f16)
 //   zps    : same order as scales, int8 (asym only)
 //   shuffle: [K] int32 act-order LUT (GPTQ desc_act), applied as a gather on the A operand
+//   reduce : [ngroups][ns*16] bf16, integer-core blobs only (the int8-compute mode's zero-point correction)
 #pragma once
 #include <cstdint>
 
@@ -49,6 +50,9 @@ struct DeviceWeight {
   int8_t* zps;
   int32_t* shuffle;
   void* owner;        // non-null when the library allocated the device memory itself (nad_* helpers)
+  void* reduce;       // bf16 [ng][red_ld]: the blob's reduce (Sum_k dequant(w) per block), integer-core blobs only
+  int32_t red_ld;     // 0: no reduce
+  int32_t blob_bs;    // the blob's own block size (per-channel: may exceed K; the int8-compute quantizer uses it)
 };
 
 // Tile (s, t) and scale row (s, g) positions.  K-major interleaves the stripes at every K position, so the waves of a
@@ -68,7 +72,7 @@ inline uint64_t align256(uint64_t x) { return (x + 255) & ~uint64_t(255); }
 
 // fill the geometry of a DeviceWeight and return the device bytes it needs
 inline uint64_t layout_geometry(DeviceWeight& w, int bits, int n, int k, int blocksize, int scale_t, bool asym,
-                                bool shuffle, int kmajor = 0) {
+                                bool shuffle, int kmajor = 0, bool reduce = false) {
   w.magic = kWeightMagic;
   w.kmajor = kmajor;
   w.bits = bits;
@@ -85,7 +89,10 @@ inline uint64_t layout_geometry(DeviceWeight& w, int bits, int n, int k, int blo
   uint64_t sbytes = uint64_t(w.ns) * w.ng * 16 * (scale_t == kScaleF32 ? 4 : 2);
   uint64_t zbytes = asym ? uint64_t(w.ns) * w.ng * 16 : 0;
   uint64_t shf = shuffle ? uint64_t(k) * 4 : 0;
-  return align256(tiles) + align256(sbytes) + align256(zbytes) + align256(shf);
+  w.red_ld = reduce ? w.ns * 16 : 0;
+  w.blob_bs = blocksize;
+  uint64_t rbytes = uint64_t(w.ng) * w.red_ld * 2;
+  return align256(tiles) + align256(sbytes) + align256(zbytes) + align256(shf) + align256(rbytes);
 }
 
 inline void layout_assign(DeviceWeight& w, void* base) {
@@ -101,6 +108,8 @@ inline void layout_assign(DeviceWeight& w, void* base) {
   p += align256(zbytes);
   w.shuffle = w.has_shuffle ? reinterpret_cast<int32_t*>(p) : nullptr;
   p += w.has_shuffle ? align256(uint64_t(w.k) * 4) : 0;
+  w.reduce = w.red_ld ? p : nullptr;
+  p += align256(uint64_t(w.ng) * w.red_ld * 2);
   w.bytes = uint64_t(p - static_cast<char*>(base));
 }
 

@@ -5,6 +5,7 @@
  */
 #include "btla_oracle.h"
 
+#include <float.h>
 #include <math.h>
 #include <stdlib.h>
 #include <string.h>
@@ -775,4 +776,131 @@ int orc_blob_gemv_timed(const float* A, const void* blob, float* C, int m, int l
   int r = 0;
   for (int it = 0; it < iters && r == 0; it++) r = orc_blob_gemv_ref(A, blob, C, m, lda, ldc);
   return r;
+}
+
+/* ------------------------------------------------------------------ int8 compute (comp_int8) */
+/* bestla_utils.h cast<float,uint8_t>: +0.5, clamp to [0,255], truncating conversion (x86 cvttss2si, low byte) */
+static inline uint8_t cast_f32_u8(float v) {
+  v += 0.5f;
+  v = smin(v, 255.f);
+  v = smax(v, 0.f);
+  return (uint8_t)(f2i_x86(v) & 0xff);
+}
+
+/* kernel_ref.h:1824-1883 quantize_fp_u8_colblock: per (row, block of `blocksize` columns) asymmetric u8.  Full blocks
+   start the running max at FLT_MIN (std::numeric_limits<float>::min()), the ragged tail block at 0. */
+static void quant_u8_block(const float* x, int len, float maxinit, uint8_t* dst, float* scale_out, uint8_t* zp_out,
+                           float* red_out) {
+  float maxval = maxinit, minval = 0.f;
+  for (int j = 0; j < len; j++) {
+    maxval = smax(x[j], maxval);
+    minval = smin(x[j], minval);
+  }
+  float scale = (maxval - minval) / 255;
+  uint8_t zp = cast_f32_u8((0 - minval) / scale);
+  float rscale = 1.f / scale;
+  *scale_out = scale;
+  *zp_out = zp;
+  int32_t sum = 0;
+  float zpf = (float)zp;
+  for (int j = 0; j < len; j++) {
+    int32_t q = cast_f32_int(x[j] * rscale);
+    sum = iadd_wrap(sum, q);
+    dst[j] = cast_f32_u8(zpf + (float)q);
+  }
+  if (red_out) *red_out = (float)sum * scale;
+}
+
+void orc_quant_u8_colblock(int row, int col, const float* src, int ld_src, uint8_t* dst, int ld_dst, float* scales,
+                           int ld_scale, uint8_t* zps, int blocksize, float* blkreduce) {
+  int colblk = (col / blocksize) * blocksize;
+  for (int i = 0; i < row; i++) {
+    int j = 0;
+    for (; j < colblk; j += blocksize) {
+      size_t si = (size_t)(j / blocksize) + (size_t)i * ld_scale;
+      quant_u8_block(src + (size_t)i * ld_src + j, blocksize, FLT_MIN, dst + (size_t)i * ld_dst + j, scales + si,
+                     zps + si, blkreduce ? blkreduce + si : NULL);
+    }
+    if (j < col) {
+      size_t si = (size_t)(j / blocksize) + (size_t)i * ld_scale;
+      quant_u8_block(src + (size_t)i * ld_src + j, col - j, 0.f, dst + (size_t)i * ld_dst + j, scales + si, zps + si,
+                     blkreduce ? blkreduce + si : NULL);
+    }
+  }
+}
+
+/* LauncherIntKBlock::run_block (bestla_wrapper.h:768-831) with a kblock u8s8 core (bestla_gemm.h:2899-3050): the
+   activation (act-order gathered first, bestla_prologue_a.h:407-422) is quantized per (row, weight block) by
+   quantize_fp_u8_colblock; per block: s32 = sum a_u8 * (q - zp), then C += float(s32) * (sA * sB) and
+   C -= (float(zpA) * sA * 1.f) * reduceB, blocks in K order.  reduceB is the blob's bf16 reduce (Sum_k dequant(w)). */
+int orc_blob_forward_int8(const float* A, const void* blob, float* C, int m, int n, int k, int lda, int ldc) {
+  blob_t b;
+  int r = blob_parse(&b, blob);
+  if (r) return r;
+  if (b.n != n || b.k != k) return -4;
+  if (!b.has_red) return -5;
+  const int8_t* base = (const int8_t*)blob;
+  int nblk = (int)updiv((size_t)k, (size_t)b.bs);
+  int8_t* Q = (int8_t*)malloc((size_t)k * n);
+  float* S = (float*)malloc(sizeof(float) * (size_t)nblk * n);
+  int8_t* Z = (int8_t*)malloc((size_t)nblk * n);
+  blob_dequant(&b, base, NULL, 0, Q, S, Z);
+  const uint16_t* red = (const uint16_t*)(base + b.r_off);
+  float* Ash = (float*)malloc(sizeof(float) * (size_t)m * k);
+  const int* idx = b.has_shf ? (const int*)(base + b.shf_off) : NULL;
+  for (int i = 0; i < m; i++)
+    for (int j = 0; j < k; j++) Ash[(size_t)i * k + j] = A[(size_t)i * lda + (idx ? idx[j] : j)];
+  uint8_t* a8 = (uint8_t*)malloc((size_t)m * k);
+  float* sa = (float*)malloc(sizeof(float) * (size_t)m * nblk);
+  uint8_t* za = (uint8_t*)malloc((size_t)m * nblk);
+  orc_quant_u8_colblock(m, k, Ash, k, a8, k, sa, nblk, za, b.bs, NULL);
+  for (int i = 0; i < m; i++)
+    for (int nn = 0; nn < n; nn++) {
+      float c = 0.f;
+      for (int g = 0; g < nblk; g++) {
+        int k0 = g * b.bs, k1 = k0 + b.bs < k ? k0 + b.bs : k;
+        int zb = Z[(size_t)g * n + nn];
+        int32_t dot = 0;
+        for (int kk = k0; kk < k1; kk++)
+          dot += (int32_t)a8[(size_t)i * k + kk] * (int32_t)(Q[(size_t)kk * n + nn] - zb);
+        float sA = sa[(size_t)i * nblk + g], sB = S[(size_t)g * n + nn];
+        float t = sA * sB;
+        c = c + (float)dot * t;
+        float zc = (float)za[(size_t)i * nblk + g] * sA * 1.f;
+        c = c - zc * orc_bf16_to_f32(red[(size_t)g * b.cstep + nn]);
+      }
+      C[(size_t)i * ldc + nn] = c;
+    }
+  free(Q);
+  free(S);
+  free(Z);
+  free(Ash);
+  free(a8);
+  free(sa);
+  free(za);
+  return 0;
+}
+
+/* kernel_ref.h:2371-2429 gemv_4bit_u8s8_fp32 restated over unpacked operands: a8 [m][k] u8, as/azp [m][nblk],
+   q [k][n] signed int4 values (nibble - 8), s [nblk][n], zp [nblk][n] (NULL: symmetric).  Float accumulation per
+   element in the reference's order: blocks, then k in fours, then the four k of a PACK_ROW group. */
+void orc_gemv_u8s8_ref(int m, int n, int k, int bs, const uint8_t* a8, const float* as, const uint8_t* azp,
+                       const int8_t* q, const float* s, const int8_t* zp, float* C) {
+  int blks = k / bs;
+  for (int im = 0; im < m; im++)
+    for (int in = 0; in < n; in++) {
+      float acc = 0.f;
+      for (int ib = 0; ib < blks; ib++) {
+        int az = azp[(size_t)im * blks + ib];
+        float asc = as[(size_t)im * blks + ib];
+        float vscale = asc * s[(size_t)ib * n + in];
+        int bz = zp ? zp[(size_t)ib * n + in] : 0;
+        for (int ik = 0; ik < bs; ik++) {
+          int kk = ib * bs + ik;
+          int prod = ((int)a8[(size_t)im * k + kk] - az) * ((int)q[(size_t)kk * n + in] - bz);
+          acc += (float)prod * vscale;
+        }
+      }
+      C[(size_t)im * n + in] = acc;
+    }
 }

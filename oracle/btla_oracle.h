@@ -97,6 +97,16 @@ int orc_blob_gemv_ref(const float* A, const void* blob, float* C, int m, int lda
 int orc_blob_gemv_par(const float* A, const void* blob, float* C, int m, int lda, int ldc, int threads);
 int orc_blob_gemv_timed(const float* A, const void* blob, float* C, int m, int lda, int ldc, int iters);
 
+
+/* int8 compute (comp_int8): kernel_ref.h:1824-1883 quantize_fp_u8_colblock, the kblock u8s8 GEMM
+   (bestla_wrapper.h:768-831 + bestla_gemm.h:2899-3050) over a blob with a reduce section, and kernel_ref.h:2371-2429
+   gemv_4bit_u8s8_fp32 over unpacked operands */
+void orc_quant_u8_colblock(int row, int col, const float* src, int ld_src, uint8_t* dst, int ld_dst, float* scales,
+                           int ld_scale, uint8_t* zps, int blocksize, float* blkreduce);
+int orc_blob_forward_int8(const float* A, const void* blob, float* C, int m, int n, int k, int lda, int ldc);
+void orc_gemv_u8s8_ref(int m, int n, int k, int bs, const uint8_t* a8, const float* as, const uint8_t* azp,
+                       const int8_t* q, const float* s, const int8_t* zp, float* C);
+
 #ifdef __cplusplus
 }
 #endif

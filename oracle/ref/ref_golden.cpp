@@ -213,6 +213,69 @@ static void case_convert(const char* cs) {
   dump(cs, "fp16_back", "f4", fh_back.data(), fh_back.size());
 }
 
+// kernel_ref.h:1824-1883 quantize_fp_u8_colblock (int8-compute activation quantizer)
+static void case_quant_u8(const char* cs, int row, int col, int bs, float amp) {
+  std::vector<float> src((size_t)row * col);
+  for (auto& v : src) v = urand(-amp, amp);
+  if (col >= 3 * bs) {  // row 0: an all-zero block, an all-positive block, an all-negative block
+    for (int j = 0; j < bs; j++) src[j] = 0.f;
+    for (int j = bs; j < 2 * bs; j++) src[j] = urand(0.1f, amp);
+    for (int j = 2 * bs; j < 3 * bs; j++) src[j] = urand(-amp, -0.1f);
+  }
+  int nblk = (col + bs - 1) / bs;
+  std::vector<uint8_t> q((size_t)row * col), zp((size_t)row * nblk);
+  std::vector<float> s((size_t)row * nblk), red((size_t)row * nblk);
+  kernel::ref::quantize_fp_u8_colblock<float>(row, col, src.data(), col, q.data(), col, s.data(), nblk, zp.data(), bs,
+                                              red.data());
+  int meta[3] = {row, col, bs};
+  dump(cs, "meta", "i4", meta, 3);
+  dump(cs, "src", "f4", src.data(), src.size());
+  dump(cs, "q", "u1", q.data(), q.size());
+  dump(cs, "s", "f4", s.data(), s.size());
+  dump(cs, "zp", "u1", zp.data(), zp.size());
+  dump(cs, "red", "f4", red.data(), red.size());
+}
+
+// kernel_ref.h:2371-2429 gemv_4bit_u8s8_fp32 on a PACK_ROW 4 stripe, activation quantized by quantize_fp_u8_colblock
+template <int NTILE, int MTILE>
+static void case_gemv_u8s8(const char* cs, int k, int bs, bool asym) {
+  int nblk = k / bs;
+  std::vector<int8_t> q((size_t)k * NTILE), zp((size_t)nblk * NTILE), qp((size_t)k * NTILE);
+  for (auto& v : q) v = (int8_t)((int)(rnd() % 16u) - 8);
+  for (auto& v : zp) v = (int8_t)((int)(rnd() % 16u) - 8);
+  for (int kk = 0; kk < k; kk++)  // [k/4][NTILE][4]
+    for (int n = 0; n < NTILE; n++) qp[(size_t)(kk / 4) * NTILE * 4 + n * 4 + kk % 4] = q[(size_t)kk * NTILE + n];
+  std::vector<float> s((size_t)nblk * NTILE), A((size_t)MTILE * k), C((size_t)MTILE * NTILE);
+  for (auto& v : s) v = urand(0.001f, 0.05f);
+  for (auto& v : A) v = urand(-0.5f, 0.5f);
+  std::vector<uint8_t> a8((size_t)MTILE * k), azp((size_t)MTILE * nblk);
+  std::vector<float> as((size_t)MTILE * nblk);
+  kernel::ref::quantize_fp_u8_colblock<float>(MTILE, k, A.data(), k, a8.data(), k, as.data(), nblk, azp.data(), bs,
+                                              nullptr);
+  std::vector<uint8_t> packed((size_t)k * NTILE / 2);
+  kernel::ref::compress_s8_s4(qp.data(), reinterpret_cast<utils::int4x2*>(packed.data()), qp.size());
+  utils::GemvParamA PA{a8.data(), as.data(), azp.data(), k, nblk};
+  utils::GemvParamB<float> B;
+  B.b4ptr = packed.data();
+  B.sptr = s.data();
+  B.zpptr = asym ? zp.data() : nullptr;
+  B.nbits = 4;
+  B.ldzp = NTILE;
+  B.kpad = k;
+  std::vector<int8_t> tmp(16384);
+  kernel::ref::gemv_4bit_u8s8_fp32<float, NTILE, MTILE>(PA, B, C.data(), NTILE, k, bs, tmp.data(), tmp.size());
+  int meta[6] = {4, k, bs, NTILE, MTILE, asym ? 1 : 0};
+  dump(cs, "meta", "i4", meta, 6);
+  dump(cs, "A", "f4", A.data(), A.size());
+  dump(cs, "a8", "u1", a8.data(), a8.size());
+  dump(cs, "as", "f4", as.data(), as.size());
+  dump(cs, "azp", "u1", azp.data(), azp.size());
+  dump(cs, "q", "i1", q.data(), q.size());
+  dump(cs, "scale", "f4", s.data(), s.size());
+  if (asym) dump(cs, "zp", "i1", zp.data(), zp.size());
+  dump(cs, "C", "f4", C.data(), C.size());
+}
+
 int main(int argc, char** argv) {
   if (argc < 2) {
     fprintf(stderr, "usage: %s <outdir>\n", argv[0]);
@@ -246,6 +309,12 @@ int main(int argc, char** argv) {
   case_gemv<48, 2>("gemv_s2_m2_sym", 2, 512, 64, false);
   case_gemv<48, 1>("gemv_s2_m1_asym", 2, 256, 64, true);
   case_convert("convert");
+  case_quant_u8("qu8_g32", 7, 256, 32, 0.5f);
+  case_quant_u8("qu8_g128_tail", 5, 300, 128, 3.0f);
+  case_quant_u8("qu8_perchannel", 4, 200, 4096, 1.0f);
+  case_quant_u8("qu8_g64_big", 3, 512, 64, 1000.f);
+  case_gemv_u8s8<48, 1>("gemv_u8s8_m1_sym", 512, 128, false);
+  case_gemv_u8s8<48, 4>("gemv_u8s8_m4_asym", 512, 32, true);
   fclose(g_man);
   return 0;
 }

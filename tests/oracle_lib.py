@@ -71,6 +71,9 @@ class Oracle:
         L.orc_core_ktile.argtypes = [C.c_uint64]
         L.orc_core_ntile.argtypes = [C.c_uint64]
         L.orc_core_packrow.argtypes = [C.c_uint64]
+        L.orc_quant_u8_colblock.argtypes = [C.c_int, C.c_int, _p, C.c_int, _p, C.c_int, _p, C.c_int, _p, C.c_int, _p]
+        L.orc_blob_forward_int8.argtypes = [_p, _p, _p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int]
+        L.orc_gemv_u8s8_ref.argtypes = [C.c_int] * 4 + [_p] * 7
 
     # ---- helpers
     def core(self, name):
@@ -145,6 +148,27 @@ class Oracle:
         m = A.shape[0]
         C_ = np.zeros((m, n), np.float32)
         assert self.lib.orc_blob_forward(_ptr(A), _ptr(blob), _ptr(C_), m, n, k, A.shape[1], n) == 0
+        return C_
+
+    def quant_u8(self, A, blocksize, want_reduce=False):
+        """kernel_ref.h:1824-1883: -> (u8 codes [m][k], scales [m][nblk], zero points [m][nblk], block reduce)"""
+        A = np.ascontiguousarray(A, dtype=np.float32)
+        m, k = A.shape
+        nblk = -(-k // blocksize)
+        q = np.zeros((m, k), np.uint8)
+        s = np.zeros((m, nblk), np.float32)
+        z = np.zeros((m, nblk), np.uint8)
+        red = np.zeros((m, nblk), np.float32) if want_reduce else None
+        self.lib.orc_quant_u8_colblock(m, k, _ptr(A), k, _ptr(q), k, _ptr(s), nblk, _ptr(z), blocksize, _ptr(red))
+        return q, s, z, red
+
+    def forward_int8(self, A, blob, n, k):
+        """int8-compute forward (kblock u8s8 core) of a blob packed for an integer core"""
+        A = np.ascontiguousarray(A, dtype=np.float32)
+        m = A.shape[0]
+        C_ = np.zeros((m, n), np.float32)
+        r = self.lib.orc_blob_forward_int8(_ptr(A), _ptr(blob), _ptr(C_), m, n, k, A.shape[1], n)
+        assert r == 0, r
         return C_
 
     def gemv_ref(self, A, blob, n):

@@ -14,7 +14,7 @@ import numpy as np
 import pytest
 
 from tests.conftest import gpu_available
-from tests.oracle_lib import BF16, F16, F32, S2, S4
+from tests.oracle_lib import BF16, F16, F32, S2, S4, S8
 from tests.test_gpu_parity import _blob, _rel_err
 
 pytestmark = pytest.mark.gpu
@@ -131,7 +131,7 @@ def test_gemm_fused_qkv_and_ffn(oracle, m):
 
 
 GEMM4_CASES = [
-    # m, n, k, bs, qtype, stype, asym, comp  -- gemm4 (woq_gemm4.hip): int4 g32 / g64, int2 groups >= 64
+    # m, n, k, bs, qtype, stype, asym, comp  -- gemm4 (woq_gemm4.hip): int4 g32 / g64, int2 groups >= 64, int8
     (64, 128, 512, 32, S4, F16, False, 4),        # int4 g32 (the reference Python default group)
     (257, 300, 640, 32, S4, BF16, False, 4),      # ragged M / N, 5 K tiles
     (96, 130, 300, 64, S4, F16, False, 4),        # int4 g64, K tail (zero padded)
@@ -141,6 +141,14 @@ GEMM4_CASES = [
     (64, 160, 1024, 128, S2, BF16, False, 4),     # int2 g128
     (100, 64, 2048, 256, S2, F16, True, 4),       # int2 g256 asym (one group per tile)
     (48, 80, 1024, 1024, S2, F32, False, 1),      # int2 per-channel
+    (128, 200, 640, 32, S4, F16, True, 4),        # int4 g32 asym (compact zero-point slots)
+    (64, 128, 512, 32, S8, F16, False, 4),        # int8 g32: one tile per half step, tile two half steps ahead
+    (257, 300, 640, 32, S8, BF16, True, 4),       # int8 g32 asym, ragged M / N
+    (96, 130, 300, 128, S8, F32, False, 1),       # int8 g128, K tail
+    (200, 96, 1024, 256, S8, F16, True, 4),       # int8 g256 asym (four tiles a group)
+    (48, 80, 512, 512, S8, BF16, False, 1),       # int8 per-channel
+    (33, 64, 64, 64, S8, F16, True, 4),           # int8, a single half step
+    (40, 48, 128, 64, S8, F16, False, 4),         # int8, two half steps
 ]
 
 

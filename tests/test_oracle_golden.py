@@ -117,7 +117,7 @@ def test_dequant_s2_chain(oracle, case):
     np.testing.assert_array_equal(_unpack_packrow(g["s8"], row, nt, pr), s8)
 
 
-@pytest.mark.parametrize("case", _cases("gemv_"))
+@pytest.mark.parametrize("case", [c for c in _cases("gemv_") if not c.startswith("gemv_u8s8")])
 def test_gemv_ref_matches_reference(oracle, case):
     """The oracle's stripe GEMV (used for the cpu_baseline) reproduces kernel_ref.h's gemv_{4,2}bit_fp32_fp32."""
     g = G[case]
