@@ -197,6 +197,15 @@ int nad_get_compute_mode(void);
  * act_dtype, q [m][ldq] u8, scales / zps [m][ld_scale] per block, blkreduce (may be NULL) = sum(round(x/s)) * s. */
 int nad_quant_u8_colblock(const void* act, int act_dtype, int m, int k, int lda, int blocksize, uint8_t* q, int ldq,
                           float* scales, uint8_t* zps, int ld_scale, float* blkreduce, void* queue);
+/* ===== GGUF Q4_0 (neural_speed/core/data_types.h:79-83): a Q4_0 matrix of N rows x K (K % 32 == 0), rows of K/32
+ * blocks {fp16 d; u8 qs[16]} as an ne_tensor of type NE_TYPE_Q4_0 holds them, loaded into the same device layout as a
+ * BTLA blob (symmetric int4, group 32, fp16 scales); every nad_device_* / bestla_device_* forward then accepts the
+ * descriptor.  Compute mode 1 reproduces the reference's Q8_0 x Q4_0 arithmetic (quantize_row_q8_0_reference,
+ * ne_vec_dot_q4_0_q8_0). */
+size_t nad_q4_0_device_size(int n, int k);
+int nad_q4_0_device_load(const void* blocks, int n, int k, void* devstor, void* deviceptr, size_t capacity, void* queue);
+/* quantize_row_q8_0 (vectors/cpu/quantize.h:422-445) on device pointers: act [m][lda] -> m rows of K/32 block_q8_0 */
+int nad_quant_q8_0(const void* act, int act_dtype, int m, int k, int lda, void* blocks, void* queue);
 /* host convenience: (re)pack one blob into fp32 dequantized [K][N] from the device tile layout (round-trip check) */
 int nad_device_unpack_fp32(const void* devstor, float* host_out, void* queue);
 

@@ -78,6 +78,9 @@ SIGNATURES = {
     "nad_set_compute_mode": (_i, [_i]),
     "nad_get_compute_mode": (_i, []),
     "nad_quant_u8_colblock": (_i, [_p, _i, _i, _i, _i, _i, _p, _i, _p, _p, _i, _p, _p]),
+    "nad_q4_0_device_size": (_sz, [_i, _i]),
+    "nad_q4_0_device_load": (_i, [_p, _i, _i, _p, _p, _sz, _p]),
+    "nad_quant_q8_0": (_i, [_p, _i, _i, _i, _i, _p, _p]),
     "nad_chain_create": (_p, [_p, _i, _i]),
     "nad_chain_run": (_i, [_p, _p]),
     "nad_chain_status": (_i, [_p]),

@@ -207,6 +207,22 @@ class DeviceWeight:
                                      _stream(stream)), "nad_synthetic_weight")
         return cls(_desc=desc, _mem=mem)
 
+    @classmethod
+    def from_q4_0(cls, blocks, n, k, device=None, stream=None):
+        """A GGUF Q4_0 matrix (n rows of k/32 block_q4_0, as an NE_TYPE_Q4_0 ne_tensor holds it) in the device tile
+        layout (nad_q4_0_device_load)."""
+        torch = _torch()
+        L = lib()
+        blocks = np.ascontiguousarray(blocks, dtype=np.uint8)
+        assert blocks.size == n * (k // 32) * 18, (blocks.size, n, k)
+        need = L.nad_q4_0_device_size(n, k)
+        if not need:
+            raise RuntimeError(last_error())
+        mem = torch.empty(need, dtype=torch.uint8, device=device or "cuda")
+        desc = (C.c_uint8 * L.bestla_device_storage_size())()
+        check(L.nad_q4_0_device_load(_ptr(blocks), n, k, desc, _ptr(mem), need, _stream(stream)), "nad_q4_0_device_load")
+        return cls(_desc=desc, _mem=mem)
+
     def forward(self, x, out=None, epilogue=EPI_NONE, bias=None, residual=None, stream=None):
         """out[m][n] = epi(sum_k x[m][k] * W[n][k]); x: cuda [M][K] fp32/fp16/bf16 (row stride honoured)."""
         torch = _torch()
@@ -259,6 +275,15 @@ def quant_u8_colblock(x, blocksize, stream=None):
     check(lib().nad_quant_u8_colblock(_ptr(x), _act_code(x), m, k, x.stride(0), blocksize, _ptr(q), k, _ptr(s),
                                       _ptr(z), nblk, _ptr(red), _stream(stream)), "nad_quant_u8_colblock")
     return q, s, z, red
+
+
+def quant_q8_0(x, stream=None):
+    """quantize_row_q8_0 (vectors/cpu/quantize.h:422-445) on the GPU: x cuda [M][K] -> uint8 [M][K/32 * 34] blocks"""
+    torch = _torch()
+    m, k = x.shape
+    out = torch.empty((m, k // 32 * 34), dtype=torch.uint8, device=x.device)
+    check(lib().nad_quant_q8_0(_ptr(x), _act_code(x), m, k, x.stride(0), _ptr(out), _stream(stream)), "nad_quant_q8_0")
+    return out
 
 
 def f32f32_forward(activation, weight, output, m, n, k, lda, ldo, stream=None):

@@ -503,7 +503,12 @@ static int compute_mode() {
   if (g_compute_mode < 0) g_compute_mode = env_int("NAD_COMPUTE_INT8", 0) ? 1 : 0;
   return g_compute_mode;
 }
-static bool int8_compute(const DeviceWeight& w) { return compute_mode() == 1 && w.reduce != nullptr; }
+// a GGUF Q4_0 matrix (nad_q4_0_device_load) carries this in src_core_id: its int8 arithmetic is Q8_0 x Q4_0
+constexpr uint64_t kGgufQ4_0 = 0x3054344655474700ull;  // "\0GGUF4Q0"
+static bool is_q4_0(const DeviceWeight& w) { return w.src_core_id == kGgufQ4_0; }
+static bool int8_compute(const DeviceWeight& w) {
+  return compute_mode() == 1 && (w.reduce != nullptr || is_q4_0(w));
+}
 
 extern "C" int nad_set_compute_mode(int mode) {
   if (mode != 0 && mode != 1) {
@@ -528,6 +533,26 @@ static size_t i8_act_bytes(int m, const DeviceWeight& w) {
 static int i8_quantize(I8Act& r, char* ws, const void* act, int act_t, int lda, int m, int k, const DeviceWeight& w,
                        hipStream_t st) {
   const int kp = w.nt * tile_k(w.bits);
+  if (is_q4_0(w)) {  // Q8_0 rows (quantize_row_q8_0_reference)
+    Q80Args q{};
+    q.A = act;
+    q.lda = lda;
+    q.M = m;
+    q.K = k;
+    q.aq = reinterpret_cast<int8_t*>(ws);
+    q.ldq = kp;
+    q.kp = kp;
+    q.sa = reinterpret_cast<float2*>(ws + align256(size_t(m) * kp));
+    hipError_t e = launch_q8_0_quant(q, act_t, st);
+    if (e != hipSuccess) {
+      set_err("Q8_0 activation quantization launch failed: %s", hipGetErrorString(e));
+      return -1;
+    }
+    r.aq = q.aq;
+    r.ldq = kp;
+    r.sa = q.sa;
+    return 0;
+  }
   QuantU8Args q{};
   q.A = act;
   q.lda = lda;
@@ -557,6 +582,7 @@ static int i8_gemm(const I8Act& x, int m, int k, const DeviceWeight& w, float* o
   I8Args a{};
   a.aq = x.aq;
   a.ldq = x.ldq;
+  a.a_signed = is_q4_0(w) ? 1 : 0;
   a.sa = x.sa;
   a.M = m;
   a.K = k;
@@ -583,8 +609,8 @@ static int run_i8(const void* act, int act_t, int lda, int m, int k, int nw, con
                   float* const* outs, const int* ldos, bool dual, int epi, const float* bias, int bias_ld,
                   const float* res, int ld_res, const float* aux, int ld_aux, hipStream_t st) {
   for (int i = 0; i < nw; i++)
-    if (!int8_compute(*ws[i])) {
-      set_err("int8 compute: every weight of a fused call needs an integer-core blob (with reduce)");
+    if (!int8_compute(*ws[i]) || is_q4_0(*ws[i]) != is_q4_0(*ws[0])) {
+      set_err("int8 compute: the weights of a fused call must all be integer-core blobs (with reduce) or all Q4_0");
       return -1;
     }
   const size_t abytes = i8_act_bytes(m, *ws[0]);
@@ -631,6 +657,67 @@ extern "C" int nad_quant_u8_colblock(const void* act, int act_dtype, int m, int 
   hipError_t e = launch_quant_u8(a, act_dtype, static_cast<hipStream_t>(queue));
   if (e != hipSuccess) {
     set_err("activation quantization launch failed: %s", hipGetErrorString(e));
+    return -1;
+  }
+  return 0;
+}
+
+// ------------------------------------------------------------------------------------------------ GGUF Q4_0
+extern "C" size_t nad_q4_0_device_size(int n, int k) {
+  if (n <= 0 || k <= 0 || k % 32) {
+    set_err("Q4_0 needs n > 0 and k a positive multiple of 32 (n=%d k=%d)", n, k);
+    return 0;
+  }
+  DeviceWeight w{};
+  return layout_geometry(w, 4, n, k, 32, kScaleF16, false, false);
+}
+
+extern "C" int nad_q4_0_device_load(const void* blocks, int n, int k, void* devstor, void* deviceptr, size_t capacity,
+                                    void* queue) {
+  const size_t need = nad_q4_0_device_size(n, k);
+  if (!need) return -1;
+  if (!blocks || !devstor || !deviceptr || capacity < need) {
+    set_err("nad_q4_0_device_load: null pointer or device buffer too small (need %zu, have %zu)", need, capacity);
+    return -1;
+  }
+  hipStream_t st = static_cast<hipStream_t>(queue);
+  DeviceWeight w{};
+  layout_geometry(w, 4, n, k, 32, kScaleF16, false, false);
+  layout_assign(w, deviceptr);
+  w.src_core_id = kGgufQ4_0;
+  w.owner = nullptr;
+  // padding columns / K tiles: nibble 8 = q 0, scale 0
+  HIP_OK(hipMemsetAsync(w.tiles, 0x88, size_t(w.ns) * w.nt * 1024, st));
+  HIP_OK(hipMemsetAsync(w.scales, 0, size_t(w.ns) * w.ng * 16 * 2, st));
+  const size_t bytes = size_t(n) * (k / 32) * 18;
+  uint8_t* stage = nullptr;
+  HIP_OK(hipMalloc(&stage, bytes));
+  HIP_OK(hipMemcpyAsync(stage, blocks, bytes, hipMemcpyHostToDevice, st));
+  hipError_t e = launch_q4_0_repack(stage, n, k, w, st);
+  HIP_OK(hipStreamSynchronize(st));
+  HIP_OK(hipFree(stage));
+  if (e != hipSuccess) {
+    set_err("Q4_0 repack launch failed: %s", hipGetErrorString(e));
+    return -1;
+  }
+  std::memcpy(devstor, &w, sizeof(w));
+  return 0;
+}
+
+extern "C" int nad_quant_q8_0(const void* act, int act_dtype, int m, int k, int lda, void* blocks, void* queue) {
+  if (m <= 0 || k <= 0 || k % 32 || lda < k || !blocks) {
+    set_err("nad_quant_q8_0: bad arguments (m=%d k=%d lda=%d)", m, k, lda);
+    return -1;
+  }
+  Q80Args a{};
+  a.A = act;
+  a.lda = lda;
+  a.M = m;
+  a.K = k;
+  a.blocks = static_cast<int8_t*>(blocks);
+  hipError_t e = launch_q8_0_quant(a, act_dtype, static_cast<hipStream_t>(queue));
+  if (e != hipSuccess) {
+    set_err("Q8_0 quantization launch failed: %s", hipGetErrorString(e));
     return -1;
   }
   return 0;

@@ -184,17 +184,28 @@ __global__ __launch_bounds__(256) void woq_i8_kernel(I8Args a) {
       sbt += __shfl_xor(sbt, 16);
       sbt += __shfl_xor(sbt, 32);
       const float sB = load_scale(W.scales, scale_row(W.kmajor, W.ns, W.ng, sc, g) * 16 + nl, a.scale_t);
-      const float redB = bf16_bits_to_f32(a.red[size_t(g) * a.red_ld + n]);
+      const float redB = a.red ? bf16_bits_to_f32(a.red[size_t(g) * a.red_ld + n]) : 0.f;
+      if (a.a_signed) {  // Q8_0 x Q4_0: sumf += sumi * d_w * d_a (vec_dot.h:201)
 #pragma unroll
-      for (int rt = 0; rt < RT; rt++)
+        for (int rt = 0; rt < RT; rt++)
 #pragma unroll
-        for (int r = 0; r < 4; r++) {
-          const int row = min(m0 + rt * 16 + kq * 4 + r, a.M - 1);
-          const float2 sz = a.sa[size_t(row) * W.ng + g];
-          const int dot = acc[rt][r] + 128 * sbt;
-          c[rt][r] = c[rt][r] + float(dot) * (sz.x * sB);
-          c[rt][r] = c[rt][r] - sz.y * redB;
-        }
+          for (int r = 0; r < 4; r++) {
+            const int row = min(m0 + rt * 16 + kq * 4 + r, a.M - 1);
+            const float2 sz = a.sa[size_t(row) * W.ng + g];
+            c[rt][r] = c[rt][r] + (float(acc[rt][r]) * sB) * sz.x;
+          }
+      } else {
+#pragma unroll
+        for (int rt = 0; rt < RT; rt++)
+#pragma unroll
+          for (int r = 0; r < 4; r++) {
+            const int row = min(m0 + rt * 16 + kq * 4 + r, a.M - 1);
+            const float2 sz = a.sa[size_t(row) * W.ng + g];
+            const int dot = acc[rt][r] + 128 * sbt;
+            c[rt][r] = c[rt][r] + float(dot) * (sz.x * sB);
+            c[rt][r] = c[rt][r] - sz.y * redB;
+          }
+      }
 #pragma unroll
       for (int rt = 0; rt < RT; rt++) acc[rt] = i4_t{0, 0, 0, 0};
       sb = 0;

@@ -133,6 +133,7 @@ struct QuantU8Args {
 struct I8Args {
   const int8_t* aq;
   int ldq;
+  int a_signed;         // 1: Q8_0 activations (s8, sa = {d, 0}; C += float(s32) * d_w * d_a); 0: u8 kblock mode
   const float2* sa;     // [M][ng]
   int M, K;
   const uint16_t* red;  // bf16 reduce [ng][red_ld]
@@ -145,6 +146,17 @@ struct I8Args {
   int ld_aux;
   SkinnyWeight w;
 };
+// GGUF Q4_0 weights / Q8_0 activations (woq_gguf.hip)
+struct Q80Args {
+  const void* A;
+  int lda, M, K;        // K % 32 == 0
+  int8_t* aq;           // [M][ldq] s8 codes, zero in [K, kp)
+  int ldq, kp;
+  float2* sa;           // [M][K/32] {float(fp16 d), 0}
+  int8_t* blocks;       // optional raw block_q8_0 rows [M][K/32][34]
+};
+hipError_t launch_q4_0_repack(const uint8_t* src, int n, int k, const DeviceWeight& w, hipStream_t stream);
+hipError_t launch_q8_0_quant(const Q80Args& a, int act_t, hipStream_t stream);
 hipError_t launch_quant_u8(const QuantU8Args& a, int act_t, hipStream_t stream);
 hipError_t launch_i8(const I8Args& a, int bits, hipStream_t stream);
 hipError_t launch_gemm4(const GemmArgs& a, int bits, const _Float16* A16, int lda16, hipStream_t stream);

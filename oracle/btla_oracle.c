@@ -904,3 +904,129 @@ void orc_gemv_u8s8_ref(int m, int n, int k, int bs, const uint8_t* a8, const flo
       C[(size_t)im * n + in] = acc;
     }
 }
+
+/* ------------------------------------------------------------------ GGUF Q4_0 x Q8_0 */
+/* block layouts (neural_speed/core/data_types.h:79-83 and the Q8_0 block beside it): q4_0 = {fp16 d; u8 qs[16]} (18 B,
+   element j < 16 in the low nibble of qs[j], element j >= 16 in the high nibble of qs[j - 16]); q8_0 = {fp16 d;
+   s8 qs[32]} (34 B). */
+static inline uint32_t f2b(float f) {
+  uint32_t u;
+  memcpy(&u, &f, 4);
+  return u;
+}
+static inline float b2f(uint32_t u) {
+  float f;
+  memcpy(&f, &u, 4);
+  return f;
+}
+/* data_types.h:204-228 ne_compute_fp32_to_fp16 */
+uint16_t orc_ne_fp32_to_fp16(float f) {
+  const float scale_to_inf = 0x1.0p+112f, scale_to_zero = 0x1.0p-110f;
+  float base = (fabsf(f) * scale_to_inf) * scale_to_zero;
+  const uint32_t w = f2b(f), shl1_w = w + w, sign = w & 0x80000000u;
+  uint32_t bias = shl1_w & 0xFF000000u;
+  if (bias < 0x71000000u) bias = 0x71000000u;
+  base = b2f((bias >> 1) + 0x07800000u) + base;
+  const uint32_t bits = f2b(base);
+  const uint32_t exp_bits = (bits >> 13) & 0x00007C00u, mantissa_bits = bits & 0x00000FFFu;
+  const uint32_t nonsign = exp_bits + mantissa_bits;
+  return (uint16_t)((sign >> 16) | (shl1_w > 0xFF000000u ? 0x7E00u : nonsign));
+}
+/* data_types.h ne_compute_fp16_to_fp32 (exact) */
+float orc_ne_fp16_to_fp32(uint16_t h) { return orc_fp16_to_f32(h); }
+
+/* vectors/cpu/quantize.h:243-276 quantize_row_q4_0_reference */
+void orc_q4_0_quantize_row(const float* x, uint8_t* y, int k) {
+  const int qk = 32, nb = k / qk;
+  for (int i = 0; i < nb; i++) {
+    float amax = 0.0f, max = 0.0f;
+    for (int j = 0; j < qk; j++) {
+      const float v = x[i * qk + j];
+      if (amax < fabsf(v)) {
+        amax = fabsf(v);
+        max = v;
+      }
+    }
+    const float d = max / -8;
+    const float id = d ? 1.0f / d : 0.0f;
+    uint8_t* blk = y + (size_t)i * 18;
+    uint16_t dh = orc_ne_fp32_to_fp16(d);
+    memcpy(blk, &dh, 2);
+    for (int j = 0; j < qk / 2; ++j) {
+      const float x0 = x[i * qk + 0 + j] * id;
+      const float x1 = x[i * qk + qk / 2 + j] * id;
+      int8_t t0 = (int8_t)(x0 + 8.5f), t1 = (int8_t)(x1 + 8.5f);
+      const uint8_t xi0 = (uint8_t)(15 < t0 ? 15 : t0);
+      const uint8_t xi1 = (uint8_t)(15 < t1 ? 15 : t1);
+      blk[2 + j] = (uint8_t)(xi0 | (xi1 << 4));
+    }
+  }
+}
+
+/* vectors/cpu/quantize.h:686-704 dequantize_row_q4_0 */
+void orc_q4_0_dequantize_row(const uint8_t* x, float* y, int k) {
+  const int qk = 32, nb = k / qk;
+  for (int i = 0; i < nb; i++) {
+    uint16_t dh;
+    memcpy(&dh, x + (size_t)i * 18, 2);
+    const float d = orc_ne_fp16_to_fp32(dh);
+    const uint8_t* qs = x + (size_t)i * 18 + 2;
+    for (int j = 0; j < qk / 2; ++j) {
+      const int x0 = (qs[j] & 0x0F) - 8, x1 = (qs[j] >> 4) - 8;
+      y[i * qk + j + 0] = x0 * d;
+      y[i * qk + j + qk / 2] = x1 * d;
+    }
+  }
+}
+
+/* vectors/cpu/quantize.h:422-445 quantize_row_q8_0_reference */
+void orc_q8_0_quantize_row(const float* x, uint8_t* y, int k) {
+  const int nb = k / 32;
+  for (int i = 0; i < nb; i++) {
+    float amax = 0.0f;
+    for (int j = 0; j < 32; j++) {
+      const float v = fabsf(x[i * 32 + j]);
+      amax = amax > v ? amax : v;
+    }
+    const float d = amax / ((1 << 7) - 1);
+    const float id = d ? 1.0f / d : 0.0f;
+    uint8_t* blk = y + (size_t)i * 34;
+    uint16_t dh = orc_ne_fp32_to_fp16(d);
+    memcpy(blk, &dh, 2);
+    for (int j = 0; j < 32; ++j) ((int8_t*)blk)[2 + j] = (int8_t)roundf(x[i * 32 + j] * id);
+  }
+}
+
+/* neural_speed/core/layers/vec_dot.h:187-204 ne_vec_dot_q4_0_q8_0, scalar path */
+float orc_vec_dot_q4_0_q8_0(int n, const uint8_t* vx, const uint8_t* vy) {
+  const int qk = 32, nb = n / qk;
+  float sumf = 0.0f;
+  for (int i = 0; i < nb; i++) {
+    const uint8_t* xb = vx + (size_t)i * 18;
+    const uint8_t* yb = vy + (size_t)i * 34;
+    const int8_t* yq = (const int8_t*)(yb + 2);
+    int sumi = 0;
+    for (int j = 0; j < qk / 2; ++j) {
+      const int v0 = (xb[2 + j] & 0x0F) - 8, v1 = (xb[2 + j] >> 4) - 8;
+      sumi += (v0 * yq[j]) + (v1 * yq[j + qk / 2]);
+    }
+    uint16_t dx, dy;
+    memcpy(&dx, xb, 2);
+    memcpy(&dy, yb, 2);
+    sumf += sumi * orc_ne_fp16_to_fp32(dx) * orc_ne_fp16_to_fp32(dy);
+  }
+  return sumf;
+}
+
+/* ne_compute_forward_mul_mat for a Q4_0 src0 (ne_layers.c: src1 rows quantized by vec_dot_type = Q8_0, then one
+   vec_dot per output): W = [n][k/32] q4_0 blocks, A [m][k] f32 -> C [m][n] */
+int orc_q4_0_forward(const float* A, const uint8_t* W, float* C, int m, int n, int k) {
+  if (k % 32) return -1;
+  uint8_t* q8 = (uint8_t*)malloc((size_t)(k / 32) * 34);
+  for (int i = 0; i < m; i++) {
+    orc_q8_0_quantize_row(A + (size_t)i * k, q8, k);
+    for (int j = 0; j < n; j++) C[(size_t)i * n + j] = orc_vec_dot_q4_0_q8_0(k, W + (size_t)j * (k / 32) * 18, q8);
+  }
+  free(q8);
+  return 0;
+}

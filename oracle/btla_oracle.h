@@ -107,6 +107,17 @@ int orc_blob_forward_int8(const float* A, const void* blob, float* C, int m, int
 void orc_gemv_u8s8_ref(int m, int n, int k, int bs, const uint8_t* a8, const float* as, const uint8_t* azp,
                        const int8_t* q, const float* s, const int8_t* zp, float* C);
 
+
+/* GGUF Q4_0 x Q8_0: data_types.h:79-83 blocks, data_types.h:204-228 fp32->fp16, vectors/cpu/quantize.h:243-276 / 422-445 /
+   686-704, core/layers/vec_dot.h:187-204 (scalar path) */
+uint16_t orc_ne_fp32_to_fp16(float f);
+float orc_ne_fp16_to_fp32(uint16_t h);
+void orc_q4_0_quantize_row(const float* x, uint8_t* y, int k);
+void orc_q4_0_dequantize_row(const uint8_t* x, float* y, int k);
+void orc_q8_0_quantize_row(const float* x, uint8_t* y, int k);
+float orc_vec_dot_q4_0_q8_0(int n, const uint8_t* vx, const uint8_t* vy);
+int orc_q4_0_forward(const float* A, const uint8_t* W, float* C, int m, int n, int k);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,7 +1,9 @@
 """Regenerate the committed golden fixtures under tests/golden/ (run in the build container only).
 
 Two sources, both the reference itself:
-  1. tests/golden/ref/   -- outputs of oracle/_ref/ref_golden, a driver compiled by oracle/ref/Makefile directly
+  1. tests/golden/gguf/  -- outputs of oracle/_ref/gguf_golden, compiled from the reference's GGUF Q4_0 / Q8_0 code
+                            (neural_speed/vectors/cpu/quantize.h, core/layers/vec_dot.h; scalar paths).
+     tests/golden/ref/   -- outputs of oracle/_ref/ref_golden, a driver compiled by oracle/ref/Makefile directly
                             against /root/reference/bestla/bestla/kernel_ref.h (quantizer, interleave, compress,
                             kblock decompress, scalar GEMV, bf16/fp16 conversions).
   2. tests/golden/gptq/  -- outputs of the reference's GPTQ/AWQ unpack functions
@@ -30,6 +32,11 @@ def make_ref():
     for f in os.listdir(out):
         os.remove(os.path.join(out, f))
     subprocess.check_call([os.path.join(REPO, "oracle", "_ref", "ref_golden"), out])
+    gg = os.path.join(HERE, "gguf")
+    os.makedirs(gg, exist_ok=True)
+    for f in os.listdir(gg):
+        os.remove(os.path.join(gg, f))
+    subprocess.check_call([os.path.join(REPO, "oracle", "_ref", "gguf_golden"), gg])
 
 
 def make_gptq():

@@ -74,6 +74,12 @@ class Oracle:
         L.orc_quant_u8_colblock.argtypes = [C.c_int, C.c_int, _p, C.c_int, _p, C.c_int, _p, C.c_int, _p, C.c_int, _p]
         L.orc_blob_forward_int8.argtypes = [_p, _p, _p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int]
         L.orc_gemv_u8s8_ref.argtypes = [C.c_int] * 4 + [_p] * 7
+        L.orc_q4_0_quantize_row.argtypes = [_p, _p, C.c_int]
+        L.orc_q4_0_dequantize_row.argtypes = [_p, _p, C.c_int]
+        L.orc_q8_0_quantize_row.argtypes = [_p, _p, C.c_int]
+        L.orc_vec_dot_q4_0_q8_0.argtypes = [C.c_int, _p, _p]
+        L.orc_vec_dot_q4_0_q8_0.restype = C.c_float
+        L.orc_q4_0_forward.argtypes = [_p, _p, _p, C.c_int, C.c_int, C.c_int]
 
     # ---- helpers
     def core(self, name):
@@ -171,6 +177,30 @@ class Oracle:
         assert r == 0, r
         return C_
 
+    def q4_0_quantize(self, W):
+        """[n][k] f32 -> [n][k/32] block_q4_0 bytes (vectors/cpu/quantize.h:243-276)"""
+        W = np.ascontiguousarray(W, dtype=np.float32)
+        n, k = W.shape
+        out = np.zeros((n, k // 32 * 18), np.uint8)
+        for r in range(n):
+            self.lib.orc_q4_0_quantize_row(_ptr(W[r]), _ptr(out[r]), k)
+        return out
+
+    def q4_0_forward(self, A, W_q4, n, k):
+        """the reference's Q4_0 mul_mat: Q8_0 activations, integer block dots (vec_dot.h scalar order)"""
+        A = np.ascontiguousarray(A, dtype=np.float32)
+        m = A.shape[0]
+        C_ = np.zeros((m, n), np.float32)
+        assert self.lib.orc_q4_0_forward(_ptr(A), _ptr(np.ascontiguousarray(W_q4)), _ptr(C_), m, n, k) == 0
+        return C_
+
+    def q4_0_dequant(self, W_q4, n, k):
+        out = np.zeros((n, k), np.float32)
+        W_q4 = np.ascontiguousarray(W_q4)
+        for r in range(n):
+            self.lib.orc_q4_0_dequantize_row(_ptr(W_q4[r]), _ptr(out[r]), k)
+        return out
+
     def gemv_ref(self, A, blob, n):
         A = np.ascontiguousarray(A, dtype=np.float32)
         m = A.shape[0]
@@ -180,9 +210,9 @@ class Oracle:
         return C_
 
 
-def load_ref_golden():
-    """tests/golden/ref/manifest.txt -> {case: {name: array}}"""
-    d = os.path.join(GOLDEN, "ref")
+def load_ref_golden(sub="ref"):
+    """tests/golden/<sub>/manifest.txt -> {case: {name: array}}"""
+    d = os.path.join(GOLDEN, sub)
     out = {}
     with open(os.path.join(d, "manifest.txt")) as f:
         for line in f:
