@@ -31,7 +31,7 @@ import torch  # noqa: E402
 
 from neural_amd import _lib, bestla  # noqa: E402
 
-G = 128
+G = int(os.environ.get("SWEEP_GROUP", "128"))  # quantization group of the synthetic weights
 SHAPES = {  # name: (n, k, weights per launch)
     "qkv": (4096, 4096, 3), "o": (4096, 4096, 1), "gate_up": (11008, 4096, 2), "down": (4096, 11008, 1),
     "lm_head": (32000, 4096, 1)}
