@@ -789,6 +789,7 @@ static int run_gemm(const void* act, int act_t, int lda, int m, int k, const Dev
   a.aux = aux;
   a.ld_aux = ld_aux;
   a.prio = env_int("NAD_GEMM3_PRIO", 0);
+  a.stagger = env_int("NAD_GEMM3_STAGGER", 1);  // measured +3-7 % (profiles/r02_gemm3_stagger.txt)
   a.w = view(w, out, ldo, bias, bias_ld);
   const int pg = pipelined_gemm(w, m);
   if (pg) {

@@ -463,8 +463,33 @@ __global__ __launch_bounds__(512, 1) void woq_gemm3_kernel(GemmArgs a, const _Fl
     return st == kScaleF32 ? __uint_as_float(x) : f16or;
   };
 
-  auto half = [&](auto Hc, int u) {
+  // hand-over: batch(u - 2) (the buffers half step u + 1 reads) has landed for this wave; batches u - 1 and u
+  // (8 A pieces + one B batch, whatever the order inside a batch) stay in flight across the barrier
+  auto hand_over = [&](auto Hc, int u) {
+    constexpr int H = decltype(Hc)::value;
+    if constexpr (H == 0) {
+      if (u + 3 < nh)
+        wait_vm<8 + NBW>();
+      else
+        wait_vm<0>();
+    } else {
+      if (u + 3 < nh)
+        wait_vm<8 + NBW>();
+      else if (u + 3 == nh)
+        wait_vm<4>();
+      else
+        wait_vm<0>();
+    }
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+
+  // L (late, waves 4-7 when staggered): the barrier of half step u comes after its first 32-deep step, so these waves'
+  // second-step MFMAs and group scaling run half a block behind waves 0-3 (MI355X_MICROARCH item 9).  Everything they
+  // read from LDS for half step u (A fragments, B words, scales) is in registers before that barrier.
+  auto half = [&](auto Hc, auto Lc, int u) {
     constexpr int H = decltype(Hc)::value;  // which 64 of the B tile's 128
+    constexpr bool L = decltype(Lc)::value;
     const int t = u >> 1;
     const char* ab = smem + (u & 3) * HBUF;
     const char* bb = smem + NA * HBUF + (t % NBR) * BBUF;
@@ -488,9 +513,20 @@ __global__ __launch_bounds__(512, 1) void woq_gemm3_kernel(GemmArgs a, const _Fl
     }
     const bool gstart = H == 0 && (TPG1 || (t & (tpg - 1)) == 0);
     const bool gend = H == 1 && (TPG1 || ((t + 1) & (tpg - 1)) == 0 || t == nt - 1);
+    uint32_t sw0 = 0, sw1 = 0;
 #pragma unroll
     for (int dd = 0; dd < 2; dd++) {
-      if (dd == 1) wait_lgk<0>(af1[0], af1[1], af1[2], af1[3], af1[4], af1[5], af1[6], af1[7]);
+      if (dd == 1) {
+        wait_lgk<0>(af1[0], af1[1], af1[2], af1[3], af1[4], af1[5], af1[6], af1[7]);
+        if constexpr (L) {
+          if (gend) {
+            sw0 = lds_b32<0>(bl + soff);
+            sw1 = lds_b32<64>(bl + soff);
+            wait_lgk<0>(sw0, sw1);
+          }
+          hand_over(Hc, u);
+        }
+      }
       h8_t bf[2];
 #pragma unroll
       for (int j = 0; j < 2; j++) {
@@ -514,37 +550,31 @@ __global__ __launch_bounds__(512, 1) void woq_gemm3_kernel(GemmArgs a, const _Fl
       }
     }
     if (gend) {
-      uint32_t sw0 = lds_b32<0>(bl + soff), sw1 = lds_b32<64>(bl + soff);
-      wait_lgk<0>(sw0, sw1);
+      if constexpr (!L) {
+        sw0 = lds_b32<0>(bl + soff);
+        sw1 = lds_b32<64>(bl + soff);
+        wait_lgk<0>(sw0, sw1);
+      }
       const float sf[2] = {scale_f32(sw0), scale_f32(sw1)};
 #pragma unroll
       for (int j = 0; j < 2; j++)
 #pragma unroll
         for (int i = 0; i < 8; i++) acc[i][j] += accg[i][j] * sf[j];
     }
-    // hand-over: batch(u - 2) (the buffers half step u + 1 reads) has landed for this wave; batches u - 1 and u
-    // (8 A pieces + one B batch, whatever the order inside a batch) stay in flight across the barrier
-    if constexpr (H == 0) {
-      if (u + 3 < nh)
-        wait_vm<8 + NBW>();
-      else
-        wait_vm<0>();
-    } else {
-      if (u + 3 < nh)
-        wait_vm<8 + NBW>();
-      else if (u + 3 == nh)
-        wait_vm<4>();
-      else
-        wait_vm<0>();
-    }
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
+    if constexpr (!L) hand_over(Hc, u);
   };
 
   if (a.prio && wave >= 4) __builtin_amdgcn_s_setprio(1);  // static priority for the younger half (wave-uniform)
-  for (int u = 0; u < nh; u += 2) {
-    half(std::integral_constant<int, 0>{}, u);
-    half(std::integral_constant<int, 1>{}, u + 1);
+  if (a.stagger && wave >= 4) {
+    for (int u = 0; u < nh; u += 2) {
+      half(std::integral_constant<int, 0>{}, std::true_type{}, u);
+      half(std::integral_constant<int, 1>{}, std::true_type{}, u + 1);
+    }
+  } else {
+    for (int u = 0; u < nh; u += 2) {
+      half(std::integral_constant<int, 0>{}, std::false_type{}, u);
+      half(std::integral_constant<int, 1>{}, std::false_type{}, u + 1);
+    }
   }
 
   // epilogue through LDS (free after the loop: the last barrier retired every read and DMA): each wave transposes its

@@ -329,8 +329,34 @@ __global__ __launch_bounds__(512, 1) void woq_gemm4_kernel(GemmArgs a, const _Fl
     return st == kScaleF32 ? __uint_as_float(x) : f16or;
   };
 
-  auto half = [&](auto Hc, int u) {
+  auto hand_over = [&](auto Hc, int u) {
+    constexpr int H = decltype(Hc)::value;
+    // hand-over: batch u - 2 has landed; batches u - 1 and u stay in flight
+    if constexpr (B2) {  // tile u + 1 (head of batch u - 1) and A(u + 1) landed; A(u + 2) and batch u in flight
+      if (u + 3 < nh)
+        wait_vm<8 + NBW>();
+      else if (u + 2 < nh)
+        wait_vm<4 + NBW>();
+      else
+        wait_vm<0>();
+    } else {
+      constexpr int bu = 4 + (((H + 3) % HPT) == 0 ? NBW : 0);   // |batch u| (when issued)
+      constexpr int bu1 = 4 + (((H + 2) % HPT) == 0 ? NBW : 0);  // |batch u - 1|
+      if (u + 3 < nh)
+        wait_vm<bu + bu1>();
+      else if (u + 2 < nh)
+        wait_vm<bu1>();
+      else
+        wait_vm<0>();
+    }
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+
+  // L (late, waves 4-7): the barrier of half step u comes after its first 32-deep step (see woq_gemm3_kernel)
+  auto half = [&](auto Hc, auto Lc, int u) {
     constexpr int H = decltype(Hc)::value;  // phase of half step u in its tile
+    constexpr bool L = decltype(Lc)::value;
     const int t = u / HPT;
     const char* ab = smem + (u & 3) * HBUF;
     const char* bb = smem + NA * HBUF + (t % NBR) * BBUF;
@@ -384,9 +410,20 @@ __global__ __launch_bounds__(512, 1) void woq_gemm4_kernel(GemmArgs a, const _Fl
                 sg[1][0], sg[1][1], af0[0], af0[1], af0[2], af0[3], af0[4], af0[5], af0[6], af0[7]);
     const bool gstart = G32 || (u & (gh - 1)) == 0;
     const bool gend = G32 || ((u + 1) & (gh - 1)) == 0 || u == nh - 1;
+    uint32_t sw0 = 0, sw1 = 0;
 #pragma unroll
     for (int dd = 0; dd < 2; dd++) {
-      if (dd == 1) wait_lgk<0>(af1[0], af1[1], af1[2], af1[3], af1[4], af1[5], af1[6], af1[7]);
+      if (dd == 1) {
+        wait_lgk<0>(af1[0], af1[1], af1[2], af1[3], af1[4], af1[5], af1[6], af1[7]);
+        if constexpr (L) {
+          if (!G32 && gend) {
+            sw0 = lds_b32v(bl + soff + slot * 512);
+            sw1 = lds_b32v(bl + soff + slot * 512 + 64);
+            wait_lgk<0>(sw0, sw1);
+          }
+          hand_over(Hc, u);
+        }
+      }
       const int zi = G32 ? dd : 0;
       h8_t bf[2];
 #pragma unroll
@@ -431,9 +468,12 @@ __global__ __launch_bounds__(512, 1) void woq_gemm4_kernel(GemmArgs a, const _Fl
         }
       }
       if (dd == 1 && gend) {  // group end: scale the group partials into the result
-        const uint32_t sa = bl + soff + slot * 512;
-        uint32_t sw0 = lds_b32v(sa), sw1 = lds_b32v(sa + 64);
-        wait_lgk<0>(sw0, sw1);
+        if constexpr (!L) {
+          const uint32_t sa = bl + soff + slot * 512;
+          sw0 = lds_b32v(sa);
+          sw1 = lds_b32v(sa + 64);
+          wait_lgk<0>(sw0, sw1);
+        }
         const float sf[2] = {scale_f32(sw0), scale_f32(sw1)};
 #pragma unroll
         for (int j = 0; j < 2; j++)
@@ -444,36 +484,23 @@ __global__ __launch_bounds__(512, 1) void woq_gemm4_kernel(GemmArgs a, const _Fl
           }
       }
     }
-    // hand-over: batch u - 2 has landed; batches u - 1 and u stay in flight
-    if constexpr (B2) {  // tile u + 1 (head of batch u - 1) and A(u + 1) landed; A(u + 2) and batch u in flight
-      if (u + 3 < nh)
-        wait_vm<8 + NBW>();
-      else if (u + 2 < nh)
-        wait_vm<4 + NBW>();
-      else
-        wait_vm<0>();
-    } else {
-      constexpr int bu = 4 + (((H + 3) % HPT) == 0 ? NBW : 0);   // |batch u| (when issued)
-      constexpr int bu1 = 4 + (((H + 2) % HPT) == 0 ? NBW : 0);  // |batch u - 1|
-      if (u + 3 < nh)
-        wait_vm<bu + bu1>();
-      else if (u + 2 < nh)
-        wait_vm<bu1>();
-      else
-        wait_vm<0>();
-    }
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
+    if constexpr (!L) hand_over(Hc, u);
   };
 
-  for (int u = 0; u < nh; u += HPT) {
-    half(std::integral_constant<int, 0>{}, u);
-    if constexpr (HPT >= 2) half(std::integral_constant<int, 1>{}, u + 1);
-    if constexpr (HPT == 4) {
-      half(std::integral_constant<int, 2>{}, u + 2);
-      half(std::integral_constant<int, 3>{}, u + 3);
+  auto loop = [&](auto Lc) {
+    for (int u = 0; u < nh; u += HPT) {
+      half(std::integral_constant<int, 0>{}, Lc, u);
+      if constexpr (HPT >= 2) half(std::integral_constant<int, 1>{}, Lc, u + 1);
+      if constexpr (HPT == 4) {
+        half(std::integral_constant<int, 2>{}, Lc, u + 2);
+        half(std::integral_constant<int, 3>{}, Lc, u + 3);
+      }
     }
-  }
+  };
+  if (a.stagger && wave >= 4)
+    loop(std::true_type{});
+  else
+    loop(std::false_type{});
 
   // epilogue through LDS (as gemm3)
   float* tw = reinterpret_cast<float*>(smem) + wave * (128 * 36);
@@ -557,11 +584,13 @@ hipError_t launch_gemm4(const GemmArgs& a, int bits, const _Float16* A16, int ld
   const int gh_log2 = g32 ? 0 : mode - 1;
   const int nbm = (a.M + g4::BM - 1) / g4::BM, nbn = (a.w.ns + 7) / 8;
   const bool asym = a.w.zps != nullptr;
+  GemmArgs ga = a;
+  if (bits == 2) ga.stagger = 0;  // measured neutral to -5 % for int2 (profiles/r02_gemm4_stagger.txt), +4-14 % else
   auto go = [&](auto k, int lds) -> hipError_t {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
                                        lds);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k, dim3(nbm * nbn), dim3(512), lds, st, a, A16, lda16, gh_log2);
+    hipLaunchKernelGGL(k, dim3(nbm * nbn), dim3(512), lds, st, ga, A16, lda16, gh_log2);
     return hipGetLastError();
   };
 #define NAD_G4(B, G, A) go(g4::woq_gemm4_kernel<B, G, A>, g4::lds_bytes<B, G, A>())

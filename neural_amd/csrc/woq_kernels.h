@@ -66,6 +66,7 @@ struct GemmArgs {
   const float* aux;
   int ld_aux;
   int prio;             // gemm3: waves 4-7 at s_setprio 1 for the whole loop (NAD_GEMM3_PRIO)
+  int stagger;          // gemm3: waves 4-7 half a step behind waves 0-3 (NAD_GEMM3_STAGGER)
   SkinnyWeight w;
 };
 

@@ -44,7 +44,8 @@ def main():
                     os.environ["NAD_GEMM_KERNEL"] = kern[0]
                     os.environ["NAD_GEMM2_DISABLE"] = "1" if kern[0] == "0" else "0"
                     os.environ["NAD_GEMM4_DISABLE"] = "1" if kern[0] != "4" else "0"
-                    os.environ["NAD_GEMM3_PRIO"] = "1" if kern.endswith("p") else "0"
+                    os.environ["NAD_GEMM3_PRIO"] = "1" if "p" in kern[1:] else "0"
+                    os.environ["NAD_GEMM3_STAGGER"] = "1" if "s" in kern[1:] else "0"
                     for _ in range(3):
                         w.forward(x, out=out)
                     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
