@@ -255,7 +255,8 @@ bool Blob::parse(const void* buf, std::string* err) {
   if (r.get<uint8_t>() != 0) return fail("double-quantized (DQ8_BNB) scales are not supported");
   has_shuffle = r.get<uint8_t>() != 0;
   if (has_shuffle) shf_off = get_aligned(r, base, &shf_size);
-  if (qtype != kS4 && qtype != kS2 && qtype != kS8) return fail("weight dtype must be S4_CLIP, S2_CLIP or S8");
+  if (!dtype_is_int(qtype) || dtype_bits(qtype) < 2 || dtype_bits(qtype) > 8)
+    return fail("weight dtype must be an integer type S2_CLIP .. S8 (S1 and the float/NF4 types are not supported)");
   if (scale_t != kF32 && scale_t != kBF16 && scale_t != kF16) return fail("scale dtype must be F32, BF16 or F16");
   CoreInfo ci = core_info(core_id);
   if (ci.ntile <= 0 || (ci.packrow != 1 && ci.packrow != 2 && ci.packrow != 4)) return fail("unknown core id");
@@ -395,7 +396,7 @@ bool pack_quantized(Blob& b, int8_t* base, const int8_t* Q, int ldq, const float
                     const int* g_idx, std::string* err) {
   const CoreInfo ci = core_info(b.core_id);
   const int bits = dtype_bits(b.qtype);
-  if (bits != 4 && bits != 2 && bits != 8) {
+  if (bits < 2 || bits > 8) {
     if (err) *err = "unsupported weight bits";
     return false;
   }
@@ -426,6 +427,33 @@ bool pack_quantized(Blob& b, int8_t* base, const int8_t* Q, int ldq, const float
   // reorderWeight + compressWeight: walk the interleaved order directly, packing as we go
   uint8_t* qp = reinterpret_cast<uint8_t*>(base + b.q_off);
   const int ntile = ci.ntile, pr = ci.packrow, kpad = b.kpad;
+  if (bits == 3 || bits == 5 || bits == 6 || bits == 7) {  // bit planes (compressBitNWeight, bestla_prologue_b.h:512-546)
+    const size_t nel = size_t(b.npad) * kpad;
+    std::memset(qp, 0, b.q_size);
+    const bool has4 = bits >= 5, has2 = bits == 3 || bits >= 6, has1 = bits == 3 || bits == 5 || bits == 7;
+    const size_t o2 = has4 ? nel / 2 : 0, o1 = o2 + (has2 ? nel / 4 : 0);
+    // one task per group of 8 elements so no two tasks write the same byte of any plane
+    parallel_for(int(nel / 8 / 64 + 1), [&](int task) {
+      for (size_t e8 = size_t(task) * 64; e8 < std::min(nel / 8, size_t(task + 1) * 64); e8++)
+        for (size_t e = e8 * 8; e < e8 * 8 + 8; e++) {
+          const size_t st = e / (size_t(ntile) * kpad), el = e % (size_t(ntile) * kpad);
+          const int kk = int(el / (size_t(ntile) * pr)) * pr + int(el % pr);
+          const int nn = int(st) * ntile + int((el / pr) % ntile);
+          const int8_t v = (kk < b.k && nn < b.n) ? Q[size_t(kk) * ldq + nn] : 0;
+          uint32_t u = uint32_t(v + (1 << (bits - 1)));
+          int sh = 0;
+          if (has4) {
+            qp[e / 2] |= uint8_t((u & 15u) << (4 * (e & 1)));
+            sh = 4;
+          }
+          if (has2) {
+            qp[o2 + e / 4] |= uint8_t(((u >> sh) & 3u) << (2 * (e & 3)));
+            sh += 2;
+          }
+          if (has1) qp[o1 + e / 8] |= uint8_t(((u >> sh) & 1u) << (e & 7));
+        }
+    });
+  } else {
   const int per_byte = 8 / bits;
   const int8_t bias = int8_t(bits == 8 ? 0 : (1 << (bits - 1)));
   const size_t stripe_elems = size_t(ntile) * kpad;
@@ -447,6 +475,7 @@ bool pack_quantized(Blob& b, int8_t* base, const int8_t* Q, int ldq, const float
       if (bits != 8) qp[(e0 + e) / per_byte] = byte;
     }
   });
+  }
   (void)ilv_index;
   if (b.has_reduce) {  // reduceWeight (bestla_prologue_b.h:455-470): sequential float sum per (block, n) -> bf16
     uint16_t* rp = reinterpret_cast<uint16_t*>(base + b.r_off);
@@ -468,6 +497,23 @@ static inline int8_t read_q(const Blob& b, const uint8_t* qp, const CoreInfo& ci
   size_t e = ilv_index(kk, nn, b.kpad, ci.ntile, ci.packrow);
   int bits = dtype_bits(b.qtype);
   if (bits == 8) return int8_t(qp[e]);
+  if (bits == 3 || bits == 5 || bits == 6 || bits == 7) {
+    const size_t nel = size_t(b.npad) * b.kpad;
+    const bool has4 = bits >= 5, has2 = bits == 3 || bits >= 6, has1 = bits == 3 || bits == 5 || bits == 7;
+    const size_t o2 = has4 ? nel / 2 : 0, o1 = o2 + (has2 ? nel / 4 : 0);
+    uint32_t u = 0;
+    int sh = 0;
+    if (has4) {
+      u = (qp[e / 2] >> (4 * (e & 1))) & 15u;
+      sh = 4;
+    }
+    if (has2) {
+      u |= ((qp[o2 + e / 4] >> (2 * (e & 3))) & 3u) << sh;
+      sh += 2;
+    }
+    if (has1) u |= ((qp[o1 + e / 8] >> (e & 7)) & 1u) << sh;
+    return int8_t(int(u) - (1 << (bits - 1)));
+  }
   int per = 8 / bits;
   int v = (qp[e / per] >> (bits * (e % per))) & ((1 << bits) - 1);
   return int8_t(v - (1 << (bits - 1)));

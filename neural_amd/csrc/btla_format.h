@@ -20,9 +20,18 @@ enum : uint32_t {
   kS8 = 8 | 0x100,
   kS4 = 4 | 0x100,
   kS2 = 2 | 0x100,
+  kS3 = 3 | 0x100,
+  kS5 = 5 | 0x100,
+  kS6 = 6 | 0x100,
+  kS7 = 7 | 0x100,
   kDQ8_BNB = 8 | (4u << 16),
 };
 inline int dtype_bits(uint32_t t) { return int(t & 0xff); }
+// bits of the device tile layout that holds a blob's integers exactly: S2 -> 2, S3/S4 -> 4, S5..S8 -> 8
+inline int device_bits(uint32_t t) {
+  const int b = dtype_bits(t);
+  return b <= 2 ? 2 : (b <= 4 ? 4 : 8);
+}
 inline bool dtype_is_int(uint32_t t) { return ((t >> 8) & 0xff) == 1; }
 
 // ne_comp_type (neural_speed/core/data_types.h:57-63)

@@ -123,7 +123,7 @@ extern "C" size_t nad_device_weight_size(const void* hostblob) {
   }
   DeviceWeight w{};
   int bs = b.blocksize >= b.k ? b.kpad : b.blocksize;
-  return layout_geometry(w, dtype_bits(b.qtype), b.n, b.k, bs, scale_code(b.scale_t), b.asym, b.has_shuffle, 0,
+  return layout_geometry(w, device_bits(b.qtype), b.n, b.k, bs, scale_code(b.scale_t), b.asym, b.has_shuffle, 0,
                          b.has_reduce);
 }
 
@@ -143,7 +143,7 @@ extern "C" int nad_device_load(const void* hostblob, void* devstor, void* device
   // per-channel (group >= K) is one group covering all tiles
   const int bs = b.blocksize >= b.k ? b.kpad : b.blocksize;
   const char* km = getenv("NAD_TILE_KMAJOR");  // layout A/B switch (development); default K-major
-  const uint64_t need = layout_geometry(w, dtype_bits(b.qtype), b.n, b.k, bs, scale_code(b.scale_t), b.asym,
+  const uint64_t need = layout_geometry(w, device_bits(b.qtype), b.n, b.k, bs, scale_code(b.scale_t), b.asym,
                                         b.has_shuffle, (km && *km) ? atoi(km) : 0, b.has_reduce);
   if (need > capacity) {
     set_err("device buffer too small for the tile layout: need %llu bytes, have %zu (see nad_device_weight_size)",
@@ -180,6 +180,8 @@ extern "C" int nad_device_load(const void* hostblob, void* devstor, void* device
   ra.packrow = ci.packrow;
   ra.kpad = b.kpad;
   ra.cstep = b.cstep;
+  ra.src_bits = dtype_bits(b.qtype);
+  ra.nel = uint64_t(b.npad) * b.kpad;
   ra.bits = w.bits;
   ra.n = w.n;
   ra.k = w.k;

@@ -17,7 +17,9 @@ struct RepackArgs {
   const void* src_s;
   const int8_t* src_z;
   int ntile, packrow, kpad, cstep;
-  // destination geometry
+  int src_bits;         // blob element bits: 2, 3, 4, 5, 6, 7, 8 (3/5/6/7 in bit planes, bestla_prologue_b.h:512-546)
+  uint64_t nel;         // NPad * KPad: plane size of the multi-plane formats
+  // destination geometry (bits: the device layout's 2 / 4 / 8 -- S3 lands in the int4 layout, S5-S7 in int8)
   int bits, n, k, ns, nt, ng, scale_t, kmajor;
   uint32_t* dst_tiles;
   void* dst_scales;

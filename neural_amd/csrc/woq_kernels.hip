@@ -1,6 +1,6 @@
 // woq_kernels.hip -- hand-written CDNA4 (gfx950) kernels for the weight-only-quantized matmul hot path.
 //
-//   nad_repack_kernel   : BTLA blob (any core layout, NTILE 24/48, PACK_ROW 1/2/4; S4/S2/S8) -> tile layout
+//   nad_repack_kernel   : BTLA blob (any core layout, NTILE 24/48, PACK_ROW 1/2/4; S2-S8) -> tile layout
 //                         (woq_layout.h).  Replaces convertTransStorage + fromHost of the SYCL backend
 //                         (bestla/bestla/bestla_prologue_b.h:129-150, neural_speed/core/layers/ne_bestla_sycl.cpp:94-144).
 //   woq_skinny_kernel   : M <= 16 ("GEMV", decode).  Replaces GEMVWrapper::gemv_kblock -> gemv_{4,2}bit_fp32_fp32
@@ -28,6 +28,40 @@ namespace nad {
 
 
 // ------------------------------------------------------------------------------------------------ repack
+// signed integer q of blob element e (interleaved order).  S2/S4: crumb / nibble = q + 2^(b-1); S8: the byte;
+// S3/S5/S6/S7: u = q + 2^(b-1) split over a nibble plane [nel/2], a crumb plane [nel/4] and a bit plane [nel/8]
+// (3 = crumb|bit, 5 = nibble|bit, 6 = nibble|crumb, 7 = nibble|crumb|bit; kernel_ref.h:178-341).
+__device__ __forceinline__ int blob_q(const RepackArgs& a, uint64_t e) {
+  const uint8_t* q = a.src_q;
+  switch (a.src_bits) {
+    case 8:
+      return int(int8_t(q[e]));
+    case 4:
+      return int((q[e >> 1] >> (4 * (e & 1))) & 0xF) - 8;
+    case 2:
+      return int((q[e >> 2] >> (2 * (e & 3))) & 0x3) - 2;
+    default:
+      break;
+  }
+  const int b = a.src_bits;
+  const bool has4 = b >= 5, has2 = b == 3 || b >= 6, has1 = b == 3 || b == 5 || b == 7;
+  uint64_t off = 0;
+  uint32_t u = 0;
+  int sh = 0;
+  if (has4) {
+    u = (q[e >> 1] >> (4 * (e & 1))) & 0xF;
+    sh = 4;
+    off = a.nel / 2;
+  }
+  if (has2) {
+    u |= ((q[off + (e >> 2)] >> (2 * (e & 3))) & 0x3u) << sh;
+    sh += 2;
+    off += a.nel / 4;
+  }
+  if (has1) u |= ((q[off + (e >> 3)] >> (e & 7)) & 0x1u) << sh;
+  return int(u) - (1 << (b - 1));
+}
+
 // One thread per output dword of the tile layout.
 __global__ void nad_repack_kernel(RepackArgs a) {
   const uint64_t total = uint64_t(a.ns) * a.nt * 256;
@@ -60,13 +94,7 @@ __global__ void nad_repack_kernel(RepackArgs a) {
       if (n < a.n && k < a.k) {
         const uint64_t e = uint64_t(n / a.ntile) * a.ntile * a.kpad + uint64_t(k / a.packrow) * a.ntile * a.packrow +
                            uint64_t(n % a.ntile) * a.packrow + uint64_t(k % a.packrow);
-        if (a.bits == 4) {
-          v = (a.src_q[e >> 1] >> (4 * (e & 1))) & 0xF;  // stored nibble = q + 8
-        } else if (a.bits == 2) {
-          v = (a.src_q[e >> 2] >> (2 * (e & 3))) & 0x3;  // stored crumb = q + 2
-        } else {
-          v = uint32_t(uint8_t(a.src_q[e]) ^ 0x80u);     // S8 stores q; device stores q + 128
-        }
+        v = uint32_t(blob_q(a, e) + (a.bits == 4 ? 8 : (a.bits == 2 ? 2 : 128)));  // device: q + 2^(bits-1)
       } else {
         v = a.bits == 4 ? 8u : (a.bits == 2 ? 2u : 128u);  // q = 0 padding
       }

@@ -104,6 +104,9 @@ static inline int8_t cast_f32_s8(float v) {
 /* bestla_utils.h:522-525 cast<float,int>: int(roundf) */
 static inline int32_t cast_f32_int(float v) { return f2i_x86(roundf(v)); }
 
+int orc_compress_planes(int bits, const int8_t* src, uint8_t* dst, size_t n);
+int orc_decompress_planes(int bits, const uint8_t* src, int8_t* dst, size_t n);
+
 /* ------------------------------------------------------------------ quantizer */
 /* kernel_ref.h:1608-1719.  dispatch_calc always takes the sNauto_* lambdas for integer types. */
 void orc_quantize_rowblock(const float* srcptr, int8_t* dstptr, int row, int col, int ld_src, int ld_dst,
@@ -500,8 +503,10 @@ static void blob_dequant(const blob_t* b, const int8_t* base, float* W, int ldw,
     orc_decompress_s4(q, flat, nel);
   else if (bits == 2)
     orc_decompress_s2(q, flat, nel);
-  else
+  else if (bits == 8)
     memcpy(flat, q, nel);
+  else
+    orc_decompress_planes(bits, q, flat, nel);
   int8_t* qkn = (int8_t*)malloc((size_t)b->k * b->n);
   orc_revert_padding_interleave(flat, qkn, b->k, b->n, b->kpad, b->npad, b->kpad, b->n, nt, pr);
   const uint8_t* sp = (const uint8_t*)(base + b->s_off);
@@ -556,7 +561,7 @@ static int blob_pack_q_impl(blob_t* b, int8_t* base, const int8_t* Q, int ldb, c
     orc_compress_s2(reordered, q, nel);
   else if (bits == 8)
     memcpy(q, reordered, nel);
-  else {
+  else if (orc_compress_planes(bits, reordered, q, nel) != 0) {
     free(reordered);
     return -3;
   }
@@ -1028,5 +1033,63 @@ int orc_q4_0_forward(const float* A, const uint8_t* W, float* C, int m, int n, i
     for (int j = 0; j < n; j++) C[(size_t)i * n + j] = orc_vec_dot_q4_0_q8_0(k, W + (size_t)j * (k / 32) * 18, q8);
   }
   free(q8);
+  return 0;
+}
+
+/* ------------------------------------------------------------------ 3/5/6/7-bit planes */
+/* kernel_ref.h:178-341 compress_{7,6,5,3}bit with the plane layout of compressBitNWeight (bestla_prologue_b.h:512-546):
+   stored u = q + 2^(bits-1) split into a nibble plane (bit4x2: element 2i in the low nibble of byte i), a crumb plane
+   (bit2x4: element 4i + j at bits 2j of byte i) and a bit plane (bit1x8: element 8i + j at bit j of byte i):
+   3 = crumb [n/4] | bit [n/8];  5 = nibble [n/2] | bit [n/8];  6 = nibble [n/2] | crumb [n/4];
+   7 = nibble [n/2] | crumb [n/4] | bit [n/8]; the high part of u sits in the later plane(s). */
+static void planes(int bits, size_t n, size_t* o4, size_t* o2, size_t* o1) {
+  *o4 = *o2 = *o1 = (size_t)-1;
+  switch (bits) {
+    case 3: *o2 = 0; *o1 = n / 4; break;
+    case 5: *o4 = 0; *o1 = n / 2; break;
+    case 6: *o4 = 0; *o2 = n / 2; break;
+    case 7: *o4 = 0; *o2 = n / 2; *o1 = n / 2 + n / 4; break;
+    default: break;
+  }
+}
+int orc_compress_planes(int bits, const int8_t* src, uint8_t* dst, size_t n) {
+  size_t o4, o2, o1;
+  planes(bits, n, &o4, &o2, &o1);
+  if (o2 == (size_t)-1 && o1 == (size_t)-1) return -1;
+  memset(dst, 0, n * bits / 8);
+  for (size_t e = 0; e < n; e++) {
+    unsigned u = (unsigned)(src[e] + (1 << (bits - 1)));
+    int sh = 0;
+    if (o4 != (size_t)-1) {
+      dst[o4 + e / 2] |= (uint8_t)((u & 15u) << (4 * (e & 1)));
+      sh = 4;
+    }
+    if (o2 != (size_t)-1) {
+      dst[o2 + e / 4] |= (uint8_t)(((u >> sh) & 3u) << (2 * (e & 3)));
+      sh += 2;
+    }
+    if (o1 != (size_t)-1) dst[o1 + e / 8] |= (uint8_t)(((u >> sh) & 1u) << (e & 7));
+  }
+  return 0;
+}
+/* decompress_s{3,5,6,7}_s8 (kernel_ref.h:412-520) */
+int orc_decompress_planes(int bits, const uint8_t* src, int8_t* dst, size_t n) {
+  size_t o4, o2, o1;
+  planes(bits, n, &o4, &o2, &o1);
+  if (o2 == (size_t)-1 && o1 == (size_t)-1) return -1;
+  for (size_t e = 0; e < n; e++) {
+    unsigned u = 0;
+    int sh = 0;
+    if (o4 != (size_t)-1) {
+      u = (src[o4 + e / 2] >> (4 * (e & 1))) & 15u;
+      sh = 4;
+    }
+    if (o2 != (size_t)-1) {
+      u |= ((src[o2 + e / 4] >> (2 * (e & 3))) & 3u) << sh;
+      sh += 2;
+    }
+    if (o1 != (size_t)-1) u |= ((src[o1 + e / 8] >> (e & 7)) & 1u) << sh;
+    dst[e] = (int8_t)((int)u - (1 << (bits - 1)));
+  }
   return 0;
 }

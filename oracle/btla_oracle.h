@@ -108,6 +108,11 @@ void orc_gemv_u8s8_ref(int m, int n, int k, int bs, const uint8_t* a8, const flo
                        const int8_t* q, const float* s, const int8_t* zp, float* C);
 
 
+/* 3/5/6/7-bit plane (de)compression: kernel_ref.h:178-341 compress_Nbit, :412-520 decompress_sN_s8, plane offsets of
+   bestla_prologue_b.h:512-546 */
+int orc_compress_planes(int bits, const int8_t* src, uint8_t* dst, size_t n);
+int orc_decompress_planes(int bits, const uint8_t* src, int8_t* dst, size_t n);
+
 /* GGUF Q4_0 x Q8_0: data_types.h:79-83 blocks, data_types.h:204-228 fp32->fp16, vectors/cpu/quantize.h:243-276 / 422-445 /
    686-704, core/layers/vec_dot.h:187-204 (scalar path) */
 uint16_t orc_ne_fp32_to_fp16(float f);

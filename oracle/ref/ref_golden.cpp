@@ -276,6 +276,45 @@ static void case_gemv_u8s8(const char* cs, int k, int bs, bool asym) {
   dump(cs, "C", "f4", C.data(), C.size());
 }
 
+// kernel_ref.h:178-341 compress_{7,6,5,3}bit (plane layouts as compressBitNWeight, bestla_prologue_b.h:512-546) and
+// :448-520 decompress_s{7,6,5,3}_s8
+static void case_compress_planes(const char* cs, size_t n) {
+  std::vector<int8_t> tmp(64);
+  for (int bits : {3, 5, 6, 7}) {
+    std::vector<int8_t> src(n), dec(n);
+    const int full = 1 << (bits - 1);
+    for (auto& v : src) v = (int8_t)((int)(rnd() % (2u * full)) - full);
+    std::vector<uint8_t> packed(n * bits / 8);
+    auto* u8 = packed.data();
+    if (bits == 3) {
+      auto* b2 = reinterpret_cast<utils::bit2x4*>(u8);
+      auto* b1 = reinterpret_cast<utils::bit1x8*>(u8 + n / 4);
+      kernel::ref::compress_3bit(src.data(), b2, b1, n);
+      kernel::ref::decompress_s3_s8(b2, b1, dec.data(), n, tmp.data(), tmp.size());
+    } else if (bits == 5) {
+      auto* b4 = reinterpret_cast<utils::bit4x2*>(u8);
+      auto* b1 = reinterpret_cast<utils::bit1x8*>(u8 + n / 2);
+      kernel::ref::compress_5bit(src.data(), b4, b1, n);
+      kernel::ref::decompress_s5_s8(b4, b1, dec.data(), n, tmp.data(), tmp.size());
+    } else if (bits == 6) {
+      auto* b4 = reinterpret_cast<utils::bit4x2*>(u8);
+      auto* b2 = reinterpret_cast<utils::bit2x4*>(u8 + n / 2);
+      kernel::ref::compress_6bit(src.data(), b4, b2, n);
+      kernel::ref::decompress_s6_s8(b4, b2, dec.data(), n, tmp.data(), tmp.size());
+    } else {
+      auto* b4 = reinterpret_cast<utils::bit4x2*>(u8);
+      auto* b2 = reinterpret_cast<utils::bit2x4*>(u8 + n / 2);
+      auto* b1 = reinterpret_cast<utils::bit1x8*>(u8 + n / 2 + n / 4);
+      kernel::ref::compress_7bit(src.data(), b4, b2, b1, n);
+      kernel::ref::decompress_s7_s8(b4, b2, b1, dec.data(), n, tmp.data(), tmp.size());
+    }
+    std::string b = std::to_string(bits);
+    dump(cs, "s" + b, "i1", src.data(), n);
+    dump(cs, "c" + b, "u1", packed.data(), packed.size());
+    dump(cs, "d" + b, "i1", dec.data(), n);
+  }
+}
+
 int main(int argc, char** argv) {
   if (argc < 2) {
     fprintf(stderr, "usage: %s <outdir>\n", argv[0]);
@@ -309,6 +348,12 @@ int main(int argc, char** argv) {
   case_gemv<48, 2>("gemv_s2_m2_sym", 2, 512, 64, false);
   case_gemv<48, 1>("gemv_s2_m1_asym", 2, 256, 64, true);
   case_convert("convert");
+  case_compress_planes("compress_planes", 4096);
+  case_quant("quant_s3_sym_g32", 128, 37, 32, BTLA_DTYPE::S3_CLIP, false, 1);
+  case_quant("quant_s3_asym_g128", 256, 19, 128, BTLA_DTYPE::S3_CLIP, true, 0);
+  case_quant("quant_s5_sym_g32", 96, 13, 32, BTLA_DTYPE::S5_CLIP, false, 1);
+  case_quant("quant_s6_asym_g64", 128, 13, 64, BTLA_DTYPE::S6_CLIP, true, 0);
+  case_quant("quant_s7_sym_g128", 256, 11, 128, BTLA_DTYPE::S7_CLIP, false, 0);
   case_quant_u8("qu8_g32", 7, 256, 32, 0.5f);
   case_quant_u8("qu8_g128_tail", 5, 300, 128, 3.0f);
   case_quant_u8("qu8_perchannel", 4, 200, 4096, 1.0f);

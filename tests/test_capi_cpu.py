@@ -6,7 +6,7 @@ import numpy as np
 import pytest
 
 from neural_amd import _lib, bestla
-from tests.oracle_lib import F32, BF16, F16, S4, S2, S8
+from tests.oracle_lib import F32, BF16, F16, S2, S3, S4, S5, S6, S7, S8
 
 
 def test_library_exports_every_header_symbol():
@@ -35,6 +35,11 @@ CFGS = [
     (40, 128, 128, S8, F32, False, bestla.COMP_INT8),
     (96, 256, 32, S4, F32, False, bestla.COMP_BF16),    # amx_bf16: PACK_ROW 2, KTILE 32
     (33, 160, 32, S4, F32, False, bestla.COMP_F32),     # ragged N
+    (64, 256, 32, S3, F32, False, bestla.COMP_F32),     # 3-bit: crumb + bit planes
+    (50, 256, 128, S3, BF16, True, bestla.COMP_INT8),
+    (48, 256, 32, S5, F32, True, bestla.COMP_F32),      # 5-bit: nibble + bit planes
+    (48, 256, 64, S6, F16, False, bestla.COMP_INT8),    # 6-bit: nibble + crumb planes
+    (40, 128, 32, S7, F32, False, bestla.COMP_F32),     # 7-bit: nibble + crumb + bit planes
 ]
 
 
@@ -44,7 +49,8 @@ def test_quant_pack_bit_exact_vs_oracle(oracle, cfg):
     rng = np.random.default_rng(n * 1000 + k)
     W = rng.uniform(-0.5, 0.5, size=(n, k)).astype(np.float32)
     W[0, :bs] = 0.0  # an all-zero block
-    blob = bestla.quantize(W, group_size=bs, weight_dtype={S4: "int4", S2: "int2", S8: "int8"}[qt],
+    blob = bestla.quantize(W, group_size=bs, weight_dtype={S4: "int4", S2: "int2", S8: "int8", S3: "int3", S5: "int5", S6: "int6",
+                                                           S7: "int7"}[qt],
                            scale_dtype={F32: "fp32", BF16: "bf16", F16: "fp16"}[st],
                            alg="asym" if asym else "sym",
                            compute_dtype={bestla.COMP_F32: "fp32", bestla.COMP_INT8: "int8", bestla.COMP_BF16: "bf16"}[comp])

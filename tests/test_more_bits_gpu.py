@@ -1,0 +1,62 @@
+"""GPU parity for the 3/5/6/7-bit integer weights (quant_config.h:22-57 "int3".."int7"; planes of
+bestla_prologue_b.h:512-546).  The repack stores S3 in the int4 tile layout and S5-S7 in the int8 one (exact: the
+integers fit), so every forward kernel serves them; checked against the oracle's fp64 forward of the same blob, the
+repacked integers bit-exact, and the int8-compute mode against the oracle's kblock GEMM."""
+import numpy as np
+import pytest
+
+from tests.conftest import gpu_available
+from tests.oracle_lib import BF16, F16, F32, S3, S5, S6, S7
+from tests.test_gpu_parity import _blob, _rel_err
+
+pytestmark = pytest.mark.gpu
+
+if gpu_available():
+    import torch
+    from neural_amd import bestla
+
+CASES = [
+    # n, k, bs, qtype, stype, asym, comp
+    (256, 1024, 128, S3, F16, False, 1),
+    (200, 768, 32, S3, BF16, True, 4),
+    (96, 512, 64, S5, F32, True, 1),
+    (128, 1024, 32, S6, F16, False, 4),
+    (64, 512, 128, S7, F32, False, 1),
+    (48, 300, 1024, S3, F32, False, 1),     # per-channel, K tail
+]
+TOL = {1: 2e-5, 64: 1e-3}
+
+
+@pytest.mark.parametrize("cfg", CASES)
+def test_repack_exact(oracle, cfg):
+    n, k, bs, qt, st, asym, comp = cfg
+    blob = _blob(oracle, n, k, bs, qt, st, asym, comp, seed=n + k)
+    w = bestla.DeviceWeight(blob)
+    assert w.bits == (4 if qt == S3 else 8)
+    assert np.array_equal(w.unpack().view(np.uint32), oracle.unpack_fp32(blob).view(np.uint32))
+
+
+@pytest.mark.parametrize("m", [1, 4, 64, 300])
+@pytest.mark.parametrize("cfg", CASES)
+def test_forward_parity(oracle, cfg, m):
+    n, k, bs, qt, st, asym, comp = cfg
+    blob = _blob(oracle, n, k, bs, qt, st, asym, comp, seed=n + k)
+    w = bestla.DeviceWeight(blob)
+    A = np.random.default_rng(m + n).uniform(-0.5, 0.5, size=(m, k)).astype(np.float32)
+    y = w.forward(torch.from_numpy(A).cuda()).cpu().numpy()
+    ref = oracle.forward(A, blob, n, k)
+    assert _rel_err(y, ref) <= (TOL[1] if m <= 16 else TOL[64]), _rel_err(y, ref)
+
+
+@pytest.mark.parametrize("m", [1, 64])
+def test_int8_mode_on_int3(oracle, m):
+    n, k = 128, 1024
+    blob = _blob(oracle, n, k, 32, S3, F32, True, 4, seed=9)
+    w = bestla.DeviceWeight(blob)
+    A = np.random.default_rng(m).uniform(-1, 1, size=(m, k)).astype(np.float32)
+    prev = bestla.set_compute_mode(bestla.COMPUTE_INT8)
+    try:
+        y = w.forward(torch.from_numpy(A).cuda()).cpu().numpy()
+    finally:
+        bestla.set_compute_mode(prev)
+    assert _rel_err(y, oracle.forward_int8(A, blob, n, k)) <= 1e-5

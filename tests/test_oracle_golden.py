@@ -203,3 +203,19 @@ def test_parallel_gemv_matches_scalar(oracle):
     assert oracle.lib.orc_blob_gemv_ref(A.ctypes.data, blob.ctypes.data, c1.ctypes.data, 2, k, n) == 0
     assert oracle.lib.orc_blob_gemv_par(A.ctypes.data, blob.ctypes.data, c2.ctypes.data, 2, k, n, 4) == 0
     np.testing.assert_array_equal(c1, c2)
+
+
+def test_compress_planes_bit_exact(oracle):
+    """3/5/6/7-bit plane packing (kernel_ref.h compress_Nbit / decompress_sN_s8, plane offsets of
+    bestla_prologue_b.h:512-546) against the reference's own outputs"""
+    g = G["compress_planes"]
+    for bits in (3, 5, 6, 7):
+        src = np.ascontiguousarray(g[f"s{bits}"])
+        n = src.size
+        c = np.zeros(n * bits // 8, np.uint8)
+        assert oracle.lib.orc_compress_planes(bits, src.ctypes.data, c.ctypes.data, n) == 0
+        assert np.array_equal(c, g[f"c{bits}"]), bits
+        d = np.zeros(n, np.int8)
+        assert oracle.lib.orc_decompress_planes(bits, np.ascontiguousarray(g[f"c{bits}"]).ctypes.data,
+                                                d.ctypes.data, n) == 0
+        assert np.array_equal(d, g[f"d{bits}"]) and np.array_equal(d, src), bits
