@@ -3,6 +3,7 @@
 Follows /root/reference/neural_speed/convert/common.py:
   unpack_gptq_weight_4bits  :398-417
   unpack_gptq_weight_8bits  :353-395
+  unpack_gptq_weight_3bits  :420-446  (ten 3-bit fields per int32 at bits 0..27; the int3 re-centring of :766-770)
   unpack_awq_weight         :449-464
 and the int4 re-centring of convert_quantized_llama.py:72-76 (w - 8, zp - 8) that precedes
 np_bestla_qpack (application/main_pybind.cpp:378-402).  Pinned by tests/golden/gptq/* (outputs of the
@@ -45,6 +46,19 @@ def unpack_gptq8(qweight, qzeros, sym):
     else:
         w = _wrap_i8(_wrap_u8(w).astype(np.int64) - 128)
     return w.astype(np.int32), z
+
+
+def unpack_gptq3(qweight, qzeros, group_size, n_groups, n):
+    """qweight int32 [R, N] -> weight [group_size * n_groups, N] in 0..7 (rows past that trimmed); qzeros int32 [G, C]
+    -> zeros [G, n] in 1..8 (ten fields per int32, columns past n dropped)."""
+    qweight = np.asarray(qweight, dtype=np.int32)
+    qzeros = np.asarray(qzeros, dtype=np.int32)
+    shifts = np.arange(0, 29, 3, dtype=np.int32)                       # range(0, 32 - 3, 3): 10 fields
+    w = (qweight[:, None, :] >> shifts[None, :, None]) & 7             # [R, 10, N]
+    w = w.reshape(-1, qweight.shape[1])[:group_size * n_groups]
+    z = ((qzeros[:, :, None] >> shifts[None, None, :]) & 7) + 1        # [G, C, 10]
+    z = z.reshape(qzeros.shape[0], -1)[:, :n]
+    return w.astype(np.int32), z.astype(np.int32)
 
 
 def unpack_awq4(qweight, qzeros):

@@ -55,6 +55,7 @@ def make_gptq():
         "gptq8_g64_sym": dict(bits=8, K=128, N=16, gs=64, method="gptq", sym=True),
         "gptq8_g64_asym": dict(bits=8, K=128, N=16, gs=64, method="gptq", sym=False),
         "awq4_g64": dict(bits=4, K=128, N=64, gs=64, method="awq", sym=False),
+        "gptq3_g64": dict(bits=3, K=320, N=40, gs=64, method="gptq", sym=False),
     }
     for name, c in cases.items():
         bits, K, N, gs = c["bits"], c["K"], c["N"], c["gs"]
@@ -62,9 +63,14 @@ def make_gptq():
         G = K // gs
         if c["method"] == "awq":
             qweight = rng.integers(-2**31, 2**31, size=(K, N // pack), dtype=np.int64).astype(np.int32)
+        elif bits == 3:  # the reference reads ten 3-bit fields per int32
+            qweight = rng.integers(-2**31, 2**31, size=(K // 10, N), dtype=np.int64).astype(np.int32)
         else:
             qweight = rng.integers(-2**31, 2**31, size=(K // pack, N), dtype=np.int64).astype(np.int32)
-        qzeros = rng.integers(-2**31, 2**31, size=(G, N // pack), dtype=np.int64).astype(np.int32)
+        if bits == 3:
+            qzeros = rng.integers(-2**31, 2**31, size=(G, -(-N // 10)), dtype=np.int64).astype(np.int32)
+        else:
+            qzeros = rng.integers(-2**31, 2**31, size=(G, N // pack), dtype=np.int64).astype(np.int32)
         scales = rng.uniform(0.001, 0.005, size=(G, N)).astype(np.float16)
         qcfg = {"quant_method": c["method"], "bits": bits, "group_size": gs, "sym": c["sym"]}
         w, s, z = common.unpack_weight(torch.from_numpy(qweight), torch.from_numpy(scales),

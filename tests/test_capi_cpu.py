@@ -139,3 +139,26 @@ def test_unsupported_inputs_fail_loudly():
     assert "WeightKBlockNInteger" in _lib.last_error() or "corrupt" in _lib.last_error()
     with pytest.raises(ValueError):
         bestla.quantize(np.zeros((16, 64), np.float32), 32, "nf4")
+
+
+def test_qpack_gptq3_bit_exact(oracle):
+    """3-bit GPTQ ingest as convert/common.py:420-446,766-770 does it: unpack (ten fields per int32), re-centre by 4,
+    np_bestla_qpack(weight_dtype="int3") -- the blob equals the oracle's and unpacks to (q - zp) * s"""
+    import os
+    from oracle import gptq_oracle
+    from tests.oracle_lib import GOLDEN
+    d = os.path.join(GOLDEN, "gptq")
+    qweight = np.load(os.path.join(d, "gptq3_g64.qweight.npy"))
+    qzeros = np.load(os.path.join(d, "gptq3_g64.qzeros.npy"))
+    scales = np.load(os.path.join(d, "gptq3_g64.scales.npy")).astype(np.float32)
+    w, z = gptq_oracle.unpack_gptq3(qweight, qzeros, 64, scales.shape[0], scales.shape[1])
+    q = (w - 4).astype(np.int8)
+    zp = (z - 4).astype(np.int8)
+    k, n = q.shape
+    blob = bestla.qpack(q, scales, zp, None, weight_dtype="int3", group_size=64, alg="asym", compute_dtype="int8")
+    core = oracle.lib.orc_select_core(bestla.COMP_INT8, S3, 64, 1, 0)
+    ref = oracle.pack_q(q, scales, zp, n, k, 64, S3, F32, True, core)
+    np.testing.assert_array_equal(blob, ref)
+    W = oracle.unpack_fp32(ref)
+    expect = (q.astype(np.float32) - np.repeat(zp, 64, axis=0)) * np.repeat(scales, 64, axis=0)
+    np.testing.assert_array_equal(W, expect)

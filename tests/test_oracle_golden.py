@@ -152,6 +152,9 @@ def test_gptq_awq_unpack(case):
     qzeros = np.load(os.path.join(d, f"{case}.qzeros.npy"))
     if method == "awq":
         w, z = gptq_oracle.unpack_awq4(qweight, qzeros)
+    elif bits == "3":
+        scales = np.load(os.path.join(d, f"{case}.scales.npy"))
+        w, z = gptq_oracle.unpack_gptq3(qweight, qzeros, int(gs), scales.shape[0], scales.shape[1])
     elif bits == "4":
         w, z = gptq_oracle.unpack_gptq4(qweight, qzeros)
     else:
