@@ -171,10 +171,13 @@ Blob Blob::describe(int n, int k, int blocksize, uint32_t qtype, uint32_t scale_
   b.blocksize = blocksize <= 0 ? b.kpad : blocksize;
   b.qtype = qtype;
   b.scale_t = scale_t;
-  b.zp_t = kS8;
-  b.red_t = kBF16;
+  const bool f4 = f4_kind(qtype) >= 0;  // StorageWeightKBlockNFloat (bestla_storage.h:836-859): no zp, no reduce
+  b.prologue = f4 ? 2 : 1;
+  b.zp_t = f4 ? 0 : kS8;
+  b.red_t = f4 ? 0 : kBF16;
+  if (f4) asym = false;
   b.asym = asym;
-  b.has_reduce = ci.int_comp;
+  b.has_reduce = ci.int_comp && !f4;
   b.has_shuffle = shuffle;
   b.q_size = updiv(uint64_t(b.npad) * b.kpad * dtype_bits(qtype), 8);
   b.cstep = b.npad;
@@ -231,7 +234,8 @@ bool Blob::parse(const void* buf, std::string* err) {
   Reader r{base};
   size = r.get<uint64_t>();
   prologue = r.get<uint32_t>();
-  if (prologue != 1) return fail("only WeightKBlockNInteger blobs (integer N-bit weights) are supported");
+  if (prologue != 1 && prologue != 2)
+    return fail("only WeightKBlockNInteger / WeightKBlockNFloat blobs (N-bit integer or 4-bit float weights) are supported");
   core_id = r.get<uint64_t>();
   npad = r.get<int32_t>();
   kpad = r.get<int32_t>();
@@ -255,8 +259,11 @@ bool Blob::parse(const void* buf, std::string* err) {
   if (r.get<uint8_t>() != 0) return fail("double-quantized (DQ8_BNB) scales are not supported");
   has_shuffle = r.get<uint8_t>() != 0;
   if (has_shuffle) shf_off = get_aligned(r, base, &shf_size);
-  if (!dtype_is_int(qtype) || dtype_bits(qtype) < 2 || dtype_bits(qtype) > 8)
-    return fail("weight dtype must be an integer type S2_CLIP .. S8 (S1 and the float/NF4 types are not supported)");
+  if (prologue == 2) {
+    if (f4_kind(qtype) < 0) return fail("NFloat weight dtype must be F4_BNB, F4_E2M1 or F4_NF4 (FP8 is not supported)");
+  } else if (!dtype_is_int(qtype) || dtype_bits(qtype) < 2 || dtype_bits(qtype) > 8) {
+    return fail("weight dtype must be an integer type S2_CLIP .. S8 (S1 is not supported)");
+  }
   if (scale_t != kF32 && scale_t != kBF16 && scale_t != kF16) return fail("scale dtype must be F32, BF16 or F16");
   CoreInfo ci = core_info(core_id);
   if (ci.ntile <= 0 || (ci.packrow != 1 && ci.packrow != 2 && ci.packrow != 4)) return fail("unknown core id");
@@ -337,8 +344,23 @@ static inline float load_scale(const uint8_t* sp, size_t i, uint32_t t) {
 }
 
 // ----------------------------------------------------------------------------------------------- quantizer
-void quantize_kblock(const float* src, int K, int N, int ld_src, int bs, int bits, int8_t* q, float* scales,
+void quantize_kblock(const float* src, int K, int N, int ld_src, int bs, uint32_t qtype, int8_t* q, float* scales,
                      int8_t* zp) {
+  const int f4 = f4_kind(qtype);
+  if (f4 >= 0) {  // quantize_f32_f4_rowblock (kernel_ref.h:1800-1822): absmax from FLT_MIN, code = f4(x * (1/absmax))
+    parallel_for(N, [&](int n) {
+      for (int j = 0; j < K; j += bs) {
+        const int len = std::min(bs, K - j);
+        float absmax = std::numeric_limits<float>::min();
+        for (int t = 0; t < len; t++) absmax = std::max(absmax, std::fabs(src[size_t(j + t) * ld_src + n]));
+        scales[size_t(j / bs) * N + n] = absmax;
+        for (int t = 0; t < len; t++)
+          q[size_t(j + t) * N + n] = f4_quantize(f4, src[size_t(j + t) * ld_src + n] * (1.f / absmax));
+      }
+    });
+    return;
+  }
+  const int bits = dtype_bits(qtype);
   const int full = 1 << (bits - 1), sym = full - 1;
   auto clip = [&](int32_t s) { return s < -full ? -full : (s > sym ? sym : s); };
   const int nblk = int(updiv(size_t(K), size_t(bs)));
@@ -455,7 +477,8 @@ bool pack_quantized(Blob& b, int8_t* base, const int8_t* Q, int ldq, const float
     });
   } else {
   const int per_byte = 8 / bits;
-  const int8_t bias = int8_t(bits == 8 ? 0 : (1 << (bits - 1)));
+  // compress_f4 (kernel_ref.h:167-176) stores the codes as they are; the integer compressors store q + 2^(bits-1)
+  const int8_t bias = int8_t((bits == 8 || f4_kind(b.qtype) >= 0) ? 0 : (1 << (bits - 1)));
   const size_t stripe_elems = size_t(ntile) * kpad;
   parallel_for(b.npad / ntile, [&](int st) {
     size_t e0 = size_t(st) * stripe_elems;
@@ -516,6 +539,7 @@ static inline int8_t read_q(const Blob& b, const uint8_t* qp, const CoreInfo& ci
   }
   int per = 8 / bits;
   int v = (qp[e / per] >> (bits * (e % per))) & ((1 << bits) - 1);
+  if (f4_kind(b.qtype) >= 0) return int8_t(v);  // the F4 code
   return int8_t(v - (1 << (bits - 1)));
 }
 
@@ -545,9 +569,62 @@ void unpack_fp32(const Blob& b, const int8_t* base, float* W, int ldw) {
     for (int nn = 0; nn < b.n; nn++) {
       size_t c = size_t(g) * b.cstep + nn;
       int z = b.asym ? base[b.z_off + c] : 0;
-      W[size_t(kk) * ldw + nn] = float(read_q(b, qp, ci, kk, nn) - z) * load_scale(sp, c, b.scale_t);
+      const int f4 = f4_kind(b.qtype);
+      W[size_t(kk) * ldw + nn] = f4 >= 0 ? f4_lut(f4, read_q(b, qp, ci, kk, nn)) * load_scale(sp, c, b.scale_t)
+                                         : float(read_q(b, qp, ci, kk, nn) - z) * load_scale(sp, c, b.scale_t);
     }
   });
+}
+
+// ----------------------------------------------------------------------------------------------- NFloat 4-bit
+static const float kF4Lut[3][16] = {
+    {0.00000000f, 5.208333333e-03f, 0.66666667f, 1.00000000f, 0.33333333f, 0.50000000f, 0.16666667f, 0.25000000f,
+     -1.f * 0.00000000f, -1.f * 5.208333333e-03f, -1.f * 0.66666667f, -1.f * 1.00000000f, -1.f * 0.33333333f,
+     -1.f * 0.50000000f, -1.f * 0.16666667f, -1.f * 0.25000000f},
+    {0.f, 0.010416666666666666f, 0.16666666666666666f, 0.25f, 0.333333333333333f, 0.5f, 0.6666666666666f, 1.f,
+     -1.f * 0.f, -1.f * 0.010416666666666666f, -1.f * 0.16666666666666666f, -1.f * 0.25f, -1.f * 0.333333333333333f,
+     -1.f * 0.5f, -1.f * 0.6666666666666f, -1.f * 1.f},
+    {0.f, -0.6961928009986877f, -0.5250730514526367f, -0.39491748809814453f, -0.28444138169288635f,
+     -0.18477343022823334f, -0.09105003625154495f, -1.f, 0.07958029955625534f, 0.16093020141124725f,
+     0.24611230194568634f, 0.33791524171829224f, 0.44070982933044434f, 0.5626170039176941f, 0.7229568362236023f,
+     1.0f}};
+
+float f4_lut(int kind, int code) { return kF4Lut[kind][code & 15]; }
+
+int8_t f4_quantize(int kind, float x) {
+  if (kind == 2) {  // nf4: thresholds are the midpoints of the sorted LUT; codes of 0 and -1 swapped
+    if (x > 0.03979014977812767f) {
+      if (x > 0.3893125355243683f) {
+        if (x > 0.6427869200706482f) return x > 0.8614784181118011f ? 0xF : 0xE;
+        return x > 0.5016634166240692f ? 0xD : 0xC;
+      }
+      if (x > 0.2035212516784668f) return x > 0.2920137718319893f ? 0xB : 0xA;
+      return x > 0.1202552504837513f ? 0x9 : 0x8;
+    }
+    if (x > -0.33967943489551544f) {
+      if (x > -0.13791173323988914f) return x > -0.045525018125772476f ? 0x0 : 0x6;
+      return x > -0.23460740596055984f ? 0x5 : 0x4;
+    }
+    if (x > -0.6106329262256622f) return x > -0.4599952697753906f ? 0x3 : 0x2;
+    return x > -0.8480964004993439f ? 0x1 : 0x7;
+  }
+  const int sign = x < 0 ? 0x8 : 0;
+  x = std::fabs(x);
+  if (kind == 0) {  // fp4 bnb
+    if (x > 0.29166667f) {
+      if (x > 0.583333f) return int8_t((x > 0.8333333f ? 0x3 : 0x2) + sign);
+      return int8_t((x > 0.4166667f ? 0x5 : 0x4) + sign);
+    }
+    if (x > 0.0859375f) return int8_t((x > 0.20833333f ? 0x7 : 0x6) + sign);
+    return int8_t((x > 0.00260417f ? 0x1 : 0x0) + sign);
+  }
+  // fp4 e2m1 (the reference's normalised table: magnitudes / 6, code 1 = 1/96)
+  if (x > 1.75f / 6) {
+    if (x > 3.5f / 6) return int8_t((x > 5.f / 6 ? 0x7 : 0x6) + sign);
+    return int8_t((x > 2.5f / 6 ? 0x5 : 0x4) + sign);
+  }
+  if (x > 0.53125f / 6) return int8_t((x > 1.25f / 6 ? 0x3 : 0x2) + sign);
+  return int8_t((x > 0.03125f / 6 ? 0x1 : 0x0) + sign);
 }
 
 }  // namespace nad

@@ -24,9 +24,18 @@ enum : uint32_t {
   kS5 = 5 | 0x100,
   kS6 = 6 | 0x100,
   kS7 = 7 | 0x100,
+  kF4E2M1 = 4,                // EleBits4 | TypeFloat (bestla.h:82-84)
+  kF4BNB = 4 | (1u << 16),
+  kF4NF4 = 4 | (2u << 16),
   kDQ8_BNB = 8 | (4u << 16),
 };
 inline int dtype_bits(uint32_t t) { return int(t & 0xff); }
+// NFloat 4-bit kind (0 F4_BNB, 1 F4_E2M1, 2 F4_NF4) or -1
+inline int f4_kind(uint32_t t) { return t == kF4BNB ? 0 : (t == kF4E2M1 ? 1 : (t == kF4NF4 ? 2 : -1)); }
+// bestla_utils.h:749-790 dequant LUTs (the values of kernel_ref.h's unpack trees)
+float f4_lut(int kind, int code);
+// kernel_ref.h f4_quantize (fp4_bnb_quantize :1233-1254, fp4_e2m1_quantize :1256-1297, nf4_quantize :1373-1419)
+int8_t f4_quantize(int kind, float x);
 // bits of the device tile layout that holds a blob's integers exactly: S2 -> 2, S3/S4 -> 4, S5..S8 -> 8
 inline int device_bits(uint32_t t) {
   const int b = dtype_bits(t);
@@ -83,7 +92,7 @@ struct Blob {
 
 // quantize_f32_sign_int_rowblock (bestla/bestla/kernel_ref.h:1608-1719), multithreaded over columns.
 // src is [K][ld_src] (K rows, N columns), outputs q [K][N], scales/zp [ceil(K/bs)][N].
-void quantize_kblock(const float* src, int K, int N, int ld_src, int blocksize, int bits, int8_t* q, float* scales,
+void quantize_kblock(const float* src, int K, int N, int ld_src, int blocksize, uint32_t qtype, int8_t* q, float* scales,
                      int8_t* zp);
 
 // packQWeight (bestla_prologue_b.h:378-398) into a buffer whose header was written by Blob::write_header.

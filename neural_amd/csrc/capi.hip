@@ -154,6 +154,7 @@ extern "C" int nad_device_load(const void* hostblob, void* devstor, void* device
   w.src_core_id = b.core_id;
   w.owner = nullptr;
   w.blob_bs = b.blocksize;
+  w.f4kind = f4_kind(b.qtype);  // F4 codes go through the int4 repack unchanged (blob_q returns code - 8, + 8 back)
   // stage the raw blob buffers on the device, repack there
   const uint8_t* base = static_cast<const uint8_t*>(hostblob);
   uint8_t* stage = nullptr;
@@ -265,6 +266,7 @@ static SkinnyWeight view(const DeviceWeight& w, float* out, int ldo, const float
   v.out = out;
   v.bias = bias;
   v.bias_ld = bias_ld;
+  v.f4 = w.f4kind;
   return v;
 }
 
@@ -316,6 +318,8 @@ static int prepare_gemv(GemvArgs& a, int& waves, int& grid, int& gpt_out, const 
         ws[i]->kmajor)
       return 0;
   if (w0.kmajor) return 0;  // the stream stages each stripe's scale block: stripe-major layout only
+  for (int i = 0; i < nw; i++)
+    if (ws[i]->f4kind >= 0) return 0;  // NFloat weights: LUT dequant lives in the skinny kernel
   int tpg = 0;
   const int gpt = gemv_groups_per_tile(w0.bits, w0.nt, w0.ng, w0.blocksize, &tpg);
   if (gpt == 0 || (gpt >= 4 && w0.asym)) return 0;
@@ -736,7 +740,8 @@ struct A16 {
 
 // 3: gemm3 (int4, groups of 128 * 2^j); 4: gemm4 (int4 g32 / g64, int2 groups >= 64); 0: register-staged fallback
 static int pipelined_gemm(const DeviceWeight& w, int m) {
-  if (env_int("NAD_GEMM2_DISABLE", 0) || w.kmajor || m < 32 || uint64_t(m) * uint64_t(w.nt) * 512 >= (1ull << 32))
+  if (env_int("NAD_GEMM2_DISABLE", 0) || w.kmajor || w.f4kind >= 0 || m < 32 ||
+      uint64_t(m) * uint64_t(w.nt) * 512 >= (1ull << 32))
     return 0;
   const int tpg = w.blocksize / 128;
   if (w.bits == 4 && w.blocksize % 128 == 0 && (tpg & (tpg - 1)) == 0 && !env_int("NAD_GEMM4_ALL", 0)) return 3;
@@ -863,7 +868,8 @@ extern "C" void bestla_device_f32f32_forward(float* activation, void* weiptr, fl
 }
 
 static bool same_kind(const DeviceWeight& a, const DeviceWeight& b) {
-  return a.bits == b.bits && a.k == b.k && a.blocksize == b.blocksize && a.scale_t == b.scale_t && a.nt == b.nt &&
+  return a.bits == b.bits && a.f4kind == b.f4kind && a.k == b.k && a.blocksize == b.blocksize &&
+         a.scale_t == b.scale_t && a.nt == b.nt &&
          a.ng == b.ng && (a.shuffle == nullptr) == (b.shuffle == nullptr);
 }
 
@@ -993,7 +999,7 @@ extern "C" void* nad_chain_create(const nad_chain_op* ops, int n_ops, int m) {
         set_err("nad_chain_create: op %d runs in the int8-compute mode, which the chain does not implement", i);
         return nullptr;
       }
-    if (w0.bits != 4 || w0.has_shuffle || w0.kmajor || w0.blocksize % 128 != 0 || o.act_dtype != act_t ||
+    if (w0.bits != 4 || w0.f4kind >= 0 || w0.has_shuffle || w0.kmajor || w0.blocksize % 128 != 0 || o.act_dtype != act_t ||
         (asym >= 0 && asym != w0.asym)) {
       set_err("nad_chain_create: op %d is not a chain op (int4, group >= 128, no shuffle, one act dtype/symmetry)", i);
       return nullptr;
@@ -1165,6 +1171,18 @@ extern "C" int nad_synthetic_weight(void* devstor, void* deviceptr, size_t capac
   return 0;
 }
 
+static __constant__ float kF4LutF[3][16] = {
+    {0.00000000f, 5.208333333e-03f, 0.66666667f, 1.00000000f, 0.33333333f, 0.50000000f, 0.16666667f, 0.25000000f,
+     -1.f * 0.00000000f, -1.f * 5.208333333e-03f, -1.f * 0.66666667f, -1.f * 1.00000000f, -1.f * 0.33333333f,
+     -1.f * 0.50000000f, -1.f * 0.16666667f, -1.f * 0.25000000f},
+    {0.f, 0.010416666666666666f, 0.16666666666666666f, 0.25f, 0.333333333333333f, 0.5f, 0.6666666666666f, 1.f,
+     -1.f * 0.f, -1.f * 0.010416666666666666f, -1.f * 0.16666666666666666f, -1.f * 0.25f, -1.f * 0.333333333333333f,
+     -1.f * 0.5f, -1.f * 0.6666666666666f, -1.f * 1.f},
+    {0.f, -0.6961928009986877f, -0.5250730514526367f, -0.39491748809814453f, -0.28444138169288635f,
+     -0.18477343022823334f, -0.09105003625154495f, -1.f, 0.07958029955625534f, 0.16093020141124725f,
+     0.24611230194568634f, 0.33791524171829224f, 0.44070982933044434f, 0.5626170039176941f, 0.7229568362236023f,
+     1.0f}};
+
 // dequantize the device tile layout back to fp32 [K][N] (exactness check of the repack)
 __global__ void nad_unrepack_kernel(DeviceWeight w, float* out) {
   const int KT = tile_k(w.bits);
@@ -1199,7 +1217,7 @@ __global__ void nad_unrepack_kernel(DeviceWeight w, float* out) {
     else
       sc = float(static_cast<const _Float16*>(w.scales)[si]);
     const int zp = w.zps ? int(w.zps[si]) : 0;
-    out[i] = float(int(v) - bias - zp) * sc;
+    out[i] = w.f4kind >= 0 ? kF4LutF[w.f4kind][v & 15] * sc : float(int(v) - bias - zp) * sc;
   }
 }
 
@@ -1601,8 +1619,8 @@ extern "C" void nad_host_cache_clear(void) {
 // ------------------------------------------------------------------------------------------------ pack API
 extern "C" size_t BTLAGemmPackBSize(size_t N, size_t K, size_t BlkSize, uint32_t QuantType, uint32_t ScaleDtype,
                                     bool isAsym, int CompType, int* shuffle_indice) {
-  if (!dtype_is_int(QuantType)) {
-    set_err("float weight dtypes (fp4/nf4/fp8) are not supported by this backend");
+  if (!dtype_is_int(QuantType) && f4_kind(QuantType) < 0) {
+    set_err("float weight dtypes other than F4_BNB / F4_E2M1 / F4_NF4 (fp8) are not supported by this backend");
     return 0;
   }
   uint64_t core = select_core(CompType, QuantType, int(BlkSize), isAsym, host_isa_profile());
@@ -1614,7 +1632,7 @@ extern "C" size_t BTLAGemmPackBSize(size_t N, size_t K, size_t BlkSize, uint32_t
 extern "C" bool BTLAGemmQuantPackB(void* PackedBuf, const float* FpData, size_t N, size_t K, size_t ldb,
                                    size_t BlkSize, uint32_t QuantType, uint32_t ScaleDtype, bool isAsym, int CompType,
                                    bool isTrans, void* ThreadPool) {
-  if (!dtype_is_int(QuantType) || !PackedBuf || !FpData) return false;
+  if ((!dtype_is_int(QuantType) && f4_kind(QuantType) < 0) || !PackedBuf || !FpData) return false;
   uint64_t core = select_core(CompType, QuantType, int(BlkSize), isAsym, host_isa_profile());
   if (!core) return false;
   Blob b = Blob::describe(int(N), int(K), int(BlkSize), QuantType, ScaleDtype, isAsym, core, false);
@@ -1634,7 +1652,7 @@ extern "C" bool BTLAGemmQuantPackB(void* PackedBuf, const float* FpData, size_t 
   const int nblk = b.ngroups_k();
   std::vector<int8_t> q(K * N), z(isAsym ? size_t(nblk) * N : 0);
   std::vector<float> s(size_t(nblk) * N);
-  quantize_kblock(src, int(K), int(N), ld, b.blocksize, dtype_bits(QuantType), q.data(), s.data(),
+  quantize_kblock(src, int(K), int(N), ld, b.blocksize, uint32_t(QuantType), q.data(), s.data(),
                   isAsym ? z.data() : nullptr);
   std::string err;
   if (!pack_quantized(b, static_cast<int8_t*>(PackedBuf), q.data(), int(N), s.data(), isAsym ? z.data() : nullptr,
@@ -1716,7 +1734,7 @@ extern "C" void bestla_packweight_copyattr(const float* f32ptr, void* dstpr, int
   const int nblk = b.ngroups_k();
   std::vector<int8_t> q(size_t(k) * n), z(s.asym ? size_t(nblk) * n : 0);
   std::vector<float> sc(size_t(nblk) * n);
-  quantize_kblock(kn.data(), k, n, n, b.blocksize, dtype_bits(b.qtype), q.data(), sc.data(),
+  quantize_kblock(kn.data(), k, n, n, b.blocksize, b.qtype, q.data(), sc.data(),
                   s.asym ? z.data() : nullptr);
   if (!pack_quantized(b, static_cast<int8_t*>(dstpr), q.data(), n, sc.data(), s.asym ? z.data() : nullptr, nullptr,
                       &err)) {

@@ -70,6 +70,75 @@ __device__ __forceinline__ h8_t dequant_step(const u4_t& b, int d, h2_t c2) {
   return r;
 }
 
+// NFloat 4-bit weights (F4_BNB, F4_E2M1, F4_NF4): code -> value LUTs of bestla_utils.h:749-790, rounded to fp16 for
+// the MFMA B operand (the fp32 group scale is applied after the MFMA, as for the integer formats)
+static __constant__ _Float16 kF4LutH[3][16] = {
+    {_Float16(0.00000000f), _Float16(5.208333333e-03f), _Float16(0.66666667f), _Float16(1.00000000f),
+     _Float16(0.33333333f), _Float16(0.50000000f), _Float16(0.16666667f), _Float16(0.25000000f),
+     _Float16(-0.00000000f), _Float16(-5.208333333e-03f), _Float16(-0.66666667f), _Float16(-1.00000000f),
+     _Float16(-0.33333333f), _Float16(-0.50000000f), _Float16(-0.16666667f), _Float16(-0.25000000f)},
+    {_Float16(0.f), _Float16(0.010416666666666666f), _Float16(0.16666666666666666f), _Float16(0.25f),
+     _Float16(0.333333333333333f), _Float16(0.5f), _Float16(0.6666666666666f), _Float16(1.f), _Float16(-0.f),
+     _Float16(-0.010416666666666666f), _Float16(-0.16666666666666666f), _Float16(-0.25f),
+     _Float16(-0.333333333333333f), _Float16(-0.5f), _Float16(-0.6666666666666f), _Float16(-1.f)},
+    {_Float16(0.f), _Float16(-0.6961928009986877f), _Float16(-0.5250730514526367f), _Float16(-0.39491748809814453f),
+     _Float16(-0.28444138169288635f), _Float16(-0.18477343022823334f), _Float16(-0.09105003625154495f),
+     _Float16(-1.f), _Float16(0.07958029955625534f), _Float16(0.16093020141124725f), _Float16(0.24611230194568634f),
+     _Float16(0.33791524171829224f), _Float16(0.44070982933044434f), _Float16(0.5626170039176941f),
+     _Float16(0.7229568362236023f), _Float16(1.0f)}};
+
+// the 16 fp16 LUT entries as byte planes: lo[i] holds the low bytes of entries 4i..4i+3, hi[i] the high bytes
+struct F4Lut {
+  uint32_t lo[4], hi[4];
+};
+__device__ __forceinline__ F4Lut f4_lut_regs(int kind) {
+  F4Lut L;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    uint32_t lo = 0, hi = 0;
+#pragma unroll
+    for (int b = 0; b < 4; b++) {
+      const uint16_t v = __builtin_bit_cast(uint16_t, kF4LutH[kind][4 * i + b]);
+      lo |= uint32_t(v & 0xFF) << (8 * b);
+      hi |= uint32_t(v >> 8) << (8 * b);
+    }
+    L.lo[i] = lo;
+    L.hi[i] = hi;
+  }
+  return L;
+}
+// four codes (low nibbles of the bytes of N) -> the low / high bytes of their fp16 values: a byte permute from each
+// half of the table, then a per-byte select on the code's bit 3
+__device__ __forceinline__ void f4_lookup(uint32_t N, const F4Lut& L, uint32_t& lob, uint32_t& hib) {
+  const uint32_t S = N & 0x07070707u;
+  const uint32_t M = ((N >> 3) & 0x01010101u) * 0xFFu;
+  const uint32_t l0 = __builtin_amdgcn_perm(L.lo[1], L.lo[0], S), l1 = __builtin_amdgcn_perm(L.lo[3], L.lo[2], S);
+  const uint32_t h0 = __builtin_amdgcn_perm(L.hi[1], L.hi[0], S), h1 = __builtin_amdgcn_perm(L.hi[3], L.hi[2], S);
+  lob = (l0 & ~M) | (l1 & M);
+  hib = (h0 & ~M) | (h1 & M);
+}
+// one 32-deep step of a 4-bit tile (int4 element order, woq_layout.h) through the LUT -> 8 fp16 B-operand values
+__device__ __forceinline__ h8_t dequant_f4(const u4_t& b, int d, const F4Lut& L) {
+  const uint32_t w = b[d];
+  uint32_t la, ha, lb, hb;
+  f4_lookup(w & 0x0F0F0F0Fu, L, la, ha);         // slots: elements 0, 4, 1, 5
+  f4_lookup((w >> 4) & 0x0F0F0F0Fu, L, lb, hb);  // slots: elements 2, 6, 3, 7
+  const h2_t p01 = as_h2(__builtin_amdgcn_perm(ha, la, 0x06020400u));
+  const h2_t p23 = as_h2(__builtin_amdgcn_perm(hb, lb, 0x06020400u));
+  const h2_t p45 = as_h2(__builtin_amdgcn_perm(ha, la, 0x07030501u));
+  const h2_t p67 = as_h2(__builtin_amdgcn_perm(hb, lb, 0x07030501u));
+  h8_t r;
+  r[0] = p01[0];
+  r[1] = p01[1];
+  r[2] = p23[0];
+  r[3] = p23[1];
+  r[4] = p45[0];
+  r[5] = p45[1];
+  r[6] = p67[0];
+  r[7] = p67[1];
+  return r;
+}
+
 template <int BITS>
 __device__ __forceinline__ constexpr int bias_of() {
   return BITS == 4 ? 8 : (BITS == 2 ? 2 : 128);

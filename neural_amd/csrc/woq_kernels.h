@@ -37,6 +37,7 @@ struct SkinnyWeight {
   float* out;
   const float* bias;  // bias[m * bias_ld + n] (bias_ld = 0 broadcasts one row)
   int bias_ld;
+  int f4;             // NFloat 4-bit weight: LUT kind 0 = F4_BNB, 1 = F4_E2M1, 2 = F4_NF4; -1 = integer weight
 };
 
 struct SkinnyArgs {

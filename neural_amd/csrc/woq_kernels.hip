@@ -350,6 +350,7 @@ __global__ __launch_bounds__(1024) void woq_skinny_kernel(SkinnyArgs a) {
 
   f4_t acc = {0.f, 0.f, 0.f, 0.f};
   f4_t accg = {0.f, 0.f, 0.f, 0.f};
+  const F4Lut f4l = f4_lut_regs(BITS == 4 && W.f4 >= 0 ? W.f4 : 0);
   // group bookkeeping in scalars: g = group of the current step, rem = steps left in it
   const int spg = a.steps_per_group;
   const int st0 = tw0 * SPT;
@@ -374,7 +375,11 @@ __global__ __launch_bounds__(1024) void woq_skinny_kernel(SkinnyArgs a) {
           const int st = t * SPT + d;
           const int k0 = st * 32 + kq * 8;
           const h2_t c2 = as_h2(zc_l[g * 16]);
-          const h8_t bf = dequant_step<BITS>(b[i], d, c2);
+          h8_t bf;
+          if (BITS == 4 && W.f4 >= 0)
+            bf = dequant_f4(b[i], d, f4l);
+          else
+            bf = dequant_step<BITS>(b[i], d, c2);
           if constexpr (ALDS) {
             const h8_t af = *reinterpret_cast<const h8_t*>(smem + (aact ? a_hi_off + k0 * 2 : zero_off));
             if (HILO == 2) {
@@ -517,6 +522,7 @@ __global__ __launch_bounds__(256, 2) void woq_gemm_kernel(GemmArgs a) {
       acc[i][j] = f4_t{0.f, 0.f, 0.f, 0.f};
       accg[i][j] = f4_t{0.f, 0.f, 0.f, 0.f};
     }
+  const F4Lut f4l = f4_lut_regs(BITS == 4 && W.f4 >= 0 ? W.f4 : 0);
 
   // A staging map: 256 threads cover BM rows x KT k; each thread handles rows r0 + 32*i, chunk ch (8 k values)
   constexpr int TPR = CHUNKS;              // threads per row chunk group
@@ -573,7 +579,10 @@ __global__ __launch_bounds__(256, 2) void woq_gemm_kernel(GemmArgs a) {
         const int s = min(s0 + j, W.ns - 1);
         const size_t zi = scale_row(W.kmajor, W.ns, W.ng, s, g) * 16 + (lane & 15);
         const int zp = W.zps ? int(W.zps[zi]) : 0;
-        bf[j] = dequant_step<BITS>(bcur[j], d, zp_const(bias_of<BITS>() + zp));
+        if (BITS == 4 && W.f4 >= 0)
+          bf[j] = dequant_f4(bcur[j], d, f4l);
+        else
+          bf[j] = dequant_step<BITS>(bcur[j], d, zp_const(bias_of<BITS>() + zp));
       }
 #pragma unroll
       for (int i = 0; i < 4; i++) {

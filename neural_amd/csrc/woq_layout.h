@@ -53,6 +53,7 @@ struct DeviceWeight {
   void* reduce;       // bf16 [ng][red_ld]: the blob's reduce (Sum_k dequant(w) per block), integer-core blobs only
   int32_t red_ld;     // 0: no reduce
   int32_t blob_bs;    // the blob's own block size (per-channel: may exceed K; the int8-compute quantizer uses it)
+  int32_t f4kind;     // NFloat 4-bit weight (codes in the int4 layout, LUT dequant): 0 BNB, 1 E2M1, 2 NF4; -1 = integer
 };
 
 // Tile (s, t) and scale row (s, g) positions.  K-major interleaves the stripes at every K position, so the waves of a
@@ -91,6 +92,7 @@ inline uint64_t layout_geometry(DeviceWeight& w, int bits, int n, int k, int blo
   uint64_t shf = shuffle ? uint64_t(k) * 4 : 0;
   w.red_ld = reduce ? w.ns * 16 : 0;
   w.blob_bs = blocksize;
+  w.f4kind = -1;
   uint64_t rbytes = uint64_t(w.ng) * w.red_ld * 2;
   return align256(tiles) + align256(sbytes) + align256(zbytes) + align256(shf) + align256(rbytes);
 }

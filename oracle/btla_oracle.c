@@ -104,6 +104,10 @@ static inline int8_t cast_f32_s8(float v) {
 /* bestla_utils.h:522-525 cast<float,int>: int(roundf) */
 static inline int32_t cast_f32_int(float v) { return f2i_x86(roundf(v)); }
 
+int orc_f4_kind(uint32_t qtype);
+float orc_f4_lut(int kind, int code);
+void orc_quantize_f4_rowblock(const float* src, int8_t* dst, int row, int col, int ld_src, int ld_dst, float* scales,
+                              int blocksize, int kind);
 int orc_compress_planes(int bits, const int8_t* src, uint8_t* dst, size_t n);
 int orc_decompress_planes(int bits, const uint8_t* src, int8_t* dst, size_t n);
 
@@ -307,18 +311,21 @@ static void blob_describe(blob_t* b, int n, int k, int blocksize, uint32_t qtype
   b->n = n;
   b->k = k;
   b->bs = blocksize <= 0 ? b->kpad : blocksize;
-  b->prologue = 1; /* BTLA_PROLOGUEB_IDS::WeightKBlockNInteger (bestla.h:91-102) */
+  const int is_f4 = orc_f4_kind(qtype) >= 0;
+  /* BTLA_PROLOGUEB_IDS (bestla.h:91-102): WeightKBlockNInteger = 1, WeightKBlockNFloat = 2 */
+  b->prologue = is_f4 ? 2 : 1;
   b->coreid = coreid;
   b->dtype = qtype;
   b->scat = stype;
-  b->zpt = ORC_S8;
-  b->redt = ORC_BF16; /* reduce dtype fixed to BF16 by the callers, bestla_gemm.cpp:229,308,408 */
+  b->zpt = is_f4 ? 0 : ORC_S8;   /* StorageWeightKBlockNFloat::resize: zp / reduce dtypes EleBitsUndef (bestla_storage.h:849) */
+  b->redt = is_f4 ? 0 : ORC_BF16; /* reduce dtype fixed to BF16 by the callers, bestla_gemm.cpp:229,308,408 */
+  if (is_f4) asym = 0;
   b->q_size = updiv((size_t)b->npad * b->kpad * dtype_bits(qtype), 8);
   int nk = (int)updiv((size_t)b->kpad, (size_t)b->bs);
   b->cstep = b->npad;
   b->csize = (size_t)nk * b->npad;
   b->asym = asym;
-  b->has_red = orc_core_is_int(coreid);
+  b->has_red = is_f4 ? 0 : orc_core_is_int(coreid);
   b->has_shf = shuffle;
   b->s_size = b->csize * dtype_bytes(stype);
   b->z_size = asym ? b->csize * 1 : 0;
@@ -421,7 +428,7 @@ static int blob_parse(blob_t* b, const void* buf) {
   const int8_t* p = base;
   b->msize = r64(&p);
   b->prologue = r32(&p);
-  if (b->prologue != 1) return -1; /* only WeightKBlockNInteger */
+  if (b->prologue != 1 && b->prologue != 2) return -1; /* WeightKBlockNInteger / WeightKBlockNFloat */
   b->coreid = r64(&p);
   b->npad = (int)r32(&p);
   b->kpad = (int)r32(&p);
@@ -499,7 +506,10 @@ static void blob_dequant(const blob_t* b, const int8_t* base, float* W, int ldw,
   int8_t* flat = (int8_t*)malloc(nel);
   const uint8_t* q = (const uint8_t*)(base + b->q_off);
   int bits = dtype_bits(b->dtype);
-  if (bits == 4)
+  const int f4 = orc_f4_kind(b->dtype);
+  if (f4 >= 0)
+    for (size_t e = 0; e < nel; e++) flat[e] = (int8_t)((q[e / 2] >> (4 * (e & 1))) & 15);
+  else if (bits == 4)
     orc_decompress_s4(q, flat, nel);
   else if (bits == 2)
     orc_decompress_s2(q, flat, nel);
@@ -518,7 +528,8 @@ static void blob_dequant(const blob_t* b, const int8_t* base, float* W, int ldw,
       int z = zp ? zp[ci] : 0;
       float s = get_scale(sp, ci, b->scat);
       int8_t qv = qkn[(size_t)kk * b->n + nn];
-      if (W) W[(size_t)kk * ldw + nn] = (float)(qv - z) * s; /* kernel_ref.h:1035 */
+      if (W) W[(size_t)kk * ldw + nn] = f4 >= 0 ? orc_f4_lut(f4, qv) * s /* f4_dequantize, kernel_ref.h:1433-1438 */
+                                               : (float)(qv - z) * s; /* kernel_ref.h:1035 */
       if (Qout) Qout[(size_t)kk * b->n + nn] = qv;
     }
   }
@@ -555,7 +566,9 @@ static int blob_pack_q_impl(blob_t* b, int8_t* base, const int8_t* Q, int ldb, c
   orc_padding_interleave(Q, reordered, k, n, b->kpad, b->npad, ldb, b->kpad, nt, pr);
   uint8_t* q = (uint8_t*)(base + b->q_off);
   int bits = dtype_bits(b->dtype);
-  if (bits == 4)
+  if (orc_f4_kind(b->dtype) >= 0) /* compress_f4 (kernel_ref.h:167-176): codes as nibbles, element 2i low */
+    for (size_t e = 0; e < nel; e += 2) q[e / 2] = (uint8_t)((reordered[e] & 15) | ((reordered[e + 1] & 15) << 4));
+  else if (bits == 4)
     orc_compress_s4(reordered, q, nel);
   else if (bits == 2)
     orc_compress_s2(reordered, q, nel);
@@ -619,7 +632,10 @@ int orc_blob_quant_pack(void* buf, const float* B, int n, int k, int ldb, int bl
   float* s = (float*)malloc(sizeof(float) * (size_t)nk * n);
   int8_t* z = asym ? (int8_t*)malloc((size_t)nk * n) : NULL;
   /* quantizeWeight (bestla_prologue_b.h:472-488) with bsize = mBlockSize (block rows align to blocksize) */
-  orc_quantize_rowblock(kn, q, k, n, n, n, s, z, b.bs, dtype_bits(qtype));
+  if (orc_f4_kind(qtype) >= 0) /* WeightKBlockNFloat::quantRowBlock (bestla_prologue_b.h:1316-1338) */
+    orc_quantize_f4_rowblock(kn, q, k, n, n, n, s, b.bs, orc_f4_kind(qtype));
+  else
+    orc_quantize_rowblock(kn, q, k, n, n, n, s, z, b.bs, dtype_bits(qtype));
   int r = blob_pack_q_impl(&b, (int8_t*)buf, q, n, s, z);
   free(kn);
   free(q);
@@ -1092,4 +1108,85 @@ int orc_decompress_planes(int bits, const uint8_t* src, int8_t* dst, size_t n) {
     dst[e] = (int8_t)((int)u - (1 << (bits - 1)));
   }
   return 0;
+}
+
+/* ------------------------------------------------------------------ NFloat 4-bit weights (F4_BNB, F4_E2M1, F4_NF4) */
+/* dequant LUTs: bestla_utils.h:749-790 (the values the reference's unpack trees kernel_ref.h:1195-1360 return) */
+static const float k_f4_lut[3][16] = {
+    {0.00000000f, 5.208333333e-03f, 0.66666667f, 1.00000000f, 0.33333333f, 0.50000000f, 0.16666667f, 0.25000000f,
+     -1.f * 0.00000000f, -1.f * 5.208333333e-03f, -1.f * 0.66666667f, -1.f * 1.00000000f, -1.f * 0.33333333f,
+     -1.f * 0.50000000f, -1.f * 0.16666667f, -1.f * 0.25000000f},
+    {0.f, 0.010416666666666666f, 0.16666666666666666f, 0.25f, 0.333333333333333f, 0.5f, 0.6666666666666f, 1.f,
+     -1.f * 0.f, -1.f * 0.010416666666666666f, -1.f * 0.16666666666666666f, -1.f * 0.25f, -1.f * 0.333333333333333f,
+     -1.f * 0.5f, -1.f * 0.6666666666666f, -1.f * 1.f},
+    {0.f, -0.6961928009986877f, -0.5250730514526367f, -0.39491748809814453f, -0.28444138169288635f,
+     -0.18477343022823334f, -0.09105003625154495f, -1.f, 0.07958029955625534f, 0.16093020141124725f,
+     0.24611230194568634f, 0.33791524171829224f, 0.44070982933044434f, 0.5626170039176941f, 0.7229568362236023f,
+     1.0f}};
+/* f4 kind: 0 = F4_BNB (0x10004), 1 = F4_E2M1 (0x4 | float), 2 = F4_NF4 */
+int orc_f4_kind(uint32_t qtype) {
+  if (qtype == ORC_F4_BNB) return 0;
+  if (qtype == ORC_F4_E2M1) return 1;
+  if (qtype == ORC_F4_NF4) return 2;
+  return -1;
+}
+float orc_f4_lut(int kind, int code) { return k_f4_lut[kind][code & 15]; }
+
+/* kernel_ref.h:1233-1254 fp4_bnb_quantize */
+static int8_t f4_bnb_q(float x) {
+  int sign = x < 0 ? 0x8 : 0;
+  x = fabsf(x);
+  if (x > 0.29166667f) {
+    if (x > 0.583333f) return (int8_t)((x > 0.8333333f ? 0x3 : 0x2) + sign);
+    return (int8_t)((x > 0.4166667f ? 0x5 : 0x4) + sign);
+  }
+  if (x > 0.0859375f) return (int8_t)((x > 0.20833333f ? 0x7 : 0x6) + sign);
+  return (int8_t)((x > 0.00260417f ? 0x1 : 0x0) + sign);
+}
+/* kernel_ref.h:1256-1297 fp4_e2m1_quantize */
+static int8_t f4_e2m1_q(float x) {
+  int sign = x < 0 ? 0x8 : 0;
+  x = fabsf(x);
+  if (x > 1.75f / 6) {
+    if (x > 3.5f / 6) return (int8_t)((x > 5.f / 6 ? 0x7 : 0x6) + sign);
+    return (int8_t)((x > 2.5f / 6 ? 0x5 : 0x4) + sign);
+  }
+  if (x > 0.53125f / 6) return (int8_t)((x > 1.25f / 6 ? 0x3 : 0x2) + sign);
+  return (int8_t)((x > 0.03125f / 6 ? 0x1 : 0x0) + sign);
+}
+/* kernel_ref.h:1373-1419 nf4_quantize (codes of 0 and -1 swapped so that 0 pads as 0) */
+static int8_t f4_nf4_q(float x) {
+  if (x > 0.03979014977812767f) {
+    if (x > 0.3893125355243683f) {
+      if (x > 0.6427869200706482f) return x > 0.8614784181118011f ? 0xF : 0xE;
+      return x > 0.5016634166240692f ? 0xD : 0xC;
+    }
+    if (x > 0.2035212516784668f) return x > 0.2920137718319893f ? 0xB : 0xA;
+    return x > 0.1202552504837513f ? 0x9 : 0x8;
+  }
+  if (x > -0.33967943489551544f) {
+    if (x > -0.13791173323988914f) return x > -0.045525018125772476f ? 0x0 : 0x6;
+    return x > -0.23460740596055984f ? 0x5 : 0x4;
+  }
+  if (x > -0.6106329262256622f) return x > -0.4599952697753906f ? 0x3 : 0x2;
+  return x > -0.8480964004993439f ? 0x1 : 0x7;
+}
+int8_t orc_f4_quantize(int kind, float x) {
+  return kind == 0 ? f4_bnb_q(x) : (kind == 1 ? f4_e2m1_q(x) : f4_nf4_q(x));
+}
+/* kernel_ref.h:1800-1822 quantize_f32_f4_rowblock: per (column, K block) absmax (running max from FLT_MIN) -> scale;
+   code = f4_quantize(x * (1 / absmax)) */
+void orc_quantize_f4_rowblock(const float* src, int8_t* dst, int row, int col, int ld_src, int ld_dst, float* scales,
+                              int blocksize, int kind) {
+  for (int i = 0; i < col; i++) {
+    int align = row / blocksize * blocksize;
+    for (int j = 0; j < row; j += blocksize) {
+      int bs = j < align ? blocksize : row - align;
+      float absmax = FLT_MIN;
+      for (int ij = 0; ij < bs; ij++) absmax = smax(absmax, fabsf(src[(size_t)(j + ij) * ld_src + i]));
+      scales[(size_t)(j / blocksize) * ld_dst + i] = absmax;
+      for (int ij = 0; ij < bs; ij++)
+        dst[(size_t)(j + ij) * ld_dst + i] = orc_f4_quantize(kind, src[(size_t)(j + ij) * ld_src + i] * (1.f / absmax));
+    }
+  }
 }

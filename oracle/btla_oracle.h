@@ -28,6 +28,9 @@ extern "C" {
 #define ORC_S8 (8u | 0x100u)
 #define ORC_S4 (4u | 0x100u)
 #define ORC_S2 (2u | 0x100u)
+#define ORC_F4_E2M1 (4u)                 /* EleBits4 | TypeFloat          (bestla.h:82) */
+#define ORC_F4_BNB (4u | (1u << 16))     /* EleBits4 | TypeFloat | SubType1 */
+#define ORC_F4_NF4 (4u | (2u << 16))     /* EleBits4 | TypeFloat | SubType2 */
 
 /* fp16/bf16 conversions (bestla/bestla/bestla_utils.h:116-229) */
 uint16_t orc_f32_to_bf16(float v);
@@ -122,6 +125,15 @@ void orc_q4_0_dequantize_row(const uint8_t* x, float* y, int k);
 void orc_q8_0_quantize_row(const float* x, uint8_t* y, int k);
 float orc_vec_dot_q4_0_q8_0(int n, const uint8_t* vx, const uint8_t* vy);
 int orc_q4_0_forward(const float* A, const uint8_t* W, float* C, int m, int n, int k);
+
+
+/* NFloat 4-bit weights: LUTs bestla_utils.h:749-790, quantizers kernel_ref.h:1233-1419, quantize_f32_f4_rowblock
+   kernel_ref.h:1800-1822.  kind: 0 = F4_BNB, 1 = F4_E2M1, 2 = F4_NF4 */
+int orc_f4_kind(uint32_t qtype);
+float orc_f4_lut(int kind, int code);
+int8_t orc_f4_quantize(int kind, float x);
+void orc_quantize_f4_rowblock(const float* src, int8_t* dst, int row, int col, int ld_src, int ld_dst, float* scales,
+                              int blocksize, int kind);
 
 #ifdef __cplusplus
 }

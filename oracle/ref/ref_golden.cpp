@@ -315,6 +315,31 @@ static void case_compress_planes(const char* cs, size_t n) {
   }
 }
 
+// NFloat 4-bit: kernel_ref.h:1800-1822 quantize_f32_f4_rowblock, f4_dequantize (the unpack trees) and the
+// bestla_utils.h:749-790 LUTs the SIMD kernels use
+template <BTLA_DTYPE F4_T>
+static void case_f4(const char* cs, int row, int col, int bs, const float* lut) {
+  std::vector<float> src((size_t)row * col);
+  for (auto& v : src) v = urand(-1.f, 1.f);
+  for (int r = 0; r < bs && r < row; r++) src[(size_t)r * col] = 0.f;  // an all-zero block
+  int nblk = (row + bs - 1) / bs;
+  std::vector<int8_t> q((size_t)row * col);
+  std::vector<float> s((size_t)nblk * col), deq((size_t)row * col), lutv(lut, lut + 16), tree(16);
+  kernel::ref::quantize_f32_f4_rowblock<F4_T>(src.data(), q.data(), row, col, col, col, s.data(), bs);
+  for (int r = 0; r < row; r++)
+    for (int c = 0; c < col; c++)
+      deq[(size_t)r * col + c] = kernel::ref::f4_dequantize<F4_T>(q[(size_t)r * col + c], s[(size_t)(r / bs) * col + c]);
+  for (int code = 0; code < 16; code++) tree[code] = kernel::ref::f4_unpack<F4_T>((int8_t)code);
+  int meta[3] = {row, col, bs};
+  dump(cs, "meta", "i4", meta, 3);
+  dump(cs, "src", "f4", src.data(), src.size());
+  dump(cs, "q", "i1", q.data(), q.size());
+  dump(cs, "s", "f4", s.data(), s.size());
+  dump(cs, "deq", "f4", deq.data(), deq.size());
+  dump(cs, "lut", "f4", lutv.data(), 16);
+  dump(cs, "tree", "f4", tree.data(), 16);
+}
+
 int main(int argc, char** argv) {
   if (argc < 2) {
     fprintf(stderr, "usage: %s <outdir>\n", argv[0]);
@@ -360,6 +385,10 @@ int main(int argc, char** argv) {
   case_quant_u8("qu8_g64_big", 3, 512, 64, 1000.f);
   case_gemv_u8s8<48, 1>("gemv_u8s8_m1_sym", 512, 128, false);
   case_gemv_u8s8<48, 4>("gemv_u8s8_m4_asym", 512, 32, true);
+  case_f4<BTLA_DTYPE::F4_BNB>("f4_bnb_g32", 128, 19, 32, fp4_bnb_dequant_fp32_LUT);
+  case_f4<BTLA_DTYPE::F4_E2M1>("f4_e2m1_g64", 192, 13, 64, fp4_e2m1_dequant_fp32_LUT);
+  case_f4<BTLA_DTYPE::F4_NF4>("f4_nf4_g32", 128, 17, 32, nf4_dequant_fp32_LUT);
+  case_f4<BTLA_DTYPE::F4_NF4>("f4_nf4_perchannel", 100, 7, 100, nf4_dequant_fp32_LUT);
   fclose(g_man);
   return 0;
 }

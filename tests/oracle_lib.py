@@ -12,6 +12,7 @@ GOLDEN = os.path.join(REPO, "tests", "golden")
 F32, F16, BF16 = 32, 16, 16 | (1 << 16)
 S8, S4, S2 = 8 | 0x100, 4 | 0x100, 2 | 0x100
 S3, S5, S6, S7 = 3 | 0x100, 5 | 0x100, 6 | 0x100, 7 | 0x100
+F4_E2M1, F4_BNB, F4_NF4 = 4, 4 | (1 << 16), 4 | (2 << 16)
 BITS_TO_QTYPE = {8: S8, 7: S7, 6: S6, 5: S5, 4: S4, 3: S3, 2: S2}
 
 _p = C.c_void_p
@@ -72,6 +73,10 @@ class Oracle:
         L.orc_core_ktile.argtypes = [C.c_uint64]
         L.orc_core_ntile.argtypes = [C.c_uint64]
         L.orc_core_packrow.argtypes = [C.c_uint64]
+        L.orc_f4_lut.restype = C.c_float
+        L.orc_f4_lut.argtypes = [C.c_int, C.c_int]
+        L.orc_f4_kind.argtypes = [C.c_uint32]
+        L.orc_quantize_f4_rowblock.argtypes = [_p, _p] + [C.c_int] * 4 + [_p, C.c_int, C.c_int]
         L.orc_compress_planes.argtypes = [C.c_int, _p, _p, C.c_size_t]
         L.orc_decompress_planes.argtypes = [C.c_int, _p, _p, C.c_size_t]
         L.orc_quant_u8_colblock.argtypes = [C.c_int, C.c_int, _p, C.c_int, _p, C.c_int, _p, C.c_int, _p, C.c_int, _p]

@@ -1,4 +1,7 @@
-"""GPU parity for the 3/5/6/7-bit integer weights (quant_config.h:22-57 "int3".."int7"; planes of
+"""GPU parity for the 3/5/6/7-bit integer weights and the NFloat 4-bit weights (F4_NF4 / F4_E2M1 / F4_BNB,
+bestla_prologue_b.h:1005-1342: codes in the int4 tile layout, dequantized through the bestla_utils.h:749-790 LUT whose
+entries are rounded to fp16 for the MFMA B operand -- <= 2^-12 relative per weight, hence the 1e-3 bar) and the
+3/5/6/7-bit integer weights (quant_config.h:22-57 "int3".."int7"; planes of
 bestla_prologue_b.h:512-546).  The repack stores S3 in the int4 tile layout and S5-S7 in the int8 one (exact: the
 integers fit), so every forward kernel serves them; checked against the oracle's fp64 forward of the same blob, the
 repacked integers bit-exact, and the int8-compute mode against the oracle's kblock GEMM."""
@@ -6,7 +9,7 @@ import numpy as np
 import pytest
 
 from tests.conftest import gpu_available
-from tests.oracle_lib import BF16, F16, F32, S3, S5, S6, S7
+from tests.oracle_lib import BF16, F16, F32, F4_BNB, F4_E2M1, F4_NF4, S3, S5, S6, S7
 from tests.test_gpu_parity import _blob, _rel_err
 
 pytestmark = pytest.mark.gpu
@@ -23,7 +26,12 @@ CASES = [
     (128, 1024, 32, S6, F16, False, 4),
     (64, 512, 128, S7, F32, False, 1),
     (48, 300, 1024, S3, F32, False, 1),     # per-channel, K tail
+    (256, 1024, 32, F4_NF4, F32, False, 1),
+    (128, 512, 64, F4_E2M1, BF16, False, 2),
+    (96, 512, 32, F4_BNB, F16, False, 1),
+    (80, 300, 128, F4_NF4, F32, False, 1),  # K tail
 ]
+F4 = (F4_NF4, F4_E2M1, F4_BNB)
 TOL = {1: 2e-5, 64: 1e-3}
 
 
@@ -32,7 +40,7 @@ def test_repack_exact(oracle, cfg):
     n, k, bs, qt, st, asym, comp = cfg
     blob = _blob(oracle, n, k, bs, qt, st, asym, comp, seed=n + k)
     w = bestla.DeviceWeight(blob)
-    assert w.bits == (4 if qt == S3 else 8)
+    assert w.bits == (4 if qt in (S3,) + F4 else 8)
     assert np.array_equal(w.unpack().view(np.uint32), oracle.unpack_fp32(blob).view(np.uint32))
 
 
@@ -45,7 +53,8 @@ def test_forward_parity(oracle, cfg, m):
     A = np.random.default_rng(m + n).uniform(-0.5, 0.5, size=(m, k)).astype(np.float32)
     y = w.forward(torch.from_numpy(A).cuda()).cpu().numpy()
     ref = oracle.forward(A, blob, n, k)
-    assert _rel_err(y, ref) <= (TOL[1] if m <= 16 else TOL[64]), _rel_err(y, ref)
+    tol = 1e-3 if qt in F4 else (TOL[1] if m <= 16 else TOL[64])
+    assert _rel_err(y, ref) <= tol, _rel_err(y, ref)
 
 
 @pytest.mark.parametrize("m", [1, 64])

@@ -222,3 +222,23 @@ def test_compress_planes_bit_exact(oracle):
         assert oracle.lib.orc_decompress_planes(bits, np.ascontiguousarray(g[f"c{bits}"]).ctypes.data,
                                                 d.ctypes.data, n) == 0
         assert np.array_equal(d, g[f"d{bits}"]) and np.array_equal(d, src), bits
+
+
+@pytest.mark.parametrize("case,kind", [("f4_bnb_g32", 0), ("f4_e2m1_g64", 1), ("f4_nf4_g32", 2),
+                                       ("f4_nf4_perchannel", 2)])
+def test_f4_quantizer_and_lut_bit_exact(oracle, case, kind):
+    """NFloat 4-bit: the oracle's quantizer (kernel_ref.h:1233-1419,1800-1822) and LUT (bestla_utils.h:749-790)
+    against the reference; the reference's unpack trees and its LUTs agree code for code"""
+    g = G[case]
+    row, col, bs = (int(v) for v in g["meta"])
+    lut = np.array([oracle.lib.orc_f4_lut(kind, c) for c in range(16)], np.float32)
+    assert np.array_equal(lut.view(np.uint32), g["lut"].view(np.uint32))
+    assert np.array_equal(np.abs(g["tree"]), np.abs(g["lut"])) and np.array_equal(g["tree"], g["lut"])
+    q = np.zeros((row, col), np.int8)
+    nblk = -(-row // bs)
+    s = np.zeros((nblk, col), np.float32)
+    src = np.ascontiguousarray(g["src"].reshape(row, col))
+    oracle.lib.orc_quantize_f4_rowblock(src.ctypes.data, q.ctypes.data, row, col, col, col, s.ctypes.data, bs, kind)
+    assert np.array_equal(q.ravel(), g["q"]) and np.array_equal(s.ravel().view(np.uint32), g["s"].view(np.uint32))
+    deq = lut[q.astype(np.int64) & 15] * np.repeat(s, bs, axis=0)[:row]
+    assert np.array_equal(deq.ravel().view(np.uint32), g["deq"].view(np.uint32))
