@@ -32,13 +32,15 @@ EPI_NONE, EPI_BIAS, EPI_SILU_MUL, EPI_GELU_MUL, EPI_GELU, EPI_ADD_GELU, EPI_SILU
 
 S3, S5, S6, S7 = 3 | 0x100, 5 | 0x100, 6 | 0x100, 7 | 0x100
 F4_E2M1, F4_BNB, F4_NF4 = 4, 4 | (1 << 16), 4 | (2 << 16)
-# quant_config.h:22-57 parse_bits ("int1" and "fp8_e4m3"/"fp8_e5m2" are not supported here); "fp4_bnb" names the
-# F4_BNB type the reference packs but has no command-line name for
+F8_E4M3, F8_E5M2, F8_E8M0 = 8, 8 | (1 << 16), 8 | (3 << 16)
+# quant_config.h:22-57 parse_bits ("int1" is not supported here); "fp4_bnb" names the F4_BNB type the reference packs
+# but has no command-line name for
 _WEIGHT_DTYPES = {"int4": S4, "int8": S8, "int2": S2, "int3": S3, "int5": S5, "int6": S6, "int7": S7,
-                  "fp4_e2m1": F4_E2M1, "fp4": F4_E2M1, "nf4": F4_NF4, "fp4_bnb": F4_BNB}
-_SCALE_DTYPES = {"fp32": F32, "bf16": BF16, "fp16": F16}
+                  "fp4_e2m1": F4_E2M1, "fp4": F4_E2M1, "nf4": F4_NF4, "fp4_bnb": F4_BNB,
+                  "fp8_e4m3": F8_E4M3, "fp8": F8_E4M3, "fp8_e5m2": F8_E5M2}
+_SCALE_DTYPES = {"fp32": F32, "bf16": BF16, "fp16": F16, "fp8": F8_E8M0}
 _COMP = {"int8": COMP_INT8, "bf16": COMP_BF16, "fp16": COMP_F16, "fp32": COMP_F32, "auto": COMP_UNDEF}
-BITS = {S4: 4, S2: 2, S8: 8, S3: 3, S5: 5, S6: 6, S7: 7, F4_E2M1: 4, F4_BNB: 4, F4_NF4: 4}
+BITS = {S4: 4, S2: 2, S8: 8, S3: 3, S5: 5, S6: 6, S7: 7, F4_E2M1: 4, F4_BNB: 4, F4_NF4: 4, F8_E4M3: 8, F8_E5M2: 8}
 
 
 def _ptr(a):
@@ -72,12 +74,24 @@ def pack_size(n, k, block_size, weight_dtype=S4, scale_dtype=F32, asym=False, co
 def quantize(w_nk, group_size=32, weight_dtype="int4", scale_dtype="fp32", alg="sym", compute_dtype="int8"):
     """bestla_quantize (quant_utils.cpp:269-354): fp32 torch-layout weight [N][K] -> packed BTLA blob (uint8)."""
     w = np.ascontiguousarray(w_nk, dtype=np.float32)
-    n, k = w.shape
     qt = parse_weight_dtype(weight_dtype)
+    if scale_dtype not in _SCALE_DTYPES:
+        raise ValueError(f"unsupported scale_dtype {scale_dtype!r} (supported: {sorted(_SCALE_DTYPES)})")
     st = _SCALE_DTYPES[scale_dtype]
-    gsize = k if group_size == -1 else group_size
-    asym = alg == "asym"
-    comp = _COMP[compute_dtype]
+    if qt in (F8_E4M3, F8_E5M2):
+        st = F8_E8M0  # quant_utils.cpp:336-341: fp8 weights always get F8_E8M0 shared-exponent scales
+    elif st == F8_E8M0:
+        st = BF16  # quant_utils.cpp:329-335: anything but fp32 / fp16 is stored as bf16
+    gsize = w.shape[1] if group_size == -1 else group_size
+    return quant_pack(w, gsize, qt, st, alg == "asym", _COMP[compute_dtype])
+
+
+def quant_pack(w_nk, block_size, qtype, scale_type, asym, comp):
+    """BTLAGemmPackBSize + BTLAGemmQuantPackB on a torch-layout [N][K] weight with BTLA_DTYPE codes (bestla_gemm.cpp);
+    unlike quantize() any scale dtype the pack API accepts may be named (e.g. F32 scales for fp8 weights)."""
+    w = np.ascontiguousarray(w_nk, dtype=np.float32)
+    n, k = w.shape
+    gsize, qt, st = block_size, qtype, scale_type
     size = pack_size(n, k, gsize, qt, st, asym, comp)
     if not size:
         raise RuntimeError(f"no packing core for this configuration: {last_error()}")

@@ -171,7 +171,7 @@ Blob Blob::describe(int n, int k, int blocksize, uint32_t qtype, uint32_t scale_
   b.blocksize = blocksize <= 0 ? b.kpad : blocksize;
   b.qtype = qtype;
   b.scale_t = scale_t;
-  const bool f4 = f4_kind(qtype) >= 0;  // StorageWeightKBlockNFloat (bestla_storage.h:836-859): no zp, no reduce
+  const bool f4 = f4_kind(qtype) >= 0 || is_f8(qtype);  // StorageWeightKBlockNFloat (bestla_storage.h:836-859)
   b.prologue = f4 ? 2 : 1;
   b.zp_t = f4 ? 0 : kS8;
   b.red_t = f4 ? 0 : kBF16;
@@ -260,11 +260,13 @@ bool Blob::parse(const void* buf, std::string* err) {
   has_shuffle = r.get<uint8_t>() != 0;
   if (has_shuffle) shf_off = get_aligned(r, base, &shf_size);
   if (prologue == 2) {
-    if (f4_kind(qtype) < 0) return fail("NFloat weight dtype must be F4_BNB, F4_E2M1 or F4_NF4 (FP8 is not supported)");
+    if (f4_kind(qtype) < 0 && !is_f8(qtype))
+      return fail("NFloat weight dtype must be F4_BNB, F4_E2M1, F4_NF4, F8_E4M3 or F8_E5M2");
   } else if (!dtype_is_int(qtype) || dtype_bits(qtype) < 2 || dtype_bits(qtype) > 8) {
     return fail("weight dtype must be an integer type S2_CLIP .. S8 (S1 is not supported)");
   }
-  if (scale_t != kF32 && scale_t != kBF16 && scale_t != kF16) return fail("scale dtype must be F32, BF16 or F16");
+  if (scale_t != kF32 && scale_t != kBF16 && scale_t != kF16 && !(scale_t == kF8E8M0 && is_f8(qtype)))
+    return fail("scale dtype must be F32, BF16 or F16 (F8_E8M0 with F8 weights)");
   CoreInfo ci = core_info(core_id);
   if (ci.ntile <= 0 || (ci.packrow != 1 && ci.packrow != 2 && ci.packrow != 4)) return fail("unknown core id");
   if (npad % ci.ntile || kpad % ci.packrow) return fail("blob padding does not match its core");
@@ -325,6 +327,10 @@ float f16_to_f32(uint16_t h) {
 }
 
 static inline void store_scale(uint8_t* sp, size_t i, uint32_t t, float v) {
+  if (t == kF8E8M0) {  // setQuantCorrection F8_E8M0 (bestla_prologue_b.h:1198-1208): static_cast<uint8_t>(float)
+    sp[i] = uint8_t(f2i(v) & 0xff);
+    return;
+  }
   if (t == kF32) {
     std::memcpy(sp + i * 4, &v, 4);
   } else {
@@ -333,6 +339,7 @@ static inline void store_scale(uint8_t* sp, size_t i, uint32_t t, float v) {
   }
 }
 static inline float load_scale(const uint8_t* sp, size_t i, uint32_t t) {
+  if (t == kF8E8M0) return float(std::pow(2, int(int8_t(sp[i]))));  // decompress_kblock_f8_fp (kernel_ref.h:1013-1015)
   if (t == kF32) {
     float v;
     std::memcpy(&v, sp + i * 4, 4);
@@ -344,8 +351,33 @@ static inline float load_scale(const uint8_t* sp, size_t i, uint32_t t) {
 }
 
 // ----------------------------------------------------------------------------------------------- quantizer
+// bestla_utils.h:414-454: exponent bits 4 / 5, quantisation mantissa bits 5 / 4 (implicit one included), mx max norm
+// (E4M3 448, E5M2 57344)
+static float f8_maxnorm(uint32_t t) { return t == kF8E4M3 ? 448.f : 57344.f; }
 void quantize_kblock(const float* src, int K, int N, int ld_src, int bs, uint32_t qtype, int8_t* q, float* scales,
-                     int8_t* zp) {
+                     int8_t* zp, bool e8m0) {
+  if (is_f8(qtype)) {  // quantize_f32_f8_rowblock_mxscale (kernel_ref.h:1764-1800): e8m0 scales hold the exponent
+    const float maxnorm = f8_maxnorm(qtype);
+    const float emax = qtype == kF8E4M3 ? 8.f : 15.f;  // 2^(ebits-1), minus 1 for E5M2
+    parallel_for(N, [&](int n) {
+      for (int j = 0; j < K; j += bs) {
+        const int len = std::min(bs, K - j);
+        float scale = std::numeric_limits<float>::min();
+        for (int t = 0; t < len; t++) scale = smax(scale, std::fabs(src[size_t(j + t) * ld_src + n]));
+        if (e8m0) {
+          if (scale == 0) scale += std::numeric_limits<float>::min();
+          scale = std::floor(std::log2(scale)) - emax;
+          scale = scale < -127.f ? -127.f : scale;
+        } else {
+          scale /= maxnorm;
+        }
+        scales[size_t(j / bs) * N + n] = scale;
+        for (int t = 0; t < len; t++)
+          q[size_t(j + t) * N + n] = f8_quantize(qtype, src[size_t(j + t) * ld_src + n], scale, e8m0);
+      }
+    });
+    return;
+  }
   const int f4 = f4_kind(qtype);
   if (f4 >= 0) {  // quantize_f32_f4_rowblock (kernel_ref.h:1800-1822): absmax from FLT_MIN, code = f4(x * (1/absmax))
     parallel_for(N, [&](int n) {
@@ -570,10 +602,49 @@ void unpack_fp32(const Blob& b, const int8_t* base, float* W, int ldw) {
       size_t c = size_t(g) * b.cstep + nn;
       int z = b.asym ? base[b.z_off + c] : 0;
       const int f4 = f4_kind(b.qtype);
-      W[size_t(kk) * ldw + nn] = f4 >= 0 ? f4_lut(f4, read_q(b, qp, ci, kk, nn)) * load_scale(sp, c, b.scale_t)
-                                         : float(read_q(b, qp, ci, kk, nn) - z) * load_scale(sp, c, b.scale_t);
+      const int8_t qv = read_q(b, qp, ci, kk, nn);
+      const float sc = load_scale(sp, c, b.scale_t);
+      W[size_t(kk) * ldw + nn] = f4 >= 0 ? f4_lut(f4, qv) * sc : (is_f8(b.qtype) ? f8_to_f32(b.qtype, qv) * sc
+                                                                                   : float(qv - z) * sc);
     }
   });
+}
+
+// ----------------------------------------------------------------------------------------------- NFloat 8-bit
+
+// f8_mx_quantize (kernel_ref.h:1721-1762), one element: scale the value, round its mantissa to the format at the value's
+// own exponent (clamped below at the format's minimum normal exponent), clamp to the max norm and re-pack the fp32 bits
+// into sign | exponent | mantissa.  An exponent that wraps out of range stores 0 (the reference's uint8 arithmetic).
+int8_t f8_quantize(uint32_t t, float v, float scale, bool e8m0) {
+  v = e8m0 ? v / float(std::pow(2, scale)) : v / scale;
+  const int ebits = t == kF8E4M3 ? 4 : 5, qm = t == kF8E4M3 ? 5 : 4, mbits = 7 - ebits;
+  float pe = std::floor(std::log2(std::fabs(v == 0 ? v + 1 : v)));
+  const float min_exp = float(2 - (1 << (ebits - 1)));
+  pe = pe < min_exp ? min_exp : pe;
+  v = float(v / std::pow(2, pe) * std::pow(2, qm - 2));
+  const float sgn = v > 0 ? 1.f : -1.f;
+  v = sgn * float(std::floor(std::fabs(v) + 0.5));
+  v = float(v / std::pow(2, qm - 2) * std::pow(2, pe));
+  const float mx = f8_maxnorm(t);
+  v = v < -mx ? -mx : (v > mx ? mx : v);
+  uint32_t u;
+  std::memcpy(&u, &v, 4);
+  const uint8_t sbit = uint8_t((u >> 24) & 0x80);
+  uint8_t e = uint8_t(uint8_t(u >> 23) - 127 + (1 << (ebits - 1)) - 1);
+  if (e > uint8_t((1 << ebits) - 1)) e = 0;
+  const uint8_t m = uint8_t(((u >> 15) & 0xff) & uint8_t(0xff00u >> mbits)) >> (1 + ebits);
+  return int8_t(sbit | uint8_t(e << mbits) | m);
+}
+
+// f8_to_fp32 (kernel_ref.h:984-1001): the exponent field is always a normal one, bias 2^(ebits-1) - 1
+float f8_to_f32(uint32_t t, int8_t code) {
+  const uint32_t x = uint32_t(uint8_t(code));
+  const int ebits = t == kF8E4M3 ? 4 : 5, mbits = 7 - ebits;
+  const uint32_t e = ((x & 0x7f) >> mbits) - (1u << (ebits - 1)) + 1 + 127;
+  const uint32_t r = ((x & 0x80) << 24) | (e << 23) | ((x << (23 - mbits)) & 0x007fffffu);
+  float f;
+  std::memcpy(&f, &r, 4);
+  return f;
 }
 
 // ----------------------------------------------------------------------------------------------- NFloat 4-bit

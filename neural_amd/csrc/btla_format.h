@@ -27,9 +27,16 @@ enum : uint32_t {
   kF4E2M1 = 4,                // EleBits4 | TypeFloat (bestla.h:82-84)
   kF4BNB = 4 | (1u << 16),
   kF4NF4 = 4 | (2u << 16),
+  kF8E4M3 = 8,                // EleBits8 | TypeFloat (bestla.h:68-71)
+  kF8E5M2 = 8 | (1u << 16),
+  kF8E8M0 = 8 | (3u << 16),   // shared-exponent scale dtype (one int8 exponent per block)
   kDQ8_BNB = 8 | (4u << 16),
 };
 inline int dtype_bits(uint32_t t) { return int(t & 0xff); }
+inline bool is_f8(uint32_t t) { return t == kF8E4M3 || t == kF8E5M2; }
+// kernel_ref.h:984-1001 f8_to_fp32 (exponent field always read as normal) and :1721-1762 f8_mx_quantize
+float f8_to_f32(uint32_t t, int8_t code);
+int8_t f8_quantize(uint32_t t, float v, float scale, bool e8m0);
 // NFloat 4-bit kind (0 F4_BNB, 1 F4_E2M1, 2 F4_NF4) or -1
 inline int f4_kind(uint32_t t) { return t == kF4BNB ? 0 : (t == kF4E2M1 ? 1 : (t == kF4NF4 ? 2 : -1)); }
 // bestla_utils.h:749-790 dequant LUTs (the values of kernel_ref.h's unpack trees)
@@ -79,7 +86,7 @@ struct Blob {
 
   int ngroups() const { return int((kpad + blocksize - 1) / blocksize); }      // rows of the scale buffer
   int ngroups_k() const { return int((k + blocksize - 1) / blocksize); }       // groups covering real K
-  size_t scale_bytes() const { return scale_t == kF32 ? 4 : 2; }
+  size_t scale_bytes() const { return scale_t == kF32 ? 4 : (scale_t == kF8E8M0 ? 1 : 2); }
 
   // describe a fresh blob (createStorage + resize, bestla_prologue_b.h:120-127, bestla_storage.h:725-753)
   static Blob describe(int n, int k, int blocksize, uint32_t qtype, uint32_t scale_t, bool asym, uint64_t core_id,
@@ -92,8 +99,9 @@ struct Blob {
 
 // quantize_f32_sign_int_rowblock (bestla/bestla/kernel_ref.h:1608-1719), multithreaded over columns.
 // src is [K][ld_src] (K rows, N columns), outputs q [K][N], scales/zp [ceil(K/bs)][N].
+// F8 weights: quantize_f32_f8_rowblock_mxscale; with e8m0 the scales are the (float) shared exponents.
 void quantize_kblock(const float* src, int K, int N, int ld_src, int blocksize, uint32_t qtype, int8_t* q, float* scales,
-                     int8_t* zp);
+                     int8_t* zp, bool e8m0 = false);
 
 // packQWeight (bestla_prologue_b.h:378-398) into a buffer whose header was written by Blob::write_header.
 bool pack_quantized(Blob& b, int8_t* base, const int8_t* Q, int ldq, const float* S, const int8_t* Z,

@@ -104,15 +104,32 @@ extern "C" void bestla_device_sync(void* queue) { (void)hipStreamSynchronize(sta
 extern "C" size_t bestla_device_storage_size(void) { return sizeof(DeviceWeight); }
 
 // ------------------------------------------------------------------------------------------------ load / repack
-static int scale_code(uint32_t t) { return t == kF32 ? kScaleF32 : (t == kBF16 ? kScaleBF16 : kScaleF16); }
+// F8_E8M0 shared exponents become exact fp32 scales 2^e on the device
+static int scale_code(uint32_t t) {
+  return (t == kF32 || t == kF8E8M0) ? kScaleF32 : (t == kBF16 ? kScaleBF16 : kScaleF16);
+}
+// NFloat kind of the device weight: 0..2 the F4 LUTs (int4 layout), 3 F8_E4M3 / 4 F8_E5M2 (int8 layout, raw codes)
+static int nfloat_kind(uint32_t qtype) {
+  return is_f8(qtype) ? (qtype == kF8E4M3 ? 3 : 4) : f4_kind(qtype);
+}
 
-static bool blob_supported(const Blob& b, std::string* err) {
+// base: the host blob, scanned for codes the device cannot hold (load time only; null skips the scan)
+static bool blob_supported(const Blob& b, const void* base, std::string* err) {
   if (b.blocksize % 32 != 0 && b.blocksize < b.k) {
     *err = "quantization group size must be a multiple of 32 (or per-channel)";
     return false;
   }
+  if (base && b.qtype == kF8E5M2) {  // exponent field 31 (2^16 and up) has no fp16 B operand; the quantizer never writes it
+    const uint8_t* q = static_cast<const uint8_t*>(base) + b.q_off;
+    for (uint64_t i = 0; i < b.q_size; i++)
+      if ((q[i] & 0x7c) == 0x7c) {
+        *err = "F8_E5M2 code with exponent field 31 (|w| >= 65536 * scale) is not supported";
+        return false;
+      }
+  }
   return true;
 }
+static bool blob_supported(const Blob& b, std::string* err) { return blob_supported(b, nullptr, err); }
 
 extern "C" size_t nad_device_weight_size(const void* hostblob) {
   Blob b;
@@ -134,7 +151,7 @@ extern "C" int nad_device_load(const void* hostblob, void* devstor, void* device
     set_err("null devstor/deviceptr");
     return -1;
   }
-  if (!b.parse(hostblob, &err) || !blob_supported(b, &err)) {
+  if (!b.parse(hostblob, &err) || !blob_supported(b, hostblob, &err)) {
     set_err("%s", err.c_str());
     return -1;
   }
@@ -154,7 +171,8 @@ extern "C" int nad_device_load(const void* hostblob, void* devstor, void* device
   w.src_core_id = b.core_id;
   w.owner = nullptr;
   w.blob_bs = b.blocksize;
-  w.f4kind = f4_kind(b.qtype);  // F4 codes go through the int4 repack unchanged (blob_q returns code - 8, + 8 back)
+  // F4 codes go through the int4 repack unchanged (blob_q returns code - 8, + 8 back); F8 codes are stored raw
+  w.f4kind = nfloat_kind(b.qtype);
   // stage the raw blob buffers on the device, repack there
   const uint8_t* base = static_cast<const uint8_t*>(hostblob);
   uint8_t* stage = nullptr;
@@ -182,6 +200,8 @@ extern "C" int nad_device_load(const void* hostblob, void* devstor, void* device
   ra.kpad = b.kpad;
   ra.cstep = b.cstep;
   ra.src_bits = dtype_bits(b.qtype);
+  ra.raw = is_f8(b.qtype) ? 1 : 0;
+  ra.src_e8m0 = b.scale_t == kF8E8M0 ? 1 : 0;
   ra.nel = uint64_t(b.npad) * b.kpad;
   ra.bits = w.bits;
   ra.n = w.n;
@@ -1217,7 +1237,15 @@ __global__ void nad_unrepack_kernel(DeviceWeight w, float* out) {
     else
       sc = float(static_cast<const _Float16*>(w.scales)[si]);
     const int zp = w.zps ? int(w.zps[si]) : 0;
-    out[i] = w.f4kind >= 0 ? kF4LutF[w.f4kind][v & 15] * sc : float(int(v) - bias - zp) * sc;
+    float q;
+    if (w.f4kind >= 3) {  // F8 raw code (f8_to_fp32, kernel_ref.h:984-1001)
+      const int eb = w.f4kind == 3 ? 4 : 5, mb = 7 - eb;
+      const uint32_t e = ((v & 0x7f) >> mb) - (1u << (eb - 1)) + 128;
+      q = __uint_as_float(((v & 0x80) << 24) | (e << 23) | ((v << (23 - mb)) & 0x7fffffu));
+    } else {
+      q = w.f4kind >= 0 ? kF4LutF[w.f4kind][v & 15] : float(int(v) - bias - zp);
+    }
+    out[i] = q * sc;
   }
 }
 
@@ -1619,8 +1647,12 @@ extern "C" void nad_host_cache_clear(void) {
 // ------------------------------------------------------------------------------------------------ pack API
 extern "C" size_t BTLAGemmPackBSize(size_t N, size_t K, size_t BlkSize, uint32_t QuantType, uint32_t ScaleDtype,
                                     bool isAsym, int CompType, int* shuffle_indice) {
-  if (!dtype_is_int(QuantType) && f4_kind(QuantType) < 0) {
-    set_err("float weight dtypes other than F4_BNB / F4_E2M1 / F4_NF4 (fp8) are not supported by this backend");
+  if (!dtype_is_int(QuantType) && f4_kind(QuantType) < 0 && !is_f8(QuantType)) {
+    set_err("weight dtype must be an integer, F4_BNB / F4_E2M1 / F4_NF4 or F8_E4M3 / F8_E5M2");
+    return 0;
+  }
+  if (ScaleDtype == kF8E8M0 && !is_f8(QuantType)) {
+    set_err("F8_E8M0 scales go with F8 weights only");
     return 0;
   }
   uint64_t core = select_core(CompType, QuantType, int(BlkSize), isAsym, host_isa_profile());
@@ -1632,7 +1664,8 @@ extern "C" size_t BTLAGemmPackBSize(size_t N, size_t K, size_t BlkSize, uint32_t
 extern "C" bool BTLAGemmQuantPackB(void* PackedBuf, const float* FpData, size_t N, size_t K, size_t ldb,
                                    size_t BlkSize, uint32_t QuantType, uint32_t ScaleDtype, bool isAsym, int CompType,
                                    bool isTrans, void* ThreadPool) {
-  if ((!dtype_is_int(QuantType) && f4_kind(QuantType) < 0) || !PackedBuf || !FpData) return false;
+  if ((!dtype_is_int(QuantType) && f4_kind(QuantType) < 0 && !is_f8(QuantType)) || !PackedBuf || !FpData) return false;
+  if (ScaleDtype == kF8E8M0 && !is_f8(QuantType)) return false;
   uint64_t core = select_core(CompType, QuantType, int(BlkSize), isAsym, host_isa_profile());
   if (!core) return false;
   Blob b = Blob::describe(int(N), int(K), int(BlkSize), QuantType, ScaleDtype, isAsym, core, false);
@@ -1653,7 +1686,7 @@ extern "C" bool BTLAGemmQuantPackB(void* PackedBuf, const float* FpData, size_t 
   std::vector<int8_t> q(K * N), z(isAsym ? size_t(nblk) * N : 0);
   std::vector<float> s(size_t(nblk) * N);
   quantize_kblock(src, int(K), int(N), ld, b.blocksize, uint32_t(QuantType), q.data(), s.data(),
-                  isAsym ? z.data() : nullptr);
+                  b.asym ? z.data() : nullptr, ScaleDtype == kF8E8M0);
   std::string err;
   if (!pack_quantized(b, static_cast<int8_t*>(PackedBuf), q.data(), int(N), s.data(), isAsym ? z.data() : nullptr,
                       nullptr, &err)) {

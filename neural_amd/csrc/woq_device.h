@@ -139,6 +139,40 @@ __device__ __forceinline__ h8_t dequant_f4(const u4_t& b, int d, const F4Lut& L)
   return r;
 }
 
+// NFloat 8-bit weights: raw codes in the int8 layout -> the exact fp16 of f8_to_fp32 (kernel_ref.h:984-1001, which
+// reads every exponent field as a normal one).  E4M3: fp16 exponent = e + 8, mantissa m << 7.  E5M2: the code is the
+// fp16's top byte for e >= 1; e = 0 (2^-15 (1 + m/4)) is the fp16 subnormal (m << 7) + 0x200 -- as bit patterns the
+// right value is max(c << 8, ((c << 8) >> 1) + 0x200) per half for every e < 31 (e = 31 is rejected at load).
+typedef uint16_t us2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t f8_pair(uint32_t w, uint32_t sel_lo, uint32_t sel_hi, bool e5m2) {
+  if (!e5m2) {
+    const uint32_t t = __builtin_amdgcn_perm(0u, w, sel_lo);  // codes in the low byte of each half
+    return (((t & 0x007F007Fu) << 7) + 0x20002000u) | ((t & 0x00800080u) << 8);
+  }
+  const uint32_t t = __builtin_amdgcn_perm(0u, w, sel_hi);    // codes in the high byte of each half
+  const uint32_t mag = t & 0x7FFF7FFFu;
+  const us2_t r = __builtin_elementwise_max(__builtin_bit_cast(us2_t, mag),
+                                            __builtin_bit_cast(us2_t, (mag >> 1) + 0x02000200u));
+  return __builtin_bit_cast(uint32_t, r) | (t & 0x80008000u);
+}
+__device__ __forceinline__ h8_t dequant_f8(const u4_t& b, int d, bool e5m2) {
+  const uint32_t w0 = b[2 * d], w1 = b[2 * d + 1];
+  const h2_t p0 = as_h2(f8_pair(w0, 0x04010400u, 0x01040004u, e5m2));
+  const h2_t p1 = as_h2(f8_pair(w0, 0x04030402u, 0x03040204u, e5m2));
+  const h2_t p2 = as_h2(f8_pair(w1, 0x04010400u, 0x01040004u, e5m2));
+  const h2_t p3 = as_h2(f8_pair(w1, 0x04030402u, 0x03040204u, e5m2));
+  h8_t r;
+  r[0] = p0[0];
+  r[1] = p0[1];
+  r[2] = p1[0];
+  r[3] = p1[1];
+  r[4] = p2[0];
+  r[5] = p2[1];
+  r[6] = p3[0];
+  r[7] = p3[1];
+  return r;
+}
+
 template <int BITS>
 __device__ __forceinline__ constexpr int bias_of() {
   return BITS == 4 ? 8 : (BITS == 2 ? 2 : 128);

@@ -19,6 +19,8 @@ struct RepackArgs {
   int ntile, packrow, kpad, cstep;
   int src_bits;         // blob element bits: 2, 3, 4, 5, 6, 7, 8 (3/5/6/7 in bit planes, bestla_prologue_b.h:512-546)
   uint64_t nel;         // NPad * KPad: plane size of the multi-plane formats
+  int raw;              // F8 weights: store the 8-bit code as it is (no + 128 bias)
+  int src_e8m0;         // source scales are F8_E8M0 exponents (one byte each) -> fp32 2^e
   // destination geometry (bits: the device layout's 2 / 4 / 8 -- S3 lands in the int4 layout, S5-S7 in int8)
   int bits, n, k, ns, nt, ng, scale_t, kmajor;
   uint32_t* dst_tiles;
@@ -37,7 +39,8 @@ struct SkinnyWeight {
   float* out;
   const float* bias;  // bias[m * bias_ld + n] (bias_ld = 0 broadcasts one row)
   int bias_ld;
-  int f4;             // NFloat 4-bit weight: LUT kind 0 = F4_BNB, 1 = F4_E2M1, 2 = F4_NF4; -1 = integer weight
+  int f4;             // NFloat weight: 0 = F4_BNB, 1 = F4_E2M1, 2 = F4_NF4 (int4 layout, LUT), 3 = F8_E4M3,
+                      // 4 = F8_E5M2 (int8 layout, raw codes); -1 = integer weight
 };
 
 struct SkinnyArgs {

@@ -94,9 +94,10 @@ __global__ void nad_repack_kernel(RepackArgs a) {
       if (n < a.n && k < a.k) {
         const uint64_t e = uint64_t(n / a.ntile) * a.ntile * a.kpad + uint64_t(k / a.packrow) * a.ntile * a.packrow +
                            uint64_t(n % a.ntile) * a.packrow + uint64_t(k % a.packrow);
-        v = uint32_t(blob_q(a, e) + (a.bits == 4 ? 8 : (a.bits == 2 ? 2 : 128)));  // device: q + 2^(bits-1)
+        v = a.raw ? uint32_t(blob_q(a, e)) & 0xFFu
+                  : uint32_t(blob_q(a, e) + (a.bits == 4 ? 8 : (a.bits == 2 ? 2 : 128)));  // device: q + 2^(bits-1)
       } else {
-        v = a.bits == 4 ? 8u : (a.bits == 2 ? 2u : 128u);  // q = 0 padding
+        v = a.raw ? 0u : (a.bits == 4 ? 8u : (a.bits == 2 ? 2u : 128u));  // q = 0 padding (F8: code 0)
       }
       out |= v << (a.bits * p);
     }
@@ -113,7 +114,9 @@ __global__ void nad_repack_scales_kernel(RepackArgs a) {
     const bool ok = n < a.n;
     const uint64_t src = uint64_t(g) * a.cstep + n;
     const uint64_t dst = scale_row(a.kmajor, a.ns, a.ng, s, g) * 16 + c;
-    if (ssz == 4) {
+    if (a.src_e8m0) {  // decompress_kblock_f8_fp (kernel_ref.h:1013-1015): scale = 2^(int8)e, exact in fp32
+      static_cast<float*>(a.dst_scales)[dst] = ok ? ldexpf(1.f, int(reinterpret_cast<const int8_t*>(a.src_s)[src])) : 0.f;
+    } else if (ssz == 4) {
       static_cast<float*>(a.dst_scales)[dst] = ok ? reinterpret_cast<const float*>(a.src_s)[src] : 0.f;
     } else {
       static_cast<uint16_t*>(a.dst_scales)[dst] = ok ? reinterpret_cast<const uint16_t*>(a.src_s)[src] : 0;
@@ -378,6 +381,8 @@ __global__ __launch_bounds__(1024) void woq_skinny_kernel(SkinnyArgs a) {
           h8_t bf;
           if (BITS == 4 && W.f4 >= 0)
             bf = dequant_f4(b[i], d, f4l);
+          else if (BITS == 8 && W.f4 >= 3)
+            bf = dequant_f8(b[i], d, W.f4 == 4);
           else
             bf = dequant_step<BITS>(b[i], d, c2);
           if constexpr (ALDS) {
@@ -581,6 +586,8 @@ __global__ __launch_bounds__(256, 2) void woq_gemm_kernel(GemmArgs a) {
         const int zp = W.zps ? int(W.zps[zi]) : 0;
         if (BITS == 4 && W.f4 >= 0)
           bf[j] = dequant_f4(bcur[j], d, f4l);
+        else if (BITS == 8 && W.f4 >= 3)
+          bf[j] = dequant_f8(bcur[j], d, W.f4 == 4);
         else
           bf[j] = dequant_step<BITS>(bcur[j], d, zp_const(bias_of<BITS>() + zp));
       }

@@ -53,7 +53,8 @@ struct DeviceWeight {
   void* reduce;       // bf16 [ng][red_ld]: the blob's reduce (Sum_k dequant(w) per block), integer-core blobs only
   int32_t red_ld;     // 0: no reduce
   int32_t blob_bs;    // the blob's own block size (per-channel: may exceed K; the int8-compute quantizer uses it)
-  int32_t f4kind;     // NFloat 4-bit weight (codes in the int4 layout, LUT dequant): 0 BNB, 1 E2M1, 2 NF4; -1 = integer
+  int32_t f4kind;     // NFloat weight: 0 F4_BNB, 1 F4_E2M1, 2 F4_NF4 (codes in the int4 layout, LUT dequant),
+                      // 3 F8_E4M3, 4 F8_E5M2 (raw codes in the int8 layout); -1 = integer
 };
 
 // Tile (s, t) and scale row (s, g) positions.  K-major interleaves the stripes at every K position, so the waves of a

@@ -106,6 +106,9 @@ static inline int32_t cast_f32_int(float v) { return f2i_x86(roundf(v)); }
 
 int orc_f4_kind(uint32_t qtype);
 float orc_f4_lut(int kind, int code);
+float orc_f8_to_f32(uint32_t t, int8_t code);
+void orc_quantize_f8_rowblock(const float* src, int8_t* dst, int row, int col, int ld_src, int ld_dst, float* scales,
+                              int blocksize, uint32_t t, int e8m0);
 void orc_quantize_f4_rowblock(const float* src, int8_t* dst, int row, int col, int ld_src, int ld_dst, float* scales,
                               int blocksize, int kind);
 int orc_compress_planes(int bits, const int8_t* src, uint8_t* dst, size_t n);
@@ -311,7 +314,7 @@ static void blob_describe(blob_t* b, int n, int k, int blocksize, uint32_t qtype
   b->n = n;
   b->k = k;
   b->bs = blocksize <= 0 ? b->kpad : blocksize;
-  const int is_f4 = orc_f4_kind(qtype) >= 0;
+  const int is_f4 = orc_f4_kind(qtype) >= 0 || qtype == ORC_F8_E4M3 || qtype == ORC_F8_E5M2; /* NFloat */
   /* BTLA_PROLOGUEB_IDS (bestla.h:91-102): WeightKBlockNInteger = 1, WeightKBlockNFloat = 2 */
   b->prologue = is_f4 ? 2 : 1;
   b->coreid = coreid;
@@ -477,7 +480,9 @@ int orc_blob_info(const void* buf, int64_t* o) {
 /* store one scale value in the blob's scale dtype (setQuantCorrection, bestla_prologue_b.h:244-271):
    BF16 via bf16(float) RNE; F16 via the host's vcvtps2ph (IEEE RNE) on AVX512-FP16 hosts */
 static void put_scale(uint8_t* sp, size_t idx, uint32_t scat, float v) {
-  if (scat == ORC_F32) {
+  if (scat == ORC_F8_E8M0) { /* setQuantCorrection F8_E8M0 (bestla_prologue_b.h:1198-1208): static_cast<uint8_t> */
+    sp[idx] = (uint8_t)(f2i_x86(v) & 0xff);
+  } else if (scat == ORC_F32) {
     memcpy(sp + idx * 4, &v, 4);
   } else if (scat == ORC_BF16) {
     uint16_t h = orc_f32_to_bf16(v);
@@ -488,6 +493,7 @@ static void put_scale(uint8_t* sp, size_t idx, uint32_t scat, float v) {
   }
 }
 static float get_scale(const uint8_t* sp, size_t idx, uint32_t scat) {
+  if (scat == ORC_F8_E8M0) return (float)pow(2, (int8_t)sp[idx]); /* decompress_kblock_f8_fp, kernel_ref.h:1013-1015 */
   if (scat == ORC_F32) {
     float v;
     memcpy(&v, sp + idx * 4, 4);
@@ -507,6 +513,7 @@ static void blob_dequant(const blob_t* b, const int8_t* base, float* W, int ldw,
   const uint8_t* q = (const uint8_t*)(base + b->q_off);
   int bits = dtype_bits(b->dtype);
   const int f4 = orc_f4_kind(b->dtype);
+  const int f8 = b->dtype == ORC_F8_E4M3 || b->dtype == ORC_F8_E5M2;
   if (f4 >= 0)
     for (size_t e = 0; e < nel; e++) flat[e] = (int8_t)((q[e / 2] >> (4 * (e & 1))) & 15);
   else if (bits == 4)
@@ -528,8 +535,10 @@ static void blob_dequant(const blob_t* b, const int8_t* base, float* W, int ldw,
       int z = zp ? zp[ci] : 0;
       float s = get_scale(sp, ci, b->scat);
       int8_t qv = qkn[(size_t)kk * b->n + nn];
-      if (W) W[(size_t)kk * ldw + nn] = f4 >= 0 ? orc_f4_lut(f4, qv) * s /* f4_dequantize, kernel_ref.h:1433-1438 */
-                                               : (float)(qv - z) * s; /* kernel_ref.h:1035 */
+      if (W)
+        W[(size_t)kk * ldw + nn] = f4 >= 0 ? orc_f4_lut(f4, qv) * s /* f4_dequantize, kernel_ref.h:1433-1438 */
+                                   : f8 ? orc_f8_to_f32(b->dtype, qv) * s /* decompress_kblock_f8_fp :1003-1026 */
+                                        : (float)(qv - z) * s;            /* kernel_ref.h:1035 */
       if (Qout) Qout[(size_t)kk * b->n + nn] = qv;
     }
   }
@@ -566,7 +575,9 @@ static int blob_pack_q_impl(blob_t* b, int8_t* base, const int8_t* Q, int ldb, c
   orc_padding_interleave(Q, reordered, k, n, b->kpad, b->npad, ldb, b->kpad, nt, pr);
   uint8_t* q = (uint8_t*)(base + b->q_off);
   int bits = dtype_bits(b->dtype);
-  if (orc_f4_kind(b->dtype) >= 0) /* compress_f4 (kernel_ref.h:167-176): codes as nibbles, element 2i low */
+  if (b->dtype == ORC_F8_E4M3 || b->dtype == ORC_F8_E5M2) /* F8: reorderWeight only (bestla_prologue_b.h:1137) */
+    memcpy(q, reordered, nel);
+  else if (orc_f4_kind(b->dtype) >= 0) /* compress_f4 (kernel_ref.h:167-176): codes as nibbles, element 2i low */
     for (size_t e = 0; e < nel; e += 2) q[e / 2] = (uint8_t)((reordered[e] & 15) | ((reordered[e + 1] & 15) << 4));
   else if (bits == 4)
     orc_compress_s4(reordered, q, nel);
@@ -634,6 +645,8 @@ int orc_blob_quant_pack(void* buf, const float* B, int n, int k, int ldb, int bl
   /* quantizeWeight (bestla_prologue_b.h:472-488) with bsize = mBlockSize (block rows align to blocksize) */
   if (orc_f4_kind(qtype) >= 0) /* WeightKBlockNFloat::quantRowBlock (bestla_prologue_b.h:1316-1338) */
     orc_quantize_f4_rowblock(kn, q, k, n, n, n, s, b.bs, orc_f4_kind(qtype));
+  else if (qtype == ORC_F8_E4M3 || qtype == ORC_F8_E5M2)
+    orc_quantize_f8_rowblock(kn, q, k, n, n, n, s, b.bs, qtype, stype == ORC_F8_E8M0);
   else
     orc_quantize_rowblock(kn, q, k, n, n, n, s, z, b.bs, dtype_bits(qtype));
   int r = blob_pack_q_impl(&b, (int8_t*)buf, q, n, s, z);
@@ -1187,6 +1200,93 @@ void orc_quantize_f4_rowblock(const float* src, int8_t* dst, int row, int col, i
       scales[(size_t)(j / blocksize) * ld_dst + i] = absmax;
       for (int ij = 0; ij < bs; ij++)
         dst[(size_t)(j + ij) * ld_dst + i] = orc_f4_quantize(kind, src[(size_t)(j + ij) * ld_src + i] * (1.f / absmax));
+    }
+  }
+}
+
+/* ------------------------------------------------------------------ NFloat 8-bit weights (F8_E4M3, F8_E5M2) */
+/* bestla_utils.h:414-454 (ebits, quant mantissa bits, mx max norm) */
+static int f8_ebits(uint32_t t) { return t == ORC_F8_E4M3 ? 4 : 5; }
+static int f8_qmbits(uint32_t t) { return t == ORC_F8_E4M3 ? 5 : 4; }
+static float f8_maxnorm(uint32_t t) {
+  int ebits = f8_ebits(t), mb = f8_qmbits(t);
+  double emax = pow(2, ebits - 1);
+  if (t == ORC_F8_E5M2) emax -= 1;
+  double max_norm = pow(2, emax);
+  if (t != ORC_F8_E4M3)
+    max_norm *= ((pow(2, mb - 1) - 1) / pow(2, mb - 2));
+  else
+    max_norm *= 1.75;
+  return (float)max_norm;
+}
+/* kernel_ref.h:1721-1762 f8_mx_quantize (float / double steps as the reference's std:: overloads resolve them) */
+int8_t orc_f8_quantize(uint32_t t, float v, float scale, int e8m0) {
+  if (e8m0)
+    v /= (float)pow(2, scale);
+  else
+    v /= scale;
+  const int ebits = f8_ebits(t), qm = f8_qmbits(t), store_mantissa = 7 - ebits;
+  float private_exp = floorf(log2f(fabsf(v == 0 ? v + 1 : v)));
+  const float min_exp = (float)(-1 * (pow(2, ebits - 1)) + 2);
+  private_exp = private_exp < min_exp ? min_exp : private_exp;
+  v = (float)(v / pow(2, private_exp) * pow(2, qm - 2));
+  const int sign = v > 0 ? 1 : -1;
+  v = sign * (float)floor(fabsf(v) + 0.5);
+  v = (float)(v / pow(2, qm - 2) * pow(2, private_exp));
+  const float max_norm = f8_maxnorm(t);
+  v = v < -1 * max_norm ? -1 * max_norm : (v > max_norm ? max_norm : v); /* std::clamp */
+  uint32_t u;
+  memcpy(&u, &v, 4);
+  const uint8_t store_signbit = (uint8_t)((u >> 24) & 0x80);
+  u <<= 1;
+  uint8_t store_ebit = (uint8_t)(u >> 24);
+  store_ebit = (uint8_t)(store_ebit - 127 + (uint8_t)pow(2, ebits - 1) - 1);
+  if (store_ebit > 15 && t == ORC_F8_E4M3) store_ebit = 0;
+  if (store_ebit > 31 && t == ORC_F8_E5M2) store_ebit = 0;
+  store_ebit = (uint8_t)(store_ebit << store_mantissa);
+  u <<= 8;
+  const int8_t mask = (int8_t)(-128 >> (store_mantissa - 1));
+  uint8_t store_mantissabit = (uint8_t)((u >> 24) & (uint8_t)mask);
+  store_mantissabit = (uint8_t)(store_mantissabit >> (1 + ebits));
+  return (int8_t)(store_signbit | store_ebit | store_mantissabit);
+}
+/* kernel_ref.h:984-1001 f8_to_fp32: the exponent field is always read as a normal one (no subnormals) */
+float orc_f8_to_f32(uint32_t t, int8_t code) {
+  uint32_t x = (uint32_t)(int32_t)code;
+  uint32_t s = (x << 24) & 0x80000000u;
+  const int ebits = f8_ebits(t), mb = 7 - ebits;
+  uint32_t e = (x & 0x7f) >> mb;
+  e = e - (uint32_t)pow(2, ebits - 1) + 1 + 127;
+  e <<= 23;
+  uint32_t m = (x << (23 - mb)) & 0x007fffffu;
+  uint32_t r = s | e | m;
+  float f;
+  memcpy(&f, &r, 4);
+  return f;
+}
+/* kernel_ref.h:1764-1800 quantize_f32_f8_rowblock_mxscale; e8m0: scales hold the (float) shared exponent */
+void orc_quantize_f8_rowblock(const float* src, int8_t* dst, int row, int col, int ld_src, int ld_dst, float* scales,
+                              int blocksize, uint32_t t, int e8m0) {
+  for (int i = 0; i < col; i++) {
+    int align = row / blocksize * blocksize;
+    for (int j = 0; j < row; j += blocksize) {
+      int bs = j < align ? blocksize : row - align;
+      float scale = FLT_MIN;
+      for (int ij = 0; ij < bs; ij++) scale = smax(scale, fabsf(src[(size_t)(j + ij) * ld_src + i]));
+      if (e8m0) {
+        if (scale == 0) scale += fabsf(FLT_MIN);
+        scale = floorf(log2f(scale));
+        float emax = (float)pow(2, f8_ebits(t) - 1);
+        if (t == ORC_F8_E5M2) emax -= 1;
+        scale -= emax;
+        const float scale_max = (float)pow(2, 7) - 1;
+        scale = scale < (-1 * scale_max) ? (-1 * scale_max) : scale;
+      } else {
+        scale /= f8_maxnorm(t);
+      }
+      scales[(size_t)(j / blocksize) * ld_dst + i] = scale;
+      for (int ij = 0; ij < bs; ij++)
+        dst[(size_t)(j + ij) * ld_dst + i] = orc_f8_quantize(t, src[(size_t)(j + ij) * ld_src + i], scale, e8m0);
     }
   }
 }

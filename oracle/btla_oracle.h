@@ -31,6 +31,9 @@ extern "C" {
 #define ORC_F4_E2M1 (4u)                 /* EleBits4 | TypeFloat          (bestla.h:82) */
 #define ORC_F4_BNB (4u | (1u << 16))     /* EleBits4 | TypeFloat | SubType1 */
 #define ORC_F4_NF4 (4u | (2u << 16))     /* EleBits4 | TypeFloat | SubType2 */
+#define ORC_F8_E4M3 (8u)                 /* EleBits8 | TypeFloat          (bestla.h:68-71) */
+#define ORC_F8_E5M2 (8u | (1u << 16))
+#define ORC_F8_E8M0 (8u | (3u << 16))    /* shared-exponent (mx) scale dtype */
 
 /* fp16/bf16 conversions (bestla/bestla/bestla_utils.h:116-229) */
 uint16_t orc_f32_to_bf16(float v);
@@ -134,6 +137,14 @@ float orc_f4_lut(int kind, int code);
 int8_t orc_f4_quantize(int kind, float x);
 void orc_quantize_f4_rowblock(const float* src, int8_t* dst, int row, int col, int ld_src, int ld_dst, float* scales,
                               int blocksize, int kind);
+
+
+/* NFloat 8-bit weights: kernel_ref.h:1721-1762 f8_mx_quantize, :984-1001 f8_to_fp32, :1764-1800
+   quantize_f32_f8_rowblock_mxscale (e8m0 != 0: F8_E8M0 scales, else F32) */
+int8_t orc_f8_quantize(uint32_t t, float v, float scale, int e8m0);
+float orc_f8_to_f32(uint32_t t, int8_t code);
+void orc_quantize_f8_rowblock(const float* src, int8_t* dst, int row, int col, int ld_src, int ld_dst, float* scales,
+                              int blocksize, uint32_t t, int e8m0);
 
 #ifdef __cplusplus
 }

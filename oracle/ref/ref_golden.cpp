@@ -340,6 +340,26 @@ static void case_f4(const char* cs, int row, int col, int bs, const float* lut) 
   dump(cs, "tree", "f4", tree.data(), 16);
 }
 
+// NFloat 8-bit: kernel_ref.h:1764-1800 quantize_f32_f8_rowblock_mxscale and :984-1001 f8_to_fp32 (all 256 codes)
+template <BTLA_DTYPE F8_T>
+static void case_f8(const char* cs, int row, int col, int bs, BTLA_DTYPE sdt, float amp) {
+  std::vector<float> src((size_t)row * col);
+  for (auto& v : src) v = urand(-amp, amp);
+  for (int r = 0; r < bs && r < row; r++) src[(size_t)r * col] = 0.f;  // an all-zero block
+  if (col > 1) src[1] = 1e-30f;                                        // an underflowing value
+  int nblk = (row + bs - 1) / bs;
+  std::vector<int8_t> q((size_t)row * col);
+  std::vector<float> s((size_t)nblk * col), dec(256);
+  kernel::ref::quantize_f32_f8_rowblock_mxscale<F8_T>(src.data(), q.data(), row, col, col, col, s.data(), bs, sdt);
+  for (int c = 0; c < 256; c++) dec[c] = kernel::ref::f8_to_fp32(utils::f8((int8_t)c), F8_T);
+  int meta[4] = {row, col, bs, sdt == BTLA_DTYPE::F8_E8M0 ? 1 : 0};
+  dump(cs, "meta", "i4", meta, 4);
+  dump(cs, "src", "f4", src.data(), src.size());
+  dump(cs, "q", "i1", q.data(), q.size());
+  dump(cs, "s", "f4", s.data(), s.size());
+  dump(cs, "dec", "f4", dec.data(), 256);
+}
+
 int main(int argc, char** argv) {
   if (argc < 2) {
     fprintf(stderr, "usage: %s <outdir>\n", argv[0]);
@@ -389,6 +409,10 @@ int main(int argc, char** argv) {
   case_f4<BTLA_DTYPE::F4_E2M1>("f4_e2m1_g64", 192, 13, 64, fp4_e2m1_dequant_fp32_LUT);
   case_f4<BTLA_DTYPE::F4_NF4>("f4_nf4_g32", 128, 17, 32, nf4_dequant_fp32_LUT);
   case_f4<BTLA_DTYPE::F4_NF4>("f4_nf4_perchannel", 100, 7, 100, nf4_dequant_fp32_LUT);
+  case_f8<BTLA_DTYPE::F8_E4M3>("f8_e4m3_e8m0_g32", 128, 11, 32, BTLA_DTYPE::F8_E8M0, 3.f);
+  case_f8<BTLA_DTYPE::F8_E5M2>("f8_e5m2_e8m0_g64", 128, 9, 64, BTLA_DTYPE::F8_E8M0, 100.f);
+  case_f8<BTLA_DTYPE::F8_E4M3>("f8_e4m3_f32_g32", 96, 7, 32, BTLA_DTYPE::F32, 0.5f);
+  case_f8<BTLA_DTYPE::F8_E5M2>("f8_e5m2_f32_g128", 256, 5, 128, BTLA_DTYPE::F32, 1.f);
   fclose(g_man);
   return 0;
 }

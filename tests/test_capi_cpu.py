@@ -6,7 +6,7 @@ import numpy as np
 import pytest
 
 from neural_amd import _lib, bestla
-from tests.oracle_lib import F32, BF16, F16, F4_BNB, F4_E2M1, F4_NF4, S2, S3, S4, S5, S6, S7, S8
+from tests.oracle_lib import F32, BF16, F16, F4_BNB, F4_E2M1, F4_NF4, F8_E4M3, F8_E5M2, F8_E8M0, S2, S3, S4, S5, S6, S7, S8
 
 
 def test_library_exports_every_header_symbol():
@@ -43,6 +43,10 @@ CFGS = [
     (64, 256, 32, F4_NF4, F32, False, bestla.COMP_F32),  # NFloat (prologue WeightKBlockNFloat): no zp / reduce
     (50, 256, 64, F4_E2M1, BF16, False, bestla.COMP_BF16),
     (48, 128, 32, F4_BNB, F32, False, bestla.COMP_INT8),  # int8 compute falls through to a float core
+    (64, 256, 32, F8_E4M3, F8_E8M0, False, bestla.COMP_F32),  # fp8: shared-exponent (E8M0) scales
+    (50, 200, 64, F8_E5M2, F8_E8M0, False, bestla.COMP_BF16),
+    (48, 256, 32, F8_E4M3, F32, False, bestla.COMP_F32),      # fp8 with fp32 scales (pack API only)
+    (40, 256, 128, F8_E5M2, F32, False, bestla.COMP_INT8),
 ]
 
 
@@ -52,10 +56,15 @@ def test_quant_pack_bit_exact_vs_oracle(oracle, cfg):
     rng = np.random.default_rng(n * 1000 + k)
     W = rng.uniform(-0.5, 0.5, size=(n, k)).astype(np.float32)
     W[0, :bs] = 0.0  # an all-zero block
-    blob = bestla.quantize(W, group_size=bs, weight_dtype={S4: "int4", S2: "int2", S8: "int8", S3: "int3", S5: "int5", S6: "int6",
+    if qt in (F8_E4M3, F8_E5M2):
+        W[1, 1:bs:2] *= np.float32(1e-6)  # tiny next to the block max: codes with exponent field 0
+    if qt in (F8_E4M3, F8_E5M2) and st == F32:
+        blob = bestla.quant_pack(W, bs, qt, st, asym, comp)
+    else:
+        blob = bestla.quantize(W, group_size=bs, weight_dtype={S4: "int4", S2: "int2", S8: "int8", S3: "int3", S5: "int5", S6: "int6",
                                                            S7: "int7", F4_NF4: "nf4", F4_E2M1: "fp4_e2m1",
-                                                           F4_BNB: "fp4_bnb"}[qt],
-                           scale_dtype={F32: "fp32", BF16: "bf16", F16: "fp16"}[st],
+                                                           F4_BNB: "fp4_bnb", F8_E4M3: "fp8_e4m3", F8_E5M2: "fp8_e5m2"}[qt],
+                           scale_dtype={F32: "fp32", BF16: "bf16", F16: "fp16", F8_E8M0: "fp8"}[st],
                            alg="asym" if asym else "sym",
                            compute_dtype={bestla.COMP_F32: "fp32", bestla.COMP_INT8: "int8", bestla.COMP_BF16: "bf16"}[comp])
     core = oracle.lib.orc_select_core(comp, qt, bs, int(asym), 0)
@@ -142,7 +151,9 @@ def test_unsupported_inputs_fail_loudly():
     assert L.nad_device_weight_size(bad.ctypes.data_as(C.c_void_p)) == 0
     assert "WeightKBlockNInteger" in _lib.last_error() or "corrupt" in _lib.last_error()
     with pytest.raises(ValueError):
-        bestla.quantize(np.zeros((16, 64), np.float32), 32, "fp8_e4m3")  # FP8 weights: not supported (loudly)
+        bestla.quantize(np.zeros((16, 64), np.float32), 32, "int1")  # S1 weights: not supported (loudly)
+    with pytest.raises(RuntimeError):  # F8_E8M0 scales with integer weights: rejected by the pack API
+        bestla.quant_pack(np.zeros((16, 64), np.float32), 32, S4, F8_E8M0, False, bestla.COMP_F32)
 
 
 def test_qpack_gptq3_bit_exact(oracle):

@@ -242,3 +242,20 @@ def test_f4_quantizer_and_lut_bit_exact(oracle, case, kind):
     assert np.array_equal(q.ravel(), g["q"]) and np.array_equal(s.ravel().view(np.uint32), g["s"].view(np.uint32))
     deq = lut[q.astype(np.int64) & 15] * np.repeat(s, bs, axis=0)[:row]
     assert np.array_equal(deq.ravel().view(np.uint32), g["deq"].view(np.uint32))
+
+
+@pytest.mark.parametrize("case,t", [("f8_e4m3_e8m0_g32", 8), ("f8_e5m2_e8m0_g64", 8 | (1 << 16)),
+                                    ("f8_e4m3_f32_g32", 8), ("f8_e5m2_f32_g128", 8 | (1 << 16))])
+def test_f8_quantizer_and_decode_bit_exact(oracle, case, t):
+    """NFloat 8-bit: f8_mx_quantize / quantize_f32_f8_rowblock_mxscale (e8m0 and f32 scales) and f8_to_fp32 for all
+    256 codes, against the reference's own outputs"""
+    g = G[case]
+    row, col, bs, e8m0 = (int(v) for v in g["meta"])
+    dec = np.array([oracle.lib.orc_f8_to_f32(t, c - 256 if c > 127 else c) for c in range(256)], np.float32)
+    assert np.array_equal(dec.view(np.uint32), g["dec"].view(np.uint32))
+    q = np.zeros((row, col), np.int8)
+    s = np.zeros((-(-row // bs), col), np.float32)
+    src = np.ascontiguousarray(g["src"].reshape(row, col))
+    oracle.lib.orc_quantize_f8_rowblock(src.ctypes.data, q.ctypes.data, row, col, col, col, s.ctypes.data, bs, t, e8m0)
+    assert np.array_equal(s.ravel().view(np.uint32), g["s"].view(np.uint32))
+    assert np.array_equal(q.ravel(), g["q"])
