@@ -381,6 +381,9 @@ static int prepare_gemv(GemvArgs& a, int& waves, int& grid, int& gpt_out, const 
   a.dq_mask = 0x000F000Fu;
   a.dq_magic = 0x64006400u;
   a.pre_stages = std::min(3, std::max(1, env_int("NAD_GEMV_PRE", 1)));
+  a.u_q = a.units / grid;
+  a.u_r = a.units % grid;
+  a.lean = env_int("NAD_GEMV_LEAN", 1);
   const size_t lds = gemv_lds_layout(a, w0.bits, waves, grid);
   if (lds > 160 * 1024) return 0;
   // buffer-resource offsets are 32-bit: every tile array, scale array and the activations must stay below 2 GiB

@@ -117,6 +117,9 @@ struct StageRegs {
   int zp[KS][GPT];
 };
 
+#ifndef NAD_TILE_AUX
+#define NAD_TILE_AUX 2  // non-temporal: the weights are read once per token
+#endif
 // Issue one stage's loads (never predicated: past-the-end tiles / stages get the out-of-range offset), then advance.
 template <int GPT, bool ASYM>
 __device__ __forceinline__ void load_stage(const GemvArgs& a, StageRegs<GPT>& S, StageCursor& c, int nv, int nsl,
@@ -124,7 +127,7 @@ __device__ __forceinline__ void load_stage(const GemvArgs& a, StageRegs<GPT>& S,
   if (c.j >= nv) {  // past this wave's last stage: the same loads, all out of range, no bookkeeping
 #pragma unroll
     for (int i = 0; i < KS; i++) {
-      S.b[i] = __builtin_bit_cast(u4_t, __builtin_amdgcn_raw_buffer_load_b128(c.rt, kOOB, 0, 2));
+      S.b[i] = __builtin_bit_cast(u4_t, __builtin_amdgcn_raw_buffer_load_b128(c.rt, kOOB, 0, NAD_TILE_AUX));
 #pragma unroll
       for (int g = 0; g < GPT; g++) {
         S.sc[i][g] = __builtin_amdgcn_raw_buffer_load_b32(c.rs, kOOB, 0, 0);
@@ -141,7 +144,7 @@ __device__ __forceinline__ void load_stage(const GemvArgs& a, StageRegs<GPT>& S,
 #pragma unroll
   for (int i = 0; i < KS; i++) {
     const bool live = !over && t0 + i < nt;
-    S.b[i] = __builtin_bit_cast(u4_t, __builtin_amdgcn_raw_buffer_load_b128(c.rt, (live ? tb + i * 1024 : kOOB) + lane * 16, 0, 2));
+    S.b[i] = __builtin_bit_cast(u4_t, __builtin_amdgcn_raw_buffer_load_b128(c.rt, (live ? tb + i * 1024 : kOOB) + lane * 16, 0, NAD_TILE_AUX));
 #pragma unroll
     for (int g = 0; g < GPT; g++) {
       const int grp = GPT == 1 ? ((t0 + i) >> a.tpg_shift) : (t0 + i) * GPT + g;
@@ -300,6 +303,16 @@ __global__ __launch_bounds__(gemv_max_threads<GPT>()) void woq_gemv_kernel(GemvA
   const int R = HILO == 0 ? M : 2 * M;
   const int nsl = (nt + KS - 1) / KS;  // K-slices per stripe
   NAD_TRACE(0);
+#ifdef NAD_EXP_KPREF
+  {  // touch every 64-B line of the argument block in one batch so the later scalar loads hit
+    const __attribute__((address_space(4))) uint32_t* kp =
+        (const __attribute__((address_space(4))) uint32_t*)__builtin_amdgcn_kernarg_segment_ptr();
+    uint32_t s = 0;
+#pragma unroll
+    for (int i = 0; i < int(sizeof(GemvArgs) + 63) / 64; i++) s ^= kp[i * 16];
+    asm volatile("; kpref %0" ::"s"(s));
+  }
+#endif
 
   // this workgroup's units (wave-uniform)
   const int G = gridDim.x, bid = blockIdx.x;
@@ -534,11 +547,234 @@ __global__ __launch_bounds__(gemv_max_threads<GPT>()) void woq_gemv_kernel(GemvA
   NAD_TRACE(3);
 }
 
+// ------------------------------------------------------------------------------------------------ M = 1 variant
+// Every launch pays its executed code again (the instruction cache starts cold per dispatch: ~0.45 us per KB at 8
+// waves per CU, tools/ifetch_probe.hip), and a decode matmul at K = 4096 streams one stripe per workgroup -- so the
+// executed instruction bytes ARE the fixed cost.  This variant of the stream for M = 1, int4, one group per tile keeps
+// that path short: the activation type is a template parameter, the workgroup's unit range comes from host-divided
+// counts (no integer division), and each wave stages only ITS K-slices of the activations into its own LDS rows
+// (hi / lo fp16, plus a zero row for the MFMA rows M = 1 leaves empty), so nothing waits on a block-wide barrier before
+// the stream; the one barrier is the final cross-wave reduction.
+constexpr int kLeanSpw = 2;                       // K-slices per wave it stages (K <= waves * 2 * 512)
+constexpr int kLeanWaveLds = 1024 + kLeanSpw * 2048;  // zero row + per slice {hi, lo} 512 fp16 each
+
+static bool lean_ok(const GemvArgs& a, int bits, int waves) {
+  int tpg = 0;
+  const int nsl = (a.nt + KS - 1) / KS;
+  return a.lean && a.M == 1 && bits == 4 && a.a_fast && gemv_groups_per_tile(4, a.nt, a.ng, a.bs, &tpg) == 1 &&
+         nsl <= waves * kLeanSpw;
+}
+
+template <int AT, bool ASYM>
+__global__ __launch_bounds__(1024) void woq_gemv_m1_kernel(GemvArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int KT = 128, SPT = KT / 32;
+  constexpr int ESZ = AT == kActF32 ? 4 : 2;
+  constexpr bool HL = AT != kActF16;  // fp32 / bf16 rows split into fp16 hi + lo (MFMA rows 0 and 8)
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));
+  const int NW = __builtin_amdgcn_readfirstlane(int(blockDim.x >> 6));
+  const int nt = a.nt;
+  const int nsl = (nt + KS - 1) / KS;
+  NAD_TRACE(0);
+  const int bid = blockIdx.x;
+  const int u0 = bid * a.u_q + min(bid, a.u_r);
+  const int u1 = u0 + a.u_q + (bid < a.u_r ? 1 : 0);
+  const int vpu = a.dual ? 2 : 1;
+  const int v0 = u0 * vpu, nv = (u1 - u0) * vpu;
+  const bool idle = wave >= nsl;
+  float* part = reinterpret_cast<float*>(smem + a.part_off);  // [nv][NW][16]
+
+  // 1) this wave's activation slices (q = wave + j NW), then the first weight stage
+  const auto ra = rsrc(a.A, a.K * ESZ);
+  uint4 x[kLeanSpw][2];
+#pragma unroll
+  for (int j = 0; j < kLeanSpw; j++) {
+    const int q = wave + j * NW, k = q * (KS * KT) + lane * 8;
+    const int off = (q < nsl && k < a.K) ? k * ESZ : kOOB;
+    x[j][0] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(ra, off, 0, 0));
+    if constexpr (ESZ == 4) x[j][1] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(ra, off + 16, 0, 0));
+  }
+  const int vs = a.scale_t == kScaleF32 ? (lane & 15) * 4 : (lane & 14) * 2;
+  StageCursor lc;
+  lc.j = idle ? nv : 0;
+  lc.q = wave;
+  lc.s = 0;
+  lc.rt = rsrc(a.w[0].tiles, 0);
+  lc.rs = lc.rt;
+  lc.rz = lc.rt;
+  if (!idle && nv > 0) cursor_stripe(a, lc, v0);
+  StageRegs<1> S0, S1, S2;
+  load_stage<1, ASYM>(a, S0, lc, nv, nsl, wave, NW, v0, lane, vs);
+  NAD_TRACE(4);
+
+  // 2) stage the slices into this wave's rows (LDS ops of one wave complete in order: no barrier)
+  char* wrow = smem + wave * kLeanWaveLds;
+  *reinterpret_cast<uint4*>(wrow + lane * 16) = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+  for (int j = 0; j < kLeanSpw; j++) {
+    h8_t hi, lo;
+    if constexpr (AT == kActF16) {
+      hi = __builtin_bit_cast(h8_t, x[j][0]);
+    } else {
+      float f[8];
+      unit_to_f32(AT, x[j][0], x[j][1], f);
+#pragma unroll
+      for (int e = 0; e < 8; e++) {
+        hi[e] = _Float16(f[e]);
+        lo[e] = _Float16(f[e] - float(hi[e]));
+      }
+    }
+    *reinterpret_cast<h8_t*>(wrow + 1024 + j * 2048 + lane * 16) = hi;
+    if constexpr (HL) *reinterpret_cast<h8_t*>(wrow + 2048 + j * 2048 + lane * 16) = lo;
+  }
+  load_stage<1, ASYM>(a, S1, lc, nv, nsl, wave, NW, v0, lane, vs);
+  load_stage<1, ASYM>(a, S2, lc, nv, nsl, wave, NW, v0, lane, vs);
+  NAD_TRACE(1);
+
+  // 3) the stream: MFMA row 0 = hi (lane m 0), row 8 = lo (lane m 8), every other row reads the zero row
+  const int m = lane & 15, kq = lane >> 4;
+  const bool isrow = m == 0 || (HL && m == 8);
+  const char* abase = wrow + (isrow ? (m == 0 ? 1024 : 2048) : 0) + kq * 16;
+  const int slice_step = isrow ? 2048 : 0;
+  const int ssh = a.scale_t == kScaleF32 ? 0 : (lane & 1) * 16;
+  Dq4 dq;
+  dq.m0 = __builtin_amdgcn_readfirstlane(a.dq_mask);
+  dq.m1 = dq.m0 << 4;
+  dq.mag = __builtin_amdgcn_readfirstlane(a.dq_magic);
+  dq.s16 = splat(1.f / 16.f);
+  const h2_t zc0 = splat(-(1024.f + 8.f)), zc1 = splat(-(64.f + 8.f));
+
+  f4_t acc = {0.f, 0.f, 0.f, 0.f};
+  int cj = idle ? nv : 0, cq = wave, cs = 0;  // compute cursor: local stripe, K-slice, slice ordinal of this wave
+
+  auto compute_stage = [&](const StageRegs<1>& S) {
+    if (cj >= nv) return;
+    const char* ab = abase + cs * slice_step;
+    f4_t accg[KS];
+#pragma unroll
+    for (int d = 0; d < SPT; d++) {
+#pragma unroll
+      for (int i = 0; i < KS; i++) {
+        h8_t bf;
+        if constexpr (ASYM) {
+          const float z = float(S.zp[i][0]);
+          bf = dequant4(S.b[i][d], dq, zc0 - splat(z), zc1 - splat(z));
+        } else {
+          bf = dequant4(S.b[i][d], dq, zc0, zc1);
+        }
+        const h8_t af = *reinterpret_cast<const h8_t*>(ab + i * KT * 2 + d * 64);
+        accg[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, bf, d == 0 ? f4_t{0.f, 0.f, 0.f, 0.f} : accg[i], 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < KS; i++) acc += accg[i] * scale_bits_to_f32(S.sc[i][0], a.scale_t, ssh);
+    cq += NW;
+    cs++;
+    if (cq >= nsl) {  // this wave's last slice of stripe cj: publish its partial (row 0 + row 8 = hi + lo)
+      float r = acc[0];
+      if constexpr (HL) r += __shfl_down(r, 32, 64);
+      if (lane < 16) part[(size_t(cj) * NW + wave) * 16 + lane] = r;
+      acc = f4_t{0.f, 0.f, 0.f, 0.f};
+      cq = wave;
+      cs = 0;
+      cj++;
+    }
+  };
+
+  while (cj < nv) {
+    compute_stage(S0);
+    load_stage<1, ASYM>(a, S0, lc, nv, nsl, wave, NW, v0, lane, vs);
+    compute_stage(S1);
+    load_stage<1, ASYM>(a, S1, lc, nv, nsl, wave, NW, v0, lane, vs);
+    compute_stage(S2);
+    load_stage<1, ASYM>(a, S2, lc, nv, nsl, wave, NW, v0, lane, vs);
+  }
+  NAD_TRACE_MAX(2);
+  __syncthreads();
+
+  // 4) sum each stripe's wave slots in wave order and apply the epilogue
+  const int nout = (u1 - u0) * 16;
+  const int nwl = min(NW, nsl);
+  for (int o = threadIdx.x; o < nout; o += blockDim.x) {
+    const int p = o >> 4, nn = o & 15;
+    float y[2] = {0.f, 0.f};
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      if (h < vpu) {
+        const float* ps = part + size_t(p * vpu + h) * NW * 16 + nn;
+        float s0 = 0.f, s1 = 0.f;
+        int w = 0;
+        for (; w + 1 < nwl; w += 2) {
+          s0 += ps[w * 16];
+          s1 += ps[(w + 1) * 16];
+        }
+        if (w < nwl) s0 += ps[w * 16];
+        y[h] = s0 + s1;
+      }
+    }
+    int wsel, s;
+    vstripe(a, v0 + p * vpu, wsel, s);
+    if (a.dual) wsel = 0;
+    const int n = s * 16 + nn;
+    if (n >= sel3(wsel, a.w[0].n, a.w[1].n, a.w[2].n)) continue;
+    float* out = sel3(wsel, a.w[0].out, a.w[1].out, a.w[2].out);
+    float v = y[0];
+    switch (a.epi) {
+      case kEpiBias:
+        v += a.w[0].bias[n];
+        break;
+      case kEpiAddGelu:
+        v = gelu_f(v + a.w[0].bias[n]);
+        break;
+      case kEpiGelu:
+        v = gelu_f(v);
+        break;
+      case kEpiSilu:
+        v = silu_f(v);
+        break;
+      case kEpiResAdd:
+        v += a.res[n];
+        break;
+      case kEpiSiluMul: {
+        const float t1 = silu_f(y[0]);
+        if (a.aux) a.aux[n] = t1;
+        v = t1 * y[1];
+        break;
+      }
+      case kEpiGeluMul: {
+        const float t1 = gelu_f(y[0]);
+        if (a.aux) a.aux[n] = t1;
+        v = t1 * y[1];
+        break;
+      }
+      default:
+        break;
+    }
+    out[n] = v;
+  }
+  NAD_TRACE(3);
+}
+
 // ------------------------------------------------------------------------------------------------ launcher
 template <int BITS, int HILO, int GPT, bool ASYM>
 static hipError_t gemv_launch4(const GemvArgs& a, dim3 g, dim3 b, size_t lds, hipStream_t st) {
   auto k = woq_gemv_kernel<BITS, HILO, GPT, ASYM>;
   static bool attr_set = false;  // opt in to > 64 KiB of dynamic LDS once per instantiation
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       160 * 1024);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(k, g, b, lds, st, a);
+  return hipGetLastError();
+}
+
+template <int AT, bool ASYM>
+static hipError_t gemv_m1_launch(const GemvArgs& a, dim3 g, dim3 b, size_t lds, hipStream_t st) {
+  auto k = woq_gemv_m1_kernel<AT, ASYM>;
+  static bool attr_set = false;
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
                                        160 * 1024);
@@ -575,6 +811,11 @@ static hipError_t gemv_launch1(const GemvArgs& a, int hilo, int gpt, dim3 g, dim
 
 // LDS layout (and its size) of one launch: activation rows, then the partial-sum slots [nv][waves][M][16]
 size_t gemv_lds_layout(GemvArgs& a, int bits, int waves, int grid) {
+  if (lean_ok(a, bits, waves)) {  // woq_gemv_m1_kernel: per-wave rows, then the partial slots [nv][waves][16]
+    const int upw = (a.units + grid - 1) / grid;
+    a.part_off = waves * kLeanWaveLds;
+    return size_t(a.part_off) + size_t(upw) * (a.dual ? 2 : 1) * waves * 16 * 4;
+  }
   const int KT = bits == 4 ? 128 : (bits == 2 ? 256 : 64);
   const int R = a.act_t == kActF16 ? a.M : 2 * a.M;
   const size_t kp = size_t(a.nt) * KT;
@@ -619,6 +860,14 @@ hipError_t launch_gemv(const GemvArgs& a, int bits, int waves, int grid, size_t 
   const int gpt = gemv_groups_per_tile(bits, a.nt, a.ng, a.bs, &tpg);
   if (gpt == 0) return hipErrorInvalidValue;
   dim3 g(grid), b(waves * 64);
+  if (lean_ok(a, bits, waves)) {
+    if (a.act_t == kActF32) return a.asym ? gemv_m1_launch<kActF32, true>(a, g, b, lds, stream)
+                                          : gemv_m1_launch<kActF32, false>(a, g, b, lds, stream);
+    if (a.act_t == kActF16) return a.asym ? gemv_m1_launch<kActF16, true>(a, g, b, lds, stream)
+                                          : gemv_m1_launch<kActF16, false>(a, g, b, lds, stream);
+    return a.asym ? gemv_m1_launch<kActBF16, true>(a, g, b, lds, stream)
+                  : gemv_m1_launch<kActBF16, false>(a, g, b, lds, stream);
+  }
   if (bits == 4) return gemv_launch1<4>(a, hilo, gpt, g, b, lds, stream);
   if (bits == 2) return gemv_launch1<2>(a, hilo, gpt, g, b, lds, stream);
   return gemv_launch1<8>(a, hilo, gpt, g, b, lds, stream);

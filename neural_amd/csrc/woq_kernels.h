@@ -105,6 +105,8 @@ struct GemvArgs {
   int norm;             // woq_chain: RMS-normalise each activation row while staging (x / rms(x) * norm_w)
   float norm_eps;
   const float* norm_w;  //   optional per-k weight (null = 1)
+  int u_q, u_r;         // units per workgroup: u_q, one more for the first u_r workgroups (host-divided)
+  int lean;             // M = 1 int4 single-group-per-tile launches may take woq_gemv_m1_kernel (NAD_GEMV_LEAN)
   SkinnyWeight w[3];
 };
 
