@@ -701,16 +701,18 @@ __global__ __launch_bounds__(1024) void woq_gemv_m1_kernel(GemvArgs a) {
     float y[2] = {0.f, 0.f};
 #pragma unroll
     for (int h = 0; h < 2; h++) {
-      if (h < vpu) {
+      if (h < vpu) {  // all slots read at once (one LDS round trip), summed in a fixed tree order
         const float* ps = part + size_t(p * vpu + h) * NW * 16 + nn;
-        float s0 = 0.f, s1 = 0.f;
-        int w = 0;
-        for (; w + 1 < nwl; w += 2) {
-          s0 += ps[w * 16];
-          s1 += ps[(w + 1) * 16];
-        }
-        if (w < nwl) s0 += ps[w * 16];
-        y[h] = s0 + s1;
+        float t[16];
+#pragma unroll
+        for (int w = 0; w < 16; w++) t[w] = ps[min(w, nwl - 1) * 16];
+#pragma unroll
+        for (int w = 0; w < 16; w++) t[w] = w < nwl ? t[w] : 0.f;
+#pragma unroll
+        for (int st = 8; st >= 1; st >>= 1)
+#pragma unroll
+          for (int w = 0; w < st; w++) t[w] += t[w + st];
+        y[h] = t[0];
       }
     }
     int wsel, s;
