@@ -701,18 +701,25 @@ __global__ __launch_bounds__(1024) void woq_gemv_m1_kernel(GemvArgs a) {
     float y[2] = {0.f, 0.f};
 #pragma unroll
     for (int h = 0; h < 2; h++) {
-      if (h < vpu) {  // all slots read at once (one LDS round trip), summed in a fixed tree order
+      if (h < vpu) {  // all slots read at once (one LDS round trip), summed in the general kernel's order
         const float* ps = part + size_t(p * vpu + h) * NW * 16 + nn;
         float t[16];
 #pragma unroll
         for (int w = 0; w < 16; w++) t[w] = ps[min(w, nwl - 1) * 16];
+        const int full = nwl & ~3;
+        float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
 #pragma unroll
-        for (int w = 0; w < 16; w++) t[w] = w < nwl ? t[w] : 0.f;
+        for (int w = 0; w < 16; w += 4)
+          if (w < full) {
+            s0 += t[w];
+            s1 += t[w + 1];
+            s2 += t[w + 2];
+            s3 += t[w + 3];
+          }
 #pragma unroll
-        for (int st = 8; st >= 1; st >>= 1)
-#pragma unroll
-          for (int w = 0; w < st; w++) t[w] += t[w + st];
-        y[h] = t[0];
+        for (int w = 0; w < 16; w++)
+          if (w >= full && w < nwl) s0 += t[w];
+        y[h] = (s0 + s1) + (s2 + s3);
       }
     }
     int wsel, s;
