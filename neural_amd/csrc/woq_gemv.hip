@@ -550,25 +550,31 @@ __global__ __launch_bounds__(gemv_max_threads<GPT>()) void woq_gemv_kernel(GemvA
 // ------------------------------------------------------------------------------------------------ M = 1 variant
 // Every launch pays its executed code again (the instruction cache starts cold per dispatch: ~0.45 us per KB at 8
 // waves per CU, tools/ifetch_probe.hip), and a decode matmul at K = 4096 streams one stripe per workgroup -- so the
-// executed instruction bytes ARE the fixed cost.  This variant of the stream for M = 1, int4, one group per tile keeps
-// that path short: the activation type is a template parameter, the workgroup's unit range comes from host-divided
+// executed instruction bytes ARE the fixed cost.  This variant of the stream for M = 1 (int4 / int2, groups of a whole
+// tile or a power-of-two part of one) keeps that path short: the activation type is a template parameter, the workgroup's unit range comes from host-divided
 // counts (no integer division), and each wave stages only ITS K-slices of the activations into its own LDS rows
 // (hi / lo fp16, plus a zero row for the MFMA rows M = 1 leaves empty), so nothing waits on a block-wide barrier before
 // the stream; the one barrier is the final cross-wave reduction.
-constexpr int kLeanSpw = 2;                       // K-slices per wave it stages (K <= waves * 2 * 512)
-constexpr int kLeanWaveLds = 1024 + kLeanSpw * 2048;  // zero row + per slice {hi, lo} 512 fp16 each
+constexpr int kLeanSpw = 2;  // K-slices per wave it stages (K <= waves * 2 * KS * KT)
+// per wave: a zero row, then per slice {hi, lo} rows of KS * KT fp16 each
+constexpr int lean_row_bytes(int bits) { return KS * (bits == 4 ? 128 : 256) * 2; }
+constexpr int lean_wave_lds(int bits) { return lean_row_bytes(bits) * (1 + 2 * kLeanSpw); }
 
 static bool lean_ok(const GemvArgs& a, int bits, int waves) {
   int tpg = 0;
   const int nsl = (a.nt + KS - 1) / KS;
-  return a.lean && a.M == 1 && bits == 4 && a.a_fast && gemv_groups_per_tile(4, a.nt, a.ng, a.bs, &tpg) == 1 &&
-         nsl <= waves * kLeanSpw;
+  const int gpt = gemv_groups_per_tile(bits, a.nt, a.ng, a.bs, &tpg);
+  const bool inst = bits == 4 ? (gpt == 1 || gpt == 2) : (bits == 2 && (gpt == 1 || gpt == 2 || (gpt == 4 && !a.asym)));
+  return a.lean && a.M == 1 && inst && a.a_fast && nsl <= waves * kLeanSpw;
 }
 
-template <int AT, bool ASYM>
-__global__ __launch_bounds__(1024) void woq_gemv_m1_kernel(GemvArgs a) {
+template <int BITS, int GPT, int AT, bool ASYM>
+__global__ __launch_bounds__(gemv_max_threads<GPT>()) void woq_gemv_m1_kernel(GemvArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int KT = 128, SPT = KT / 32;
+  constexpr int KT = BITS == 4 ? 128 : 256, SPT = KT / 32, SPG = SPT / GPT;
+  constexpr int RB = lean_row_bytes(BITS);  // one fp16 row of a slice
+  constexpr int UPL = KS * KT / 8 / 64;      // 8-element staging units per lane per slice
+  constexpr int BIAS = BITS == 4 ? 8 : 2;
   constexpr int ESZ = AT == kActF32 ? 4 : 2;
   constexpr bool HL = AT != kActF16;  // fp32 / bf16 rows split into fp16 hi + lo (MFMA rows 0 and 8)
   const int lane = threadIdx.x & 63;
@@ -587,10 +593,10 @@ __global__ __launch_bounds__(1024) void woq_gemv_m1_kernel(GemvArgs a) {
 
   // 1) this wave's activation slices (q = wave + j NW), then the first weight stage
   const auto ra = rsrc(a.A, a.K * ESZ);
-  uint4 x[kLeanSpw][2];
+  uint4 x[kLeanSpw * UPL][2];
 #pragma unroll
-  for (int j = 0; j < kLeanSpw; j++) {
-    const int q = wave + j * NW, k = q * (KS * KT) + lane * 8;
+  for (int j = 0; j < kLeanSpw * UPL; j++) {
+    const int q = wave + (j / UPL) * NW, k = q * (KS * KT) + ((j % UPL) * 64 + lane) * 8;
     const int off = (q < nsl && k < a.K) ? k * ESZ : kOOB;
     x[j][0] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(ra, off, 0, 0));
     if constexpr (ESZ == 4) x[j][1] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(ra, off + 16, 0, 0));
@@ -604,15 +610,16 @@ __global__ __launch_bounds__(1024) void woq_gemv_m1_kernel(GemvArgs a) {
   lc.rs = lc.rt;
   lc.rz = lc.rt;
   if (!idle && nv > 0) cursor_stripe(a, lc, v0);
-  StageRegs<1> S0, S1, S2;
-  load_stage<1, ASYM>(a, S0, lc, nv, nsl, wave, NW, v0, lane, vs);
+  StageRegs<GPT> S0, S1, S2;
+  load_stage<GPT, ASYM>(a, S0, lc, nv, nsl, wave, NW, v0, lane, vs);
   NAD_TRACE(4);
 
   // 2) stage the slices into this wave's rows (LDS ops of one wave complete in order: no barrier)
-  char* wrow = smem + wave * kLeanWaveLds;
-  *reinterpret_cast<uint4*>(wrow + lane * 16) = make_uint4(0u, 0u, 0u, 0u);
+  char* wrow = smem + wave * lean_wave_lds(BITS);
 #pragma unroll
-  for (int j = 0; j < kLeanSpw; j++) {
+  for (int u = 0; u < UPL; u++) *reinterpret_cast<uint4*>(wrow + (u * 64 + lane) * 16) = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+  for (int j = 0; j < kLeanSpw * UPL; j++) {
     h8_t hi, lo;
     if constexpr (AT == kActF16) {
       hi = __builtin_bit_cast(h8_t, x[j][0]);
@@ -625,50 +632,59 @@ __global__ __launch_bounds__(1024) void woq_gemv_m1_kernel(GemvArgs a) {
         lo[e] = _Float16(f[e] - float(hi[e]));
       }
     }
-    *reinterpret_cast<h8_t*>(wrow + 1024 + j * 2048 + lane * 16) = hi;
-    if constexpr (HL) *reinterpret_cast<h8_t*>(wrow + 2048 + j * 2048 + lane * 16) = lo;
+    char* row = wrow + RB + (j / UPL) * 2 * RB + ((j % UPL) * 64 + lane) * 16;
+    *reinterpret_cast<h8_t*>(row) = hi;
+    if constexpr (HL) *reinterpret_cast<h8_t*>(row + RB) = lo;
   }
-  load_stage<1, ASYM>(a, S1, lc, nv, nsl, wave, NW, v0, lane, vs);
-  load_stage<1, ASYM>(a, S2, lc, nv, nsl, wave, NW, v0, lane, vs);
+  load_stage<GPT, ASYM>(a, S1, lc, nv, nsl, wave, NW, v0, lane, vs);
+  load_stage<GPT, ASYM>(a, S2, lc, nv, nsl, wave, NW, v0, lane, vs);
   NAD_TRACE(1);
 
   // 3) the stream: MFMA row 0 = hi (lane m 0), row 8 = lo (lane m 8), every other row reads the zero row
   const int m = lane & 15, kq = lane >> 4;
   const bool isrow = m == 0 || (HL && m == 8);
-  const char* abase = wrow + (isrow ? (m == 0 ? 1024 : 2048) : 0) + kq * 16;
-  const int slice_step = isrow ? 2048 : 0;
+  const char* abase = wrow + (isrow ? (m == 0 ? RB : 2 * RB) : 0) + kq * 16;
+  const int slice_step = isrow ? 2 * RB : 0;
   const int ssh = a.scale_t == kScaleF32 ? 0 : (lane & 1) * 16;
   Dq4 dq;
   dq.m0 = __builtin_amdgcn_readfirstlane(a.dq_mask);
   dq.m1 = dq.m0 << 4;
   dq.mag = __builtin_amdgcn_readfirstlane(a.dq_magic);
   dq.s16 = splat(1.f / 16.f);
-  const h2_t zc0 = splat(-(1024.f + 8.f)), zc1 = splat(-(64.f + 8.f));
+  const h2_t zc0 = splat(-(1024.f + BIAS)), zc1 = splat(-(64.f + BIAS));
 
   f4_t acc = {0.f, 0.f, 0.f, 0.f};
   int cj = idle ? nv : 0, cq = wave, cs = 0;  // compute cursor: local stripe, K-slice, slice ordinal of this wave
 
-  auto compute_stage = [&](const StageRegs<1>& S) {
+  auto compute_stage = [&](const StageRegs<GPT>& S) {
     if (cj >= nv) return;
     const char* ab = abase + cs * slice_step;
     f4_t accg[KS];
 #pragma unroll
     for (int d = 0; d < SPT; d++) {
+      const int g = GPT == 1 ? 0 : d / SPG;
 #pragma unroll
       for (int i = 0; i < KS; i++) {
         h8_t bf;
-        if constexpr (ASYM) {
-          const float z = float(S.zp[i][0]);
-          bf = dequant4(S.b[i][d], dq, zc0 - splat(z), zc1 - splat(z));
+        if constexpr (BITS == 4) {
+          if constexpr (ASYM) {
+            const float z = float(S.zp[i][g]);
+            bf = dequant4(S.b[i][d], dq, zc0 - splat(z), zc1 - splat(z));
+          } else {
+            bf = dequant4(S.b[i][d], dq, zc0, zc1);
+          }
         } else {
-          bf = dequant4(S.b[i][d], dq, zc0, zc1);
+          bf = dequant_step<BITS>(S.b[i], d, zp_const(BIAS + S.zp[i][g]));
         }
         const h8_t af = *reinterpret_cast<const h8_t*>(ab + i * KT * 2 + d * 64);
-        accg[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, bf, d == 0 ? f4_t{0.f, 0.f, 0.f, 0.f} : accg[i], 0, 0, 0);
+        accg[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, bf, d % SPG == 0 ? f4_t{0.f, 0.f, 0.f, 0.f} : accg[i], 0,
+                                                         0, 0);
+      }
+      if ((d + 1) % SPG == 0) {  // group end: scale each tile's group partial into the stripe sum, in tile order
+#pragma unroll
+        for (int i = 0; i < KS; i++) acc += accg[i] * scale_bits_to_f32(S.sc[i][g], a.scale_t, ssh);
       }
     }
-#pragma unroll
-    for (int i = 0; i < KS; i++) acc += accg[i] * scale_bits_to_f32(S.sc[i][0], a.scale_t, ssh);
     cq += NW;
     cs++;
     if (cq >= nsl) {  // this wave's last slice of stripe cj: publish its partial (row 0 + row 8 = hi + lo)
@@ -684,11 +700,11 @@ __global__ __launch_bounds__(1024) void woq_gemv_m1_kernel(GemvArgs a) {
 
   while (cj < nv) {
     compute_stage(S0);
-    load_stage<1, ASYM>(a, S0, lc, nv, nsl, wave, NW, v0, lane, vs);
+    load_stage<GPT, ASYM>(a, S0, lc, nv, nsl, wave, NW, v0, lane, vs);
     compute_stage(S1);
-    load_stage<1, ASYM>(a, S1, lc, nv, nsl, wave, NW, v0, lane, vs);
+    load_stage<GPT, ASYM>(a, S1, lc, nv, nsl, wave, NW, v0, lane, vs);
     compute_stage(S2);
-    load_stage<1, ASYM>(a, S2, lc, nv, nsl, wave, NW, v0, lane, vs);
+    load_stage<GPT, ASYM>(a, S2, lc, nv, nsl, wave, NW, v0, lane, vs);
   }
   NAD_TRACE_MAX(2);
   __syncthreads();
@@ -780,9 +796,9 @@ static hipError_t gemv_launch4(const GemvArgs& a, dim3 g, dim3 b, size_t lds, hi
   return hipGetLastError();
 }
 
-template <int AT, bool ASYM>
-static hipError_t gemv_m1_launch(const GemvArgs& a, dim3 g, dim3 b, size_t lds, hipStream_t st) {
-  auto k = woq_gemv_m1_kernel<AT, ASYM>;
+template <int BITS, int GPT, int AT, bool ASYM>
+static hipError_t gemv_m1_launch4(const GemvArgs& a, dim3 g, dim3 b, size_t lds, hipStream_t st) {
+  auto k = woq_gemv_m1_kernel<BITS, GPT, AT, ASYM>;
   static bool attr_set = false;
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -792,6 +808,29 @@ static hipError_t gemv_m1_launch(const GemvArgs& a, dim3 g, dim3 b, size_t lds, 
   }
   hipLaunchKernelGGL(k, g, b, lds, st, a);
   return hipGetLastError();
+}
+template <int BITS, int GPT>
+static hipError_t gemv_m1_launch2(const GemvArgs& a, dim3 g, dim3 b, size_t lds, hipStream_t st) {
+  if (a.act_t == kActF32) return a.asym ? gemv_m1_launch4<BITS, GPT, kActF32, true>(a, g, b, lds, st)
+                                        : gemv_m1_launch4<BITS, GPT, kActF32, false>(a, g, b, lds, st);
+  if (a.act_t == kActF16) return a.asym ? gemv_m1_launch4<BITS, GPT, kActF16, true>(a, g, b, lds, st)
+                                        : gemv_m1_launch4<BITS, GPT, kActF16, false>(a, g, b, lds, st);
+  return a.asym ? gemv_m1_launch4<BITS, GPT, kActBF16, true>(a, g, b, lds, st)
+                : gemv_m1_launch4<BITS, GPT, kActBF16, false>(a, g, b, lds, st);
+}
+// int4 / int2 with one group per tile or 2 per tile; int2 also 4 per tile (sym only, as the general kernel)
+static hipError_t gemv_m1_launch(const GemvArgs& a, int bits, int gpt, dim3 g, dim3 b, size_t lds, hipStream_t st) {
+  if (bits == 4) {
+    if (gpt == 1) return gemv_m1_launch2<4, 1>(a, g, b, lds, st);
+    if (gpt == 2) return gemv_m1_launch2<4, 2>(a, g, b, lds, st);
+  } else {
+    if (gpt == 1) return gemv_m1_launch2<2, 1>(a, g, b, lds, st);
+    if (gpt == 2) return gemv_m1_launch2<2, 2>(a, g, b, lds, st);
+    if (gpt == 4 && !a.asym) return a.act_t == kActF32 ? gemv_m1_launch4<2, 4, kActF32, false>(a, g, b, lds, st)
+                                   : (a.act_t == kActF16 ? gemv_m1_launch4<2, 4, kActF16, false>(a, g, b, lds, st)
+                                                         : gemv_m1_launch4<2, 4, kActBF16, false>(a, g, b, lds, st));
+  }
+  return hipErrorInvalidValue;
 }
 
 // Instantiated: groups of >= KT (GPT 1), KT/2 (GPT 2) and KT/4 (GPT 4), sym and asym.  Finer groups fall back to
@@ -822,7 +861,7 @@ static hipError_t gemv_launch1(const GemvArgs& a, int hilo, int gpt, dim3 g, dim
 size_t gemv_lds_layout(GemvArgs& a, int bits, int waves, int grid) {
   if (lean_ok(a, bits, waves)) {  // woq_gemv_m1_kernel: per-wave rows, then the partial slots [nv][waves][16]
     const int upw = (a.units + grid - 1) / grid;
-    a.part_off = waves * kLeanWaveLds;
+    a.part_off = waves * lean_wave_lds(bits);
     return size_t(a.part_off) + size_t(upw) * (a.dual ? 2 : 1) * waves * 16 * 4;
   }
   const int KT = bits == 4 ? 128 : (bits == 2 ? 256 : 64);
@@ -869,14 +908,7 @@ hipError_t launch_gemv(const GemvArgs& a, int bits, int waves, int grid, size_t 
   const int gpt = gemv_groups_per_tile(bits, a.nt, a.ng, a.bs, &tpg);
   if (gpt == 0) return hipErrorInvalidValue;
   dim3 g(grid), b(waves * 64);
-  if (lean_ok(a, bits, waves)) {
-    if (a.act_t == kActF32) return a.asym ? gemv_m1_launch<kActF32, true>(a, g, b, lds, stream)
-                                          : gemv_m1_launch<kActF32, false>(a, g, b, lds, stream);
-    if (a.act_t == kActF16) return a.asym ? gemv_m1_launch<kActF16, true>(a, g, b, lds, stream)
-                                          : gemv_m1_launch<kActF16, false>(a, g, b, lds, stream);
-    return a.asym ? gemv_m1_launch<kActBF16, true>(a, g, b, lds, stream)
-                  : gemv_m1_launch<kActBF16, false>(a, g, b, lds, stream);
-  }
+  if (lean_ok(a, bits, waves)) return gemv_m1_launch(a, bits, gpt, g, b, lds, stream);
   if (bits == 4) return gemv_launch1<4>(a, hilo, gpt, g, b, lds, stream);
   if (bits == 2) return gemv_launch1<2>(a, hilo, gpt, g, b, lds, stream);
   return gemv_launch1<8>(a, hilo, gpt, g, b, lds, stream);
