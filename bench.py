@@ -443,14 +443,14 @@ def main(argv=None):
         kernel, bytes_per_launch, launch_s = "woq_chain_kernel (whole decode step, one persistent launch)", tot_bytes, \
             chain_us
     else:
-        kernel, bytes_per_launch, launch_s = "woq_gemv_kernel (decode GEMV, one launch per matmul)", \
+        kernel, bytes_per_launch, launch_s = "woq_gemv_m1_kernel (decode GEMV, one launch per matmul)", \
             tot_bytes / n_per_op_launches, per_op_time / n_per_op_launches
     achieved = bytes_per_launch / launch_s / 1e9
     traffic = None
     pmc = os.path.join(REPO, "profiles", "pmc_traffic.json")
     if os.path.exists(pmc):
         try:
-            rec = json.load(open(pmc))["woq_chain_kernel" if chain is not None else "woq_gemv_kernel"]
+            rec = json.load(open(pmc))["woq_chain_kernel" if chain is not None else "woq_gemv_m1_kernel"]
             traffic = int(rec["traffic_over_algorithmic"] * bytes_per_launch)
         except Exception:
             traffic = None

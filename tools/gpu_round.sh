@@ -21,4 +21,14 @@ if [ "${SKIP_PROF:-0}" = 0 ]; then
   timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --prefill-steps 1 --no-cpu-baseline > gpurun_out/prof_bench_$TAG.json 2> gpurun_out/prof_$TAG.err; rc=$?
   echo "rocprof rc=$rc"; find gpurun_out/prof_$TAG -name "*stats*" | head; [ $rc -eq 0 ] || exit $rc
 fi
+if [ "${SKIP_PMC:-0}" = 0 ]; then
+  echo "== PMC traffic passes (FETCH_SIZE, WRITE_SIZE: one counter block per run)"; date
+  export TMPDIR=/tmp
+  rm -rf gpurun_out/pmc_$TAG; mkdir -p gpurun_out/pmc_$TAG
+  PMC_ALG_OUT=gpurun_out/pmc_$TAG/alg.json timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_$TAG/fetch -o run --output-format csv -- python tools/pmc_decode.py > gpurun_out/pmc_$TAG/fetch.log 2>&1; rc=$?
+  echo "fetch rc=$rc"; [ $rc -eq 0 ] || exit $rc
+  timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_$TAG/write -o run --output-format csv -- python tools/pmc_decode.py > gpurun_out/pmc_$TAG/write.log 2>&1; rc=$?
+  echo "write rc=$rc"; [ $rc -eq 0 ] || exit $rc
+  python tools/pmc_traffic.py gpurun_out/pmc_$TAG gpurun_out/pmc_traffic_$TAG.json
+fi
 echo "== done"; date

@@ -20,3 +20,10 @@ for _ in range(2):
 pre = bench.Runner(stack, 2048, None, "cuda")
 pre.step()
 torch.cuda.synchronize()
+# algorithmic bytes of the per-op decode launches above (tools/pmc_traffic.py divides the counters by these)
+if os.environ.get("PMC_ALG_OUT"):
+    import json
+    L1 = stack.launches(1)
+    launches = sum(c for *_, c in L1)
+    json.dump({"decode_bytes_per_token": sum(b * c for _, b, _, c in L1), "decode_launches_per_token": launches,
+               "decode_tokens": 3, "chain_tokens": 2}, open(os.environ["PMC_ALG_OUT"], "w"))
