@@ -9,8 +9,8 @@ import torch  # noqa: E402
 
 import bench  # noqa: E402
 
-bench.LAYERS = int(os.environ.get("PMC_LAYERS", "4"))
-stack = bench.Stack(0, 1)
+cfg = dict(bench.LLAMA, layers=int(os.environ.get("PMC_LAYERS", "4")))
+stack = bench.Stack(cfg, 0, 1)
 dec = bench.Runner(stack, 1, None, "cuda")
 for _ in range(3):
     dec.step()
