@@ -763,7 +763,7 @@ struct A16 {
 
 // 3: gemm3 (int4, groups of 128 * 2^j); 4: gemm4 (int4 g32 / g64, int2 groups >= 64); 0: register-staged fallback
 static int pipelined_gemm(const DeviceWeight& w, int m) {
-  if (env_int("NAD_GEMM2_DISABLE", 0) || w.kmajor || w.f4kind >= 0 || m < 32 ||
+  if (env_int("NAD_GEMM2_DISABLE", 0) || w.kmajor || w.f4kind >= 0 || m <= 16 ||
       uint64_t(m) * uint64_t(w.nt) * 512 >= (1ull << 32))
     return 0;
   const int tpg = w.blocksize / 128;
@@ -797,6 +797,25 @@ static int prepare_a16(A16& r, const void* act, int act_t, int lda, int m, int k
   return 1;
 }
 
+// Split-K plan of a pipelined GEMM whose 256 x 128 output tiles alone leave most CUs idle (M up to a few hundred, or
+// narrow N): runs of whole groups, at least two K tiles each, at most one workgroup per CU in total.  Returns the run
+// count (1 = no split) and the K tiles per run.
+static int splitk_plan(const DeviceWeight& w, int m, int* ktiles) {
+  *ktiles = w.nt;
+  if (env_int("NAD_SPLITK_DISABLE", 0)) return 1;
+  const int tiles = ((m + 255) / 256) * ((w.ns + 7) / 8);
+  if (tiles > 128) return 1;
+  const int tpg = std::max(1, w.blocksize / k_tile(w));
+  const int unit = tpg >= 2 ? tpg : 2;  // K tiles per run at least: one whole group and two tiles
+  int s = std::min(256 / tiles, w.nt / unit);
+  if (s < 2) return 1;
+  int kt = (w.nt + s - 1) / s;
+  kt = (kt + tpg - 1) / tpg * tpg;
+  s = (w.nt + kt - 1) / kt;
+  if (s < 2) return 1;
+  *ktiles = kt;
+  return s;
+}
 static int run_gemm(const void* act, int act_t, int lda, int m, int k, const DeviceWeight& w, float* out, int ldo,
                     int epi, const float* bias, int bias_ld, const float* res, int ld_res, const float* aux,
                     int ld_aux, hipStream_t st, const A16* pre = nullptr) {
@@ -828,9 +847,22 @@ static int run_gemm(const void* act, int act_t, int lda, int m, int k, const Dev
       if (prepare_a16(own, act, act_t, lda, m, k, w, st) < 0) return -1;
       pre = &own;
     }
-    hipError_t e = pg == 4                                ? launch_gemm4(a, w.bits, pre->p, pre->ld, st)
-                   : env_int("NAD_GEMM_KERNEL", 3) == 2 ? launch_gemm2(a, pre->p, pre->ld, st)
-                                                        : launch_gemm3(a, pre->p, pre->ld, st);
+    const bool g2 = pg == 3 && env_int("NAD_GEMM_KERNEL", 3) == 2;
+    int ktiles = w.nt;
+    const int ks = !g2 ? splitk_plan(w, m, &ktiles) : 1;
+    if (ks > 1) {  // partials after the fp16 activations in the same workspace (stream-ordered reuse)
+      a.ksplit = ks;
+      a.ktiles = ktiles;
+      a.ldp = (w.n + 3) / 4 * 4;
+      const size_t a16 = (size_t(m) * w.nt * k_tile(w) * 2 + 255) / 256 * 256;
+      char* base = static_cast<char*>(workspace_for(a16 + size_t(ks) * m * a.ldp * 4, st));
+      if (!base) return -1;
+      a.part = reinterpret_cast<float*>(base + a16);
+    }
+    hipError_t e = pg == 4 ? launch_gemm4(a, w.bits, pre->p, pre->ld, st)
+                   : g2    ? launch_gemm2(a, pre->p, pre->ld, st)
+                           : launch_gemm3(a, pre->p, pre->ld, st);
+    if (e == hipSuccess && ks > 1) e = launch_splitk_reduce(a, st);
     if (e != hipSuccess) {
       set_err("gemm2 kernel launch failed: %s", hipGetErrorString(e));
       return -1;

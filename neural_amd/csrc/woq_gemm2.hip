@@ -368,17 +368,24 @@ __global__ __launch_bounds__(512, 1) void woq_gemm3_kernel(GemmArgs a, const _Fl
   const int M = a.M, nt = W.nt, ng = W.ng, ns = W.ns;
   const int tpg = W.bs / KT;
   const int tsh = __builtin_ctz(unsigned(tpg));
-  const int nh = 2 * nt;
 
-  // XCD-aware remap (as gemm2)
+  // XCD-aware remap (as gemm2); with split-K the remapped id is (run, tile), so one XCD walks the N tiles of one
+  // (M tile, K run) and its L2 holds that run's A rows
   const int nbm = (M + BM - 1) / BM;
   const int nbn = (ns + 7) / 8;
-  const int nwg = nbm * nbn;
+  const int ntile = nbm * nbn;
+  const int nsplit = a.ksplit > 1 ? a.ksplit : 1;
+  const int nwg = ntile * nsplit;
   int bid = blockIdx.x;
   {
     const int q = nwg / 8, r = nwg % 8, x = bid % 8, o = bid / 8;
     bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + o;
   }
+  const int ks = bid / ntile;
+  bid -= ks * ntile;
+  const int kt0 = nsplit > 1 ? ks * a.ktiles : 0;          // first K tile of this run (a multiple of tpg)
+  const int ntl = nsplit > 1 ? min(a.ktiles, nt - kt0) : nt;
+  const int nh = 2 * ntl;
   const int bm = bid / nbn, bn = bid % nbn;
   const int m0 = bm * BM;
   const int nl = lane & 15, kq = lane >> 4;
@@ -391,12 +398,13 @@ __global__ __launch_bounds__(512, 1) void woq_gemm3_kernel(GemmArgs a, const _Fl
     const int grow = min(m0 + row, M - 1);  // rows past M re-read row M-1 (never stored)
     aoff[i] = uint32_t(grow) * uint32_t(lda16) * 2u + uint32_t(((lane & 7) ^ ((row >> 1) & 7)) * 16);
   }
-  const char* abase = reinterpret_cast<const char*>(A16);
+  const char* abase = reinterpret_cast<const char*>(A16) + size_t(kt0) * KT * 2;
   // B: wave w copies stripe 8 bn + w (clamped: stripes past N are never stored); scale / zero-point piece w & 1 covers
   // stripes 8 bn + 4 (w & 1) + (lane >> 4), column lane & 15
-  const char* btile = static_cast<const char*>(W.tiles) + (size_t(min(bn * 8 + wave, ns - 1)) * nt * 64 + lane) * 16;
+  const char* btile =
+      static_cast<const char*>(W.tiles) + (size_t(min(bn * 8 + wave, ns - 1)) * nt * 64 + lane) * 16 + size_t(kt0) * 1024;
   const int sstripe = min(bn * 8 + (wave & 1) * 4 + (lane >> 4), ns - 1);
-  const size_t srow0 = size_t(sstripe) * ng * 16 + nl;
+  const size_t srow0 = size_t(sstripe) * ng * 16 + nl + size_t(kt0 >> tsh) * 16;
   const int st = a.scale_t;
   const uint32_t* sbase = static_cast<const uint32_t*>(W.scales);
   const uint32_t* zbase = reinterpret_cast<const uint32_t*>(W.zps);
@@ -512,7 +520,7 @@ __global__ __launch_bounds__(512, 1) void woq_gemm3_kernel(GemmArgs a, const _Fl
       zp[1] = int(int8_t((zw1 >> zsh) & 0xFFu));
     }
     const bool gstart = H == 0 && (TPG1 || (t & (tpg - 1)) == 0);
-    const bool gend = H == 1 && (TPG1 || ((t + 1) & (tpg - 1)) == 0 || t == nt - 1);
+    const bool gend = H == 1 && (TPG1 || ((t + 1) & (tpg - 1)) == 0 || t == ntl - 1);
     uint32_t sw0 = 0, sw1 = 0;
 #pragma unroll
     for (int dd = 0; dd < 2; dd++) {
@@ -599,6 +607,10 @@ __global__ __launch_bounds__(512, 1) void woq_gemm3_kernel(GemmArgs a, const _Fl
     const int n0 = col0 + c4 * 4;
     const float4 t = *reinterpret_cast<const float4*>(tw + rl * 36 + c4 * 4);
     if (row >= M || n0 >= W.n) continue;
+    if (nsplit > 1) {  // raw partial of this K run (ldp % 4 == 0, 16-B aligned rows): the reduce applies the epilogue
+      *reinterpret_cast<float4*>(a.part + (size_t(ks) * M + row) * a.ldp + n0) = t;
+      continue;
+    }
     float v[4] = {t.x, t.y, t.z, t.w};
 #pragma unroll
     for (int e = 0; e < 4; e++) {
@@ -640,6 +652,61 @@ __global__ __launch_bounds__(512, 1) void woq_gemm3_kernel(GemmArgs a, const _Fl
 
 }  // namespace g3
 
+// ------------------------------------------------------------------------------------------------------------------
+// split-K reduce: out[row][n] = epi(sum over runs r = 0 .. S-1, in order, of part[r][row][n]); 4 columns per thread
+__global__ __launch_bounds__(256) void nad_splitk_reduce_kernel(GemmArgs a) {
+  const SkinnyWeight& W = a.w;
+  const int nq = (W.n + 3) >> 2;
+  const size_t q = size_t(blockIdx.x) * 256 + threadIdx.x;
+  if (q >= size_t(a.M) * nq) return;
+  const int row = int(q / nq), n0 = int(q - size_t(row) * nq) * 4;
+  const size_t rs = size_t(a.M) * a.ldp;
+  const float* p = a.part + size_t(row) * a.ldp + n0;
+  float4 s = *reinterpret_cast<const float4*>(p);
+  for (int r = 1; r < a.ksplit; r++) {
+    const float4 t = *reinterpret_cast<const float4*>(p + r * rs);
+    s.x += t.x;
+    s.y += t.y;
+    s.z += t.z;
+    s.w += t.w;
+  }
+  float v[4] = {s.x, s.y, s.z, s.w};
+#pragma unroll
+  for (int e = 0; e < 4; e++) {
+    const int n = n0 + e;
+    if (n >= W.n) break;
+    switch (a.epi) {
+      case kEpiBias:
+        v[e] += W.bias[size_t(row) * W.bias_ld + n];
+        break;
+      case kEpiAddGelu:
+        v[e] = gelu_f(v[e] + W.bias[size_t(row) * W.bias_ld + n]);
+        break;
+      case kEpiGelu:
+        v[e] = gelu_f(v[e]);
+        break;
+      case kEpiSilu:
+        v[e] = silu_f(v[e]);
+        break;
+      case kEpiResAdd:
+        v[e] += a.res[size_t(row) * a.ld_res + n];
+        break;
+      case kEpiSiluMul:
+        v[e] = a.aux[size_t(row) * a.ld_aux + n] * v[e];
+        break;
+      default:
+        break;
+    }
+    W.out[size_t(row) * W.ldo + n] = v[e];
+  }
+}
+
+hipError_t launch_splitk_reduce(const GemmArgs& a, hipStream_t st) {
+  const size_t work = size_t(a.M) * ((a.w.n + 3) / 4);
+  hipLaunchKernelGGL(nad_splitk_reduce_kernel, dim3(unsigned((work + 255) / 256)), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
 hipError_t launch_gemm3(const GemmArgs& a, const _Float16* A16, int lda16, hipStream_t st) {
   const int nbm = (a.M + g3::BM - 1) / g3::BM, nbn = (a.w.ns + 7) / 8;
   const bool tpg1 = a.w.bs == g3::KT;
@@ -652,7 +719,7 @@ hipError_t launch_gemm3(const GemmArgs& a, const _Float16* A16, int lda16, hipSt
       if (e != hipSuccess) return e;
       done = true;
     }
-    hipLaunchKernelGGL(k, dim3(nbm * nbn), dim3(512), g3::LDS_BYTES, st, a, A16, lda16);
+    hipLaunchKernelGGL(k, dim3(nbm * nbn * (a.ksplit > 1 ? a.ksplit : 1)), dim3(512), g3::LDS_BYTES, st, a, A16, lda16);
     return hipGetLastError();
   };
   const bool asym = a.w.zps != nullptr;

@@ -209,18 +209,24 @@ __global__ __launch_bounds__(512, 1) void woq_gemm4_kernel(GemmArgs a, const _Fl
   const int wm = wave >> 2, wn = wave & 3;
   const SkinnyWeight& W = a.w;
   const int M = a.M, nt = W.nt, ng = W.ng, ns = W.ns;
-  const int nh = HPT * nt;  // half steps
   const int gh = 1 << gh_log2;
 
   // XCD-aware remap (as gemm2 / gemm3)
   const int nbm = (M + BM - 1) / BM;
   const int nbn = (ns + 7) / 8;
-  const int nwg = nbm * nbn;
+  const int ntile = nbm * nbn;
+  const int nsplit = a.ksplit > 1 ? a.ksplit : 1;  // split-K runs of whole groups (see woq_gemm3_kernel)
+  const int nwg = ntile * nsplit;
   int bid = blockIdx.x;
   {
     const int q = nwg / 8, r = nwg % 8, x = bid % 8, o = bid / 8;
     bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + o;
   }
+  const int ks = bid / ntile;
+  bid -= ks * ntile;
+  const int kt0 = nsplit > 1 ? ks * a.ktiles : 0;
+  const int ntl = nsplit > 1 ? min(a.ktiles, nt - kt0) : nt;
+  const int nh = HPT * ntl;  // half steps of this run
   const int bm = bid / nbn, bn = bid % nbn;
   const int m0 = bm * BM;
   const int nl = lane & 15, kq = lane >> 4;
@@ -232,7 +238,7 @@ __global__ __launch_bounds__(512, 1) void woq_gemm4_kernel(GemmArgs a, const _Fl
     const int grow = min(m0 + row, M - 1);
     aoff[i] = uint32_t(grow) * uint32_t(lda16) * 2u + uint32_t(((lane & 7) ^ ((row >> 1) & 7)) * 16);
   }
-  const char* abase = reinterpret_cast<const char*>(A16);
+  const char* abase = reinterpret_cast<const char*>(A16) + size_t(kt0) * HPT * ROWB;
   const char* btile = static_cast<const char*>(W.tiles) + (size_t(min(bn * 8 + wave, ns - 1)) * nt * 64 + lane) * 16;
   const int sstripe = min(bn * 8 + (wave & 1) * 4 + (lane >> 4), ns - 1);
   const size_t srow0 = size_t(sstripe) * ng * 16 + nl;
@@ -256,12 +262,13 @@ __global__ __launch_bounds__(512, 1) void woq_gemm4_kernel(GemmArgs a, const _Fl
   };
 
   // batch(u): A(u + 3) and, when u + 3 starts a tile, that tile + its scale (+ zero-point) pieces
-  auto issue_tile = [&](int t) {
+  auto issue_tile = [&](int t) {  // t: tile of this run (ring slot), tg: tile of the weight
     char* bb = smem + NA * HBUF + (t % NBR) * BBUF;
-    glds16(btile + size_t(t) * 1024, bb + wave * 1024);
-    const size_t si = srow0 + size_t(slot_group(t, slot_w)) * 16;
+    const int tg = t + kt0;
+    glds16(btile + size_t(tg) * 1024, bb + wave * 1024);
+    const size_t si = srow0 + size_t(slot_group(tg, slot_w)) * 16;
     glds4(sbase + (st == kScaleF32 ? si : (si >> 1)), bb + BTILES + slot_w * 512 + (wave & 1) * 256);
-    if constexpr (ASYM) glds4(zbase + ((zrow0 + size_t(slot_group(t, zslot)) * 16) >> 2), bb + BTILES + BSC + zq * 256);
+    if constexpr (ASYM) glds4(zbase + ((zrow0 + size_t(slot_group(tg, zslot)) * 16) >> 2), bb + BTILES + BSC + zq * 256);
   };
   auto issue = [&](auto Pc, int u) {
     constexpr int P = decltype(Pc)::value;  // (u + 3) % HPT
@@ -521,6 +528,10 @@ __global__ __launch_bounds__(512, 1) void woq_gemm4_kernel(GemmArgs a, const _Fl
     const int n0 = col0 + c4 * 4;
     const float4 tv = *reinterpret_cast<const float4*>(tw + rl * 36 + c4 * 4);
     if (row >= M || n0 >= W.n) continue;
+    if (nsplit > 1) {  // raw partial of this K run; launch_splitk_reduce applies the epilogue
+      *reinterpret_cast<float4*>(a.part + (size_t(ks) * M + row) * a.ldp + n0) = tv;
+      continue;
+    }
     float v[4] = {tv.x, tv.y, tv.z, tv.w};
 #pragma unroll
     for (int e = 0; e < 4; e++) {
@@ -590,7 +601,7 @@ hipError_t launch_gemm4(const GemmArgs& a, int bits, const _Float16* A16, int ld
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
                                        lds);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k, dim3(nbm * nbn), dim3(512), lds, st, ga, A16, lda16, gh_log2);
+    hipLaunchKernelGGL(k, dim3(nbm * nbn * (a.ksplit > 1 ? a.ksplit : 1)), dim3(512), lds, st, ga, A16, lda16, gh_log2);
     return hipGetLastError();
   };
 #define NAD_G4(B, G, A) go(g4::woq_gemm4_kernel<B, G, A>, g4::lds_bytes<B, G, A>())

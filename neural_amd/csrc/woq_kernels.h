@@ -73,6 +73,13 @@ struct GemmArgs {
   int ld_aux;
   int prio;             // gemm3: waves 4-7 at s_setprio 1 for the whole loop (NAD_GEMM3_PRIO)
   int stagger;          // gemm3: waves 4-7 half a step behind waves 0-3 (NAD_GEMM3_STAGGER)
+  // split-K (gemm3 / gemm4 when the output tiles alone cannot fill the chip): the K tiles are cut into ksplit runs of
+  // ktiles (a multiple of the tiles per group); run r of tile b writes its raw fp32 partial to
+  // part[(r * M + row) * ldp + n] and launch_splitk_reduce sums the runs in order and applies the epilogue.
+  int ksplit;           // 0 / 1: no split
+  int ktiles;
+  float* part;
+  int ldp;
   SkinnyWeight w;
 };
 
@@ -169,6 +176,8 @@ hipError_t launch_q8_0_quant(const Q80Args& a, int act_t, hipStream_t stream);
 hipError_t launch_quant_u8(const QuantU8Args& a, int act_t, hipStream_t stream);
 hipError_t launch_i8(const I8Args& a, int bits, hipStream_t stream);
 hipError_t launch_gemm4(const GemmArgs& a, int bits, const _Float16* A16, int lda16, hipStream_t stream);
+// sum a.ksplit partials of a split-K gemm3 / gemm4 launch in run order and apply a.epi into a.w.out (woq_gemm2.hip)
+hipError_t launch_splitk_reduce(const GemmArgs& a, hipStream_t stream);
 hipError_t launch_cvt_act(const void* A, int act_t, int lda, int M, int K, int Kp, const int32_t* shuffle,
                           _Float16* out, hipStream_t stream);
 // groups per K tile the GEMV handles (1, 2, 4, 8) for this geometry, 0 if unsupported; *tpg = tiles per group

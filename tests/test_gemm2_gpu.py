@@ -1,7 +1,7 @@
 """Prefill GEMMs (woq_gemm2.hip): gemm3 (default: every operand by LDS-DMA, three 64-deep half steps in flight) and
 gemm2 (NAD_GEMM_KERNEL=2: A by LDS-DMA one K step ahead, B in registers).
 
-Both run for int4 weights with group size a power-of-two multiple of 128 and M >= 32 (capi.hip gemm2_ok); these
+Both run for int4 weights with group size a power-of-two multiple of 128 and M > 16 (capi.hip gemm2_ok); these
 cases pin them against the oracle (fp64 GEMM on the reference's dequantized weights) on ragged M/N, K tails, all
 scale dtypes, asymmetric zero points, per-channel scales and act-order shuffles.
 
@@ -179,3 +179,87 @@ def test_gemm4_takes_the_fallback_configs(oracle, monkeypatch):
     monkeypatch.setenv("NAD_GEMM4_DISABLE", "1")
     y1 = w.forward(x).cpu().numpy()
     assert _rel_err(y4, y1.astype(np.float64)) <= 2e-5
+
+
+SPLITK_CASES = [
+    # m, n, k, bs, asym, act -- few 256 x 128 output tiles: gemm3 runs split-K (capi.hip splitk_plan) + the ordered reduce
+    (17, 4096, 4096, 128, False, "fp16"),     # smallest M past the GEMV (was the register-staged fallback)
+    (31, 1024, 4096, 128, True, "fp32"),
+    (64, 4096, 4096, 128, False, "fp32"),     # batched decode at the Llama O shape: 32 tiles x 8 runs of 4 K tiles
+    (100, 1024, 11008, 128, True, "bf16"),    # down-like K = 86 tiles: runs of 3, the last one shorter
+    (256, 2048, 4096, 256, False, "fp16"),    # 2 K tiles per group: runs of whole groups
+    (512, 1536, 4096, 128, True, "fp16"),     # a TP-8 QKV shard width at a 512-token prefill chunk
+]
+
+
+@pytest.mark.parametrize("cfg", SPLITK_CASES)
+def test_gemm_splitk_parity(oracle, monkeypatch, cfg):
+    """Split-K gemm3 against the oracle, and against the same GEMM without the split (fp32 sums in another order)."""
+    m, n, k, bs, asym, act = cfg
+    blob = _blob(oracle, n, k, bs, S4, F16, asym, 4, seed=m + n + k)
+    w = bestla.DeviceWeight(blob)
+    A = np.random.default_rng(m + 17).uniform(-0.5, 0.5, size=(m, k)).astype(np.float32)
+    x = torch.from_numpy(A).cuda()
+    if act != "fp32":
+        x = x.to(torch.float16 if act == "fp16" else torch.bfloat16)
+    ref = oracle.forward(x.float().cpu().numpy(), blob, n, k)
+    y = w.forward(x).cpu().numpy()
+    assert _rel_err(y, ref) <= TOL[act], (_rel_err(y, ref), act)
+    monkeypatch.setenv("NAD_SPLITK_DISABLE", "1")
+    y1 = w.forward(x).cpu().numpy()
+    assert _rel_err(y, y1.astype(np.float64)) <= 2e-5
+
+
+def test_gemm_splitk_epilogues(oracle):
+    """The split-K reduce applies bias, residual and the FFN's SiLU*mul after summing the runs."""
+    m, n, k = 48, 1024, 2048
+    blob = _blob(oracle, n, k, 128, S4, F16, False, 4, seed=91)
+    w = bestla.DeviceWeight(blob)
+    rng = np.random.default_rng(9)
+    A = rng.uniform(-0.5, 0.5, size=(m, k)).astype(np.float32)
+    x = torch.from_numpy(A).cuda()
+    ref = oracle.forward(A, blob, n, k).astype(np.float64)
+    b = rng.uniform(-1, 1, size=(n,)).astype(np.float32)
+    r = rng.uniform(-1, 1, size=(m, n)).astype(np.float32)
+    y = w.forward(x, epilogue=bestla.EPI_BIAS, bias=torch.from_numpy(b).cuda()).cpu().numpy()
+    assert _rel_err(y, ref + b) <= TOL["fp32"]
+    y = w.forward(x, epilogue=bestla.EPI_RES_ADD, residual=torch.from_numpy(r).cuda()).cpu().numpy()
+    assert _rel_err(y, ref + r) <= TOL["fp32"]
+    fin, fmid, fout = 2048, 1024, 2048
+    b1, b3, b2 = (_blob(oracle, nn, kk, 128, S4, F16, False, 4, seed=s)
+                  for nn, kk, s in ((fmid, fin, 61), (fmid, fin, 63), (fout, fmid, 62)))
+    w1, w2, w3 = (bestla.DeviceWeight(bb) for bb in (b1, b2, b3))
+    y = bestla.ffn_forward(x, w1, w2, w3, act="silu").cpu().numpy()
+    h1 = oracle.forward(A, b1, fmid, fin).astype(np.float64)
+    h3 = oracle.forward(A, b3, fmid, fin).astype(np.float64)
+    ref = oracle.forward((h1 / (1 + np.exp(-h1)) * h3).astype(np.float32), b2, fout, fmid)
+    assert _rel_err(y, ref) <= 2 * TOL["fp32"]
+
+
+SPLITK4_CASES = [
+    # m, n, k, bs, qtype, asym, act -- gemm4 formats with few output tiles: split-K runs of whole groups
+    (256, 1024, 4096, 64, S2, False, "fp16"),    # Mistral k/v projection (int2 g64) at a 256-token chunk
+    (64, 4096, 4096, 32, S4, True, "fp32"),      # int4 g32 asym (the reference Python default group), batched decode
+    (48, 2048, 2048, 128, S8, False, "bf16"),    # int8 g128: runs of two 64-deep tiles per group
+    (96, 512, 4096, 128, S2, True, "fp16"),      # int2 g128 asym, 4 half steps per tile
+    (17, 4096, 4096, 32, S4, False, "fp32"),     # M just past the GEMV (was the register-staged fallback)
+    (24, 1024, 4096, 64, S2, True, "bf16"),
+    (31, 768, 2048, 32, S8, True, "fp16"),
+]
+
+
+@pytest.mark.parametrize("cfg", SPLITK4_CASES)
+def test_gemm4_splitk_parity(oracle, monkeypatch, cfg):
+    m, n, k, bs, qt, asym, act = cfg
+    blob = _blob(oracle, n, k, bs, qt, F16, asym, 4, seed=m + 3 * n + k)
+    w = bestla.DeviceWeight(blob)
+    A = np.random.default_rng(m + 5).uniform(-0.5, 0.5, size=(m, k)).astype(np.float32)
+    x = torch.from_numpy(A).cuda()
+    if act != "fp32":
+        x = x.to(torch.float16 if act == "fp16" else torch.bfloat16)
+    ref = oracle.forward(x.float().cpu().numpy(), blob, n, k)
+    y = w.forward(x).cpu().numpy()
+    assert _rel_err(y, ref) <= TOL[act], (_rel_err(y, ref), act)
+    monkeypatch.setenv("NAD_SPLITK_DISABLE", "1")
+    y1 = w.forward(x).cpu().numpy()
+    assert _rel_err(y, y1.astype(np.float64)) <= 2e-5
