@@ -167,7 +167,9 @@ int nad_device_qkv_forward(const void* act, int act_dtype, const void* wq, const
 int nad_device_ffn_gate_up(const void* act, int act_dtype, const void* w1, const void* w3, float* tmp1, float* tmp2,
                            int m, int fin, int fmid, int lda, int epi, void* queue);
 /* fused FFN (ip_fusion_ffn.cpp:407-457): tmp1 = act1(X.W1^T) [optional], tmp2 = tmp1 * (X.W3^T), out = tmp2 . W2^T.
- * epi = NAD_EPI_SILU_MUL or NAD_EPI_GELU_MUL. */
+ * epi = NAD_EPI_SILU_MUL or NAD_EPI_GELU_MUL.  tmp1 / tmp2 are scratch: for M > 16 with the pipelined GEMMs they hold
+ * the intermediates as fp16 (the down GEMM reads tmp2 as its fp16 operand; NAD_FFN_F32=1 keeps fp32).  The
+ * reference-named bestla_fusion_FFN_* entries always return the fp32 intermediates in tmp1 / tmp2. */
 int nad_device_ffn_forward(const void* act, int act_dtype, const void* w1, const void* w2, const void* w3, float* tmp1,
                            float* tmp2, float* out, int m, int fin, int fmid, int fout, int lda, int epi, void* queue);
 /* tensor-parallel slicing of a packed blob without re-quantization (the reference re-quantizes,

@@ -773,6 +773,15 @@ static int pipelined_gemm(const DeviceWeight& w, int m) {
 }
 static bool gemm2_ok(const DeviceWeight& w, int m) { return pipelined_gemm(w, m) != 0; }
 static int k_tile(const DeviceWeight& w) { return w.bits == 4 ? 128 : (w.bits == 2 ? 256 : 64); }
+// The FFN's prefill keeps its intermediates in fp16 when all three GEMMs are the pipelined ones reading the unshuffled
+// fp16 operand and fmid is a whole number of w2's K tiles (NAD_FFN_F32=1: the fp32 intermediates, A/B)
+static bool ffn16_ok(const DeviceWeight& w1, const DeviceWeight& w2, const DeviceWeight& w3, int m, int fmid) {
+  auto ok = [&](const DeviceWeight& w) {
+    return pipelined_gemm(w, m) && !w.shuffle && !int8_compute(w);
+  };
+  return !env_int("NAD_FFN_F32", 0) && env_int("NAD_GEMM_KERNEL", 3) != 2 && ok(w1) && ok(w2) && ok(w3) &&
+         w2.nt * k_tile(w2) == fmid && fmid % 8 == 0;
+}
 
 // 1 ready, -1 error (no workspace under capture, launch error)
 static int prepare_a16(A16& r, const void* act, int act_t, int lda, int m, int k, const DeviceWeight& w,
@@ -816,9 +825,16 @@ static int splitk_plan(const DeviceWeight& w, int m, int* ktiles) {
   *ktiles = kt;
   return s;
 }
+// fp16 result / SiLU*mul operand of a pipelined GEMM (the FFN's intermediates, ffn16_ok)
+struct Half16 {
+  _Float16* out = nullptr;
+  int ldo = 0;
+  const _Float16* aux = nullptr;
+};
+
 static int run_gemm(const void* act, int act_t, int lda, int m, int k, const DeviceWeight& w, float* out, int ldo,
                     int epi, const float* bias, int bias_ld, const float* res, int ld_res, const float* aux,
-                    int ld_aux, hipStream_t st, const A16* pre = nullptr) {
+                    int ld_aux, hipStream_t st, const A16* pre = nullptr, const Half16* h16 = nullptr) {
   if (int8_compute(w)) {
     const DeviceWeight* ws[1] = {&w};
     float* outs[1] = {out};
@@ -841,6 +857,15 @@ static int run_gemm(const void* act, int act_t, int lda, int m, int k, const Dev
   a.stagger = env_int("NAD_GEMM3_STAGGER", 1);  // measured +3-7 % (profiles/r02_gemm3_stagger.txt)
   a.w = view(w, out, ldo, bias, bias_ld);
   const int pg = pipelined_gemm(w, m);
+  if (h16) {
+    if (!pg) {
+      set_err("fp16 GEMM output needs the pipelined GEMM");
+      return -1;
+    }
+    a.out16 = h16->out;
+    a.ldo16 = h16->ldo;
+    a.aux16 = h16->aux;
+  }
   if (pg) {
     A16 own;
     if (!pre || pre->kp != w.nt * k_tile(w) || w.shuffle) {
@@ -994,9 +1019,11 @@ extern "C" int nad_device_ffn_gate_up(const void* act, int act_dtype, const void
                   pp);
 }
 
-extern "C" int nad_device_ffn_forward(const void* act, int act_dtype, const void* w1p, const void* w2p,
-                                      const void* w3p, float* tmp1, float* tmp2, float* out, int m, int fin, int fmid,
-                                      int fout, int lda, int epi, void* queue) {
+// f16_tmp: the prefill may keep tmp1 / tmp2 as fp16 scratch (ffn16_ok); the reference-named host entries, whose
+// tmp2 the caller reads back as the fp32 intermediate (ip_fusion_ffn.cpp), pass false
+static int ffn_forward(const void* act, int act_dtype, const void* w1p, const void* w2p, const void* w3p, float* tmp1,
+                       float* tmp2, float* out, int m, int fin, int fmid, int fout, int lda, int epi, void* queue,
+                       bool f16_tmp) {
   const DeviceWeight* w1 = as_weight(w1p);
   const DeviceWeight* w2 = as_weight(w2p);
   const DeviceWeight* w3 = as_weight(w3p);
@@ -1011,6 +1038,26 @@ extern "C" int nad_device_ffn_forward(const void* act, int act_dtype, const void
     return -1;
   }
   hipStream_t st = static_cast<hipStream_t>(queue);
+  if (f16_tmp && m > kSkinnyMaxM && tmp1 && ffn16_ok(*w1, *w2, *w3, m, fmid)) {
+    // prefill with fp16 intermediates: gate -> act(x.w1) as fp16 in tmp1, up -> act(x.w1) * (x.w3) as fp16 in tmp2,
+    // which IS down's fp16 A operand (fmid = whole K tiles): no fp32 round trip, no conversion pass before down
+    A16 pre;
+    if (prepare_a16(pre, act, act_dtype, lda, m, fin, *w1, st) < 0) return -1;
+    _Float16* h1 = reinterpret_cast<_Float16*>(tmp1);
+    _Float16* h2 = reinterpret_cast<_Float16*>(tmp2);
+    const Half16 g{h1, fmid, nullptr}, u{h2, fmid, h1};
+    const int e1 = epi == kEpiSiluMul ? kEpiSilu : kEpiGelu;
+    if (run_gemm(act, act_dtype, lda, m, fin, *w1, nullptr, fmid, e1, nullptr, 0, nullptr, 0, nullptr, 0, st, &pre,
+                 &g) ||
+        run_gemm(act, act_dtype, lda, m, fin, *w3, nullptr, fmid, kEpiSiluMul, nullptr, 0, nullptr, 0, nullptr, fmid,
+                 st, &pre, &u))
+      return -1;
+    A16 d;
+    d.p = h2;
+    d.ld = fmid;
+    d.kp = fmid;
+    return run_gemm(h2, kActF16, fmid, m, fmid, *w2, out, fout, kEpiNone, nullptr, 0, nullptr, 0, nullptr, 0, st, &d);
+  }
   if (nad_device_ffn_gate_up(act, act_dtype, w1p, w3p, tmp1, tmp2, m, fin, fmid, lda, epi, queue)) return -1;
   if (m <= kSkinnyMaxM) {
     const DeviceWeight* ws[1] = {w2};
@@ -1020,6 +1067,12 @@ extern "C" int nad_device_ffn_forward(const void* act, int act_dtype, const void
                       st);
   }
   return run_gemm(tmp2, kActF32, fmid, m, fmid, *w2, out, fout, kEpiNone, nullptr, 0, nullptr, 0, nullptr, 0, st);
+}
+
+extern "C" int nad_device_ffn_forward(const void* act, int act_dtype, const void* w1p, const void* w2p,
+                                      const void* w3p, float* tmp1, float* tmp2, float* out, int m, int fin, int fmid,
+                                      int fout, int lda, int epi, void* queue) {
+  return ffn_forward(act, act_dtype, w1p, w2p, w3p, tmp1, tmp2, out, m, fin, fmid, fout, lda, epi, queue, true);
 }
 
 // ------------------------------------------------------------------------------------------------ decode chain
@@ -1584,9 +1637,8 @@ static void host_ffn3(float* act, void* w1p, void* w2p, void* w3p, float* tmp1, 
                                {tmp2, size_t(seq) * fmid * 4, true, nullptr},
                                {out, size_t(seq) * fout * 4, true, nullptr}};
   if (with_staged(bufs, d->stream) ||
-      nad_device_ffn_forward(bufs[0].dev, kActF32, w1, w2, w3, static_cast<float*>(bufs[1].dev),
-                             static_cast<float*>(bufs[2].dev), static_cast<float*>(bufs[3].dev), seq, fin, fmid, fout,
-                             fin, epi, d->stream) ||
+      ffn_forward(bufs[0].dev, kActF32, w1, w2, w3, static_cast<float*>(bufs[1].dev), static_cast<float*>(bufs[2].dev),
+                  static_cast<float*>(bufs[3].dev), seq, fin, fmid, fout, fin, epi, d->stream, false) ||
       finish_staged(bufs, d->stream))
     report(name);
 }

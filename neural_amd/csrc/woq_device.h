@@ -235,4 +235,58 @@ __device__ __forceinline__ float gelu_f(float x) {
   return 0.5f * x * (1.f + tanhf(0.7978845834732056f * (x + 0.044714998453855515f * x * x * x)));
 }
 
+// Prefill epilogue of four consecutive outputs (row, n0 .. n0 + 3) of a gemm3 / gemm4 / split-K reduce: the fused op,
+// then the store -- fp32 into w.out, or fp16 (RNE) into out16 when the FFN keeps its intermediates in fp16.
+__device__ __forceinline__ void gemm_epilogue4(const GemmArgs& a, int row, int n0, float (&v)[4]) {
+  const SkinnyWeight& W = a.w;
+#pragma unroll
+  for (int e = 0; e < 4; e++) {
+    const int n = n0 + e;
+    if (n >= W.n) break;
+    switch (a.epi) {
+      case kEpiBias:
+        v[e] += W.bias[size_t(row) * W.bias_ld + n];
+        break;
+      case kEpiAddGelu:
+        v[e] = gelu_f(v[e] + W.bias[size_t(row) * W.bias_ld + n]);
+        break;
+      case kEpiGelu:
+        v[e] = gelu_f(v[e]);
+        break;
+      case kEpiSilu:
+        v[e] = silu_f(v[e]);
+        break;
+      case kEpiResAdd:
+        v[e] += a.res[size_t(row) * a.ld_res + n];
+        break;
+      case kEpiSiluMul:  // second GEMM of the FFN: aux holds act(x.w1)
+        v[e] = (a.aux16 ? float(a.aux16[size_t(row) * a.ld_aux + n]) : a.aux[size_t(row) * a.ld_aux + n]) * v[e];
+        break;
+      default:
+        break;
+    }
+  }
+  const bool full = n0 + 3 < W.n;
+  if (a.out16) {
+    _Float16* o = a.out16 + size_t(row) * a.ldo16 + n0;
+    if (full && (reinterpret_cast<uintptr_t>(o) & 7) == 0) {
+      typedef _Float16 h4v __attribute__((ext_vector_type(4)));
+      *reinterpret_cast<h4v*>(o) = h4v{_Float16(v[0]), _Float16(v[1]), _Float16(v[2]), _Float16(v[3])};
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; e++)
+        if (n0 + e < W.n) o[e] = _Float16(v[e]);
+    }
+    return;
+  }
+  float* o = W.out + size_t(row) * W.ldo + n0;
+  if (full && (reinterpret_cast<uintptr_t>(o) & 15) == 0) {
+    *reinterpret_cast<float4*>(o) = make_float4(v[0], v[1], v[2], v[3]);
+  } else {
+#pragma unroll
+    for (int e = 0; e < 4; e++)
+      if (n0 + e < W.n) o[e] = v[e];
+  }
+}
+
 }  // namespace nad

@@ -519,7 +519,6 @@ __global__ __launch_bounds__(512, 1) void woq_gemm4_kernel(GemmArgs a, const _Fl
       for (int rr = 0; rr < 4; rr++) tw[(i * 16 + kq * 4 + rr) * 36 + j * 16 + nl] = acc[i][j][rr];
   const int s0 = bn * 8 + wn * 2;
   const int col0 = s0 * 16;
-  const bool vec_out = (reinterpret_cast<uintptr_t>(W.out) % 16 == 0) && (W.ldo % 4 == 0);
 #pragma unroll 4
   for (int q = 0; q < 16; q++) {
     const int c = q * 64 + lane;
@@ -533,41 +532,7 @@ __global__ __launch_bounds__(512, 1) void woq_gemm4_kernel(GemmArgs a, const _Fl
       continue;
     }
     float v[4] = {tv.x, tv.y, tv.z, tv.w};
-#pragma unroll
-    for (int e = 0; e < 4; e++) {
-      const int n = n0 + e;
-      if (n >= W.n) break;
-      switch (a.epi) {
-        case kEpiBias:
-          v[e] += W.bias[size_t(row) * W.bias_ld + n];
-          break;
-        case kEpiAddGelu:
-          v[e] = gelu_f(v[e] + W.bias[size_t(row) * W.bias_ld + n]);
-          break;
-        case kEpiGelu:
-          v[e] = gelu_f(v[e]);
-          break;
-        case kEpiSilu:
-          v[e] = silu_f(v[e]);
-          break;
-        case kEpiResAdd:
-          v[e] += a.res[size_t(row) * a.ld_res + n];
-          break;
-        case kEpiSiluMul:
-          v[e] = a.aux[size_t(row) * a.ld_aux + n] * v[e];
-          break;
-        default:
-          break;
-      }
-    }
-    float* o = W.out + size_t(row) * W.ldo + n0;
-    if (vec_out && n0 + 3 < W.n) {
-      *reinterpret_cast<float4*>(o) = make_float4(v[0], v[1], v[2], v[3]);
-    } else {
-#pragma unroll
-      for (int e = 0; e < 4; e++)
-        if (n0 + e < W.n) o[e] = v[e];
-    }
+    gemm_epilogue4(a, row, n0, v);
   }
 }
 

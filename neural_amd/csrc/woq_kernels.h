@@ -80,6 +80,11 @@ struct GemmArgs {
   int ktiles;
   float* part;
   int ldp;
+  // FFN prefill with fp16 intermediates: out16 set = the result goes to out16[row * ldo16 + n] as fp16 (RNE) instead of
+  // w.out; aux16 set = the SiLU*mul operand is read as fp16 from aux16[row * ld_aux + n]
+  _Float16* out16;
+  int ldo16;
+  const _Float16* aux16;
   SkinnyWeight w;
 };
 

@@ -263,3 +263,24 @@ def test_gemm4_splitk_parity(oracle, monkeypatch, cfg):
     monkeypatch.setenv("NAD_SPLITK_DISABLE", "1")
     y1 = w.forward(x).cpu().numpy()
     assert _rel_err(y, y1.astype(np.float64)) <= 2e-5
+
+
+@pytest.mark.parametrize("qt,bs", [(S4, 128), (S2, 64), (S4, 32)])
+def test_ffn_prefill_fp16_intermediates(oracle, monkeypatch, qt, bs):
+    """The prefill FFN keeps act(x.W1) and act(x.W1)*(x.W3) in fp16 (the down GEMM reads the second one as its operand
+    directly): within the fp32-path tolerance of the oracle and of the fp32-intermediate path (NAD_FFN_F32=1)."""
+    m, fin, fmid, fout = 160, 1024, 1536, 1024
+    b1, b3, b2 = (_blob(oracle, nn, kk, bs, qt, F16, False, 4, seed=s)
+                  for nn, kk, s in ((fmid, fin, 71), (fmid, fin, 73), (fout, fmid, 72)))
+    w1, w2, w3 = (bestla.DeviceWeight(bb) for bb in (b1, b2, b3))
+    A = np.random.default_rng(13).uniform(-1, 1, size=(m, fin)).astype(np.float32)
+    x = torch.from_numpy(A).cuda()
+    y = bestla.ffn_forward(x, w1, w2, w3, act="silu").cpu().numpy()
+    h1 = oracle.forward(A, b1, fmid, fin).astype(np.float64)
+    h3 = oracle.forward(A, b3, fmid, fin).astype(np.float64)
+    ref = oracle.forward((h1 / (1 + np.exp(-h1)) * h3).astype(np.float32), b2, fout, fmid)
+    assert _rel_err(y, ref) <= 2 * TOL["fp32"], _rel_err(y, ref)
+    monkeypatch.setenv("NAD_FFN_F32", "1")
+    y32 = bestla.ffn_forward(x, w1, w2, w3, act="silu").cpu().numpy()
+    assert _rel_err(y, y32.astype(np.float64)) <= 2 * TOL["fp32"]
+    assert not np.array_equal(y, y32)   # the fp16 path really ran (different rounding of the intermediates)
