@@ -36,9 +36,11 @@ MFMA_F16_PEAK_TFLOPS = 2500.0
 LLAMA = dict(name="Llama-2-7B", hidden=4096, ffn=11008, layers=32, vocab=32000, kv=4096, head=128, group=128,
              bits=dict(q=4, k=4, v=4, o=4, gate=4, up=4, down=4, lm=4), asym=False, fuse_qkv=True)
 LLAMA_ASYM = dict(LLAMA, asym=True, scale="bf16")   # GPTQ/AWQ zero points, bf16 scales as qpack stores them
-# Mistral-7B: kv heads 8 (n_head_kv != n_head -> no QKV fusion, llama.cpp:212-215); int2 policy keeps wv, w2 int4 sym
+# Mistral-7B: kv heads 8 (n_head_kv != n_head: the reference's CPU graph runs three matmuls, llama.cpp:212-215); int2
+# policy keeps wv, w2 int4 sym.  Here nad_device_qkv_forward takes Q, K, V of different N and format: decode runs one
+# stream launch for {Q, K} (int2) and one for V (int4), each output bit-identical to its own launch.
 MISTRAL = dict(name="Mistral-7B", hidden=4096, ffn=14336, layers=32, vocab=32000, kv=1024, head=128, group=64,
-               bits=dict(q=2, k=2, v=4, o=2, gate=2, up=2, down=4, lm=2), asym=False, fuse_qkv=False,
+               bits=dict(q=2, k=2, v=4, o=2, gate=2, up=2, down=4, lm=2), asym=False, fuse_qkv=False, group_qkv=True,
                int4_roles_sym=True)
 
 
@@ -92,7 +94,11 @@ class Stack:
         wb = lambda role, n, k: weight_bytes(n, k, b[role], g, self.sbytes, self.asym_of(role))  # noqa: E731
         qkv = [("qkv", wb("q", self.nq, H) + wb("k", self.nkv, H) + wb("v", self.nkv, H) +
                 (m * H + m * (self.nq + 2 * self.nkv)) * a, 2 * m * (self.nq + 2 * self.nkv) * H, L)]
-        if not c["fuse_qkv"]:
+        if c.get("group_qkv"):   # {Q, K} one launch (same format), V its own
+            qkv = [("qk", wb("q", self.nq, H) + wb("k", self.nkv, H) + (m * H + m * (self.nq + self.nkv)) * a,
+                    2 * m * (self.nq + self.nkv) * H, L),
+                   ("v", wb("v", self.nkv, H) + (m * H + m * self.nkv) * a, 2 * m * self.nkv * H, L)]
+        elif not c["fuse_qkv"]:
             qkv = [("q", wb("q", self.nq, H) + (m * H + m * self.nq) * a, 2 * m * self.nq * H, L),
                    ("k", wb("k", self.nkv, H) + (m * H + m * self.nkv) * a, 2 * m * self.nkv * H, L),
                    ("v", wb("v", self.nkv, H) + (m * H + m * self.nkv) * a, 2 * m * self.nkv * H, L)]
@@ -128,6 +134,8 @@ class Runner:
     def qkv_op(self, L):
         if self.st.cfg["fuse_qkv"]:
             self.b.qkv_forward(self.x, L["wq"], L["wk"], L["wv"], out=self.qkv)
+        elif self.st.cfg.get("group_qkv"):
+            self.b.qkv_forward(self.x, L["wq"], L["wk"], L["wv"], out=(self.qkv[0], self.kv[0], self.kv[1]))
         else:
             L["wq"].forward(self.x, out=self.qkv[0])
             L["wk"].forward(self.x, out=self.kv[0])
@@ -463,7 +471,7 @@ def main(argv=None):
         extra["llama2_7b_int4_g128_asym_bf16scale"] = decode_workload(LLAMA_ASYM, torch)
         extra["mistral_7b_int2_g64_policy"] = decode_workload(MISTRAL, torch)
         extra["mistral_7b_int2_g64_policy"]["policy"] = "q,k,o,gate,up,lm_head int2 g64 sym; wv, w2 int4 g64 sym " \
-                                                          "(llama_utils.cpp:269-287); q/k/v unfused (kv heads 8)"
+                                                          "(llama_utils.cpp:269-287); kv heads 8: {q, k} one launch, v one"
 
     if rank == 0:
         cpu = None if (args.no_cpu_baseline or world > 1) else cpu_baseline()

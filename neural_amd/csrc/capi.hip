@@ -958,15 +958,27 @@ extern "C" int nad_device_qkv_forward(const void* act, int act_dtype, const void
                                       int ldo_v, void* queue) {
   const DeviceWeight* ws[3] = {as_weight(wq), as_weight(wk), as_weight(wv)};
   if (!ws[0] || !ws[1] || !ws[2]) return -1;
-  if (!same_kind(*ws[0], *ws[1]) || !same_kind(*ws[0], *ws[2]) || ws[0]->k != k) {
-    set_err("QKV fusion needs weights of the same K, group size, bits and scale dtype");
+  if (ws[0]->k != k || ws[1]->k != k || ws[2]->k != k) {
+    set_err("QKV fusion needs three weights with K = %d", k);
     return -1;
   }
   hipStream_t st = static_cast<hipStream_t>(queue);
   float* outs[3] = {oq, okk, ov};
   int ldos[3] = {ldo_q, ldo_k, ldo_v};
-  if (m <= kSkinnyMaxM)
-    return run_skinny(act, act_dtype, lda, m, k, 3, ws, outs, ldos, kEpiNone, nullptr, 0, nullptr, 0, nullptr, 0, st);
+  if (m <= kSkinnyMaxM) {
+    // one stream launch over every run of consecutive weights of one kind (Q, K and V may differ in N; a mixed-format
+    // model such as the int2 policy's int4 wv gets {Q, K} + {V}), each output computed exactly as on its own
+    auto kin = [&](int i, int j) { return same_kind(*ws[i], *ws[j]) && ws[i]->asym == ws[j]->asym; };
+    for (int i = 0; i < 3;) {
+      int n = 1;
+      while (i + n < 3 && kin(i, i + n)) n++;
+      if (run_skinny(act, act_dtype, lda, m, k, n, ws + i, outs + i, ldos + i, kEpiNone, nullptr, 0, nullptr, 0, nullptr,
+                     0, st))
+        return -1;
+      i += n;
+    }
+    return 0;
+  }
   A16 pre;
   const A16* pp = nullptr;
   if (gemm2_ok(*ws[0], m) && !ws[0]->shuffle && !int8_compute(*ws[0])) {

@@ -339,3 +339,22 @@ def test_legacy_skinny_kernel(oracle, monkeypatch, cfg):
     ref = oracle.forward(A, blob, n, k)
     y = w.forward(torch.from_numpy(A).cuda()).cpu().numpy()
     assert _rel_err(y, ref) <= TOL_DECODE
+
+
+@pytest.mark.parametrize("m", [1, 3, 40])
+@pytest.mark.parametrize("kinds", ["int2_policy", "all_differ"])
+def test_qkv_mixed_formats(oracle, m, kinds):
+    """QKV over weights of different formats and N (the Mistral int2 policy: Q, K int2 g64, V int4 g64 with 4x fewer
+    rows): decode runs one stream launch per run of same-format weights ({Q, K} + {V}), each output exactly as alone."""
+    k = 1024
+    if kinds == "int2_policy":
+        spec = [(512, 64, S2, False), (128, 64, S2, False), (128, 64, S4, False)]
+    else:
+        spec = [(256, 128, S4, True), (128, 64, S2, False), (128, 128, S4, False)]
+    blobs = [_blob(oracle, n, k, bs, qt, F16, asym, 4, seed=70 + i) for i, (n, bs, qt, asym) in enumerate(spec)]
+    ws = [bestla.DeviceWeight(b) for b in blobs]
+    A = np.random.default_rng(m).uniform(-1, 1, size=(m, k)).astype(np.float32)
+    x = torch.from_numpy(A).cuda()
+    for y, w, b, (n, *_) in zip(bestla.qkv_forward(x, *ws), ws, blobs, spec):
+        assert _rel_err(y.cpu().numpy(), oracle.forward(A, b, n, k)) <= (TOL_DECODE if m <= 16 else TOL_PREFILL)
+        assert torch.equal(y, w.forward(x))    # fusion does not change a single bit
