@@ -330,7 +330,8 @@ static int device_cus() {
 // Fill the GemvArgs of one decode op; returns 1 when the stripe-stream GEMV handles it, 0 when not eligible.
 static int prepare_gemv(GemvArgs& a, int& waves, int& grid, int& gpt_out, const void* act, int act_t, int lda, int m,
                         int k, int nw, const DeviceWeight* const* ws, float* const* outs, const int* ldos, int epi,
-                        const float* bias, int bias_ld, const float* res, int ld_res, float* aux, int ld_aux) {
+                        const float* bias, int bias_ld, const float* res, int ld_res, float* aux, int ld_aux,
+                        bool single_op = true) {
   const DeviceWeight& w0 = *ws[0];
   for (int i = 1; i < nw; i++)
     if (ws[i]->shuffle != w0.shuffle || ws[i]->nt != w0.nt || ws[i]->ng != w0.ng || ws[i]->bits != w0.bits ||
@@ -384,6 +385,9 @@ static int prepare_gemv(GemvArgs& a, int& waves, int& grid, int& gpt_out, const 
   a.u_q = a.units / grid;
   a.u_r = a.units % grid;
   a.lean = env_int("NAD_GEMV_LEAN", 1);
+  // M = 1 single-op launches may stream 2-tile K-slices, one per wave (up to 16 waves); the chain keeps 4-tile ones
+  if (single_op)
+    gemv_lean_slices(a, w0.bits, &waves, env_int("NAD_GEMV_WAVES", 0) > 0 ? 4 : env_int("NAD_GEMV_KS", 2));
   const size_t lds = gemv_lds_layout(a, w0.bits, waves, grid);
   if (lds > 160 * 1024) return 0;
   // buffer-resource offsets are 32-bit: every tile array, scale array and the activations must stay below 2 GiB
@@ -1136,7 +1140,7 @@ extern "C" void* nad_chain_create(const nad_chain_op* ops, int n_ops, int m) {
     int wv = 0, gr = 0, gpt = 0;
     GemvArgs& a = host[size_t(i)];
     if (!prepare_gemv(a, wv, gr, gpt, o.act, o.act_dtype, o.lda, m, w0.k, nw, ws, outs, ldos, epi, o.bias,
-                      o.bias_ld, o.res, o.ld_res, o.aux, o.ld_aux) ||
+                      o.bias_ld, o.res, o.ld_res, o.aux, o.ld_aux, false) ||
         gpt != 1) {
       set_err("nad_chain_create: op %d not eligible for the stripe stream", i);
       return nullptr;

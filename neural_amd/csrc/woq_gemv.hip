@@ -110,23 +110,23 @@ __device__ __forceinline__ void cursor_stripe(const GemvArgs& a, StageCursor& c,
   c.rz = rsrc(sel3(w, a.w[0].zps, a.w[1].zps, a.w[2].zps), ns * a.ng * 16);
 }
 
-template <int GPT>
+template <int GPT, int KSN = KS>
 struct StageRegs {
-  u4_t b[KS];
-  uint32_t sc[KS][GPT];  // raw scale bits (the dword holding this lane's 16-bit scale, or the f32)
-  int zp[KS][GPT];
+  u4_t b[KSN];
+  uint32_t sc[KSN][GPT];  // raw scale bits (the dword holding this lane's 16-bit scale, or the f32)
+  int zp[KSN][GPT];
 };
 
 #ifndef NAD_TILE_AUX
 #define NAD_TILE_AUX 2  // non-temporal: the weights are read once per token
 #endif
 // Issue one stage's loads (never predicated: past-the-end tiles / stages get the out-of-range offset), then advance.
-template <int GPT, bool ASYM>
-__device__ __forceinline__ void load_stage(const GemvArgs& a, StageRegs<GPT>& S, StageCursor& c, int nv, int nsl,
+template <int GPT, bool ASYM, int KSN = KS>
+__device__ __forceinline__ void load_stage(const GemvArgs& a, StageRegs<GPT, KSN>& S, StageCursor& c, int nv, int nsl,
                                            int wave, int NW, int v0, int lane, int vs) {
   if (c.j >= nv) {  // past this wave's last stage: the same loads, all out of range, no bookkeeping
 #pragma unroll
-    for (int i = 0; i < KS; i++) {
+    for (int i = 0; i < KSN; i++) {
       S.b[i] = __builtin_bit_cast(u4_t, __builtin_amdgcn_raw_buffer_load_b128(c.rt, kOOB, 0, NAD_TILE_AUX));
 #pragma unroll
       for (int g = 0; g < GPT; g++) {
@@ -138,11 +138,11 @@ __device__ __forceinline__ void load_stage(const GemvArgs& a, StageRegs<GPT>& S,
   }
   const int nt = a.nt, ng = a.ng;
   const bool over = false;
-  const int t0 = c.q * KS;
+  const int t0 = c.q * KSN;
   const int tb = (c.s * nt + t0) * 1024;
   const int rowb = a.scale_t == kScaleF32 ? 64 : 32;  // bytes per scale row of 16
 #pragma unroll
-  for (int i = 0; i < KS; i++) {
+  for (int i = 0; i < KSN; i++) {
     const bool live = !over && t0 + i < nt;
     S.b[i] = __builtin_bit_cast(u4_t, __builtin_amdgcn_raw_buffer_load_b128(c.rt, (live ? tb + i * 1024 : kOOB) + lane * 16, 0, NAD_TILE_AUX));
 #pragma unroll
@@ -555,25 +555,29 @@ __global__ __launch_bounds__(gemv_max_threads<GPT>()) void woq_gemv_kernel(GemvA
 // counts (no integer division), and each wave stages only ITS K-slices of the activations into its own LDS rows
 // (hi / lo fp16, plus a zero row for the MFMA rows M = 1 leaves empty), so nothing waits on a block-wide barrier before
 // the stream; the one barrier is the final cross-wave reduction.
-constexpr int kLeanSpw = 2;  // K-slices per wave it stages (K <= waves * 2 * KS * KT)
-// per wave: a zero row, then per slice {hi, lo} rows of KS * KT fp16 each
-constexpr int lean_row_bytes(int bits) { return KS * (bits == 4 ? 128 : 256) * 2; }
-constexpr int lean_wave_lds(int bits) { return lean_row_bytes(bits) * (1 + 2 * kLeanSpw); }
+constexpr int kLeanSpw = 2;  // K-slices per wave it stages (K <= waves * 2 * ks * KT)
+// per wave: a zero row, then per slice {hi, lo} rows of ks * KT fp16 each
+constexpr int lean_row_bytes(int bits, int ks) { return ks * (bits == 4 ? 128 : 256) * 2; }
+constexpr int lean_wave_lds(int bits, int ks) { return lean_row_bytes(bits, ks) * (1 + 2 * kLeanSpw); }
+static int lean_ks(const GemvArgs& a) { return a.lean_ks == 2 ? 2 : KS; }
 
 static bool lean_ok(const GemvArgs& a, int bits, int waves) {
   int tpg = 0;
-  const int nsl = (a.nt + KS - 1) / KS;
+  const int ks = lean_ks(a);
+  const int nsl = (a.nt + ks - 1) / ks;
   const int gpt = gemv_groups_per_tile(bits, a.nt, a.ng, a.bs, &tpg);
   const bool inst = bits == 4 ? (gpt == 1 || gpt == 2) : (bits == 2 && (gpt == 1 || gpt == 2 || (gpt == 4 && !a.asym)));
   return a.lean && a.M == 1 && inst && a.a_fast && nsl <= waves * kLeanSpw;
 }
 
-template <int BITS, int GPT, int AT, bool ASYM>
+template <int BITS, int GPT, int AT, bool ASYM, int KSN>
 __global__ __launch_bounds__(gemv_max_threads<GPT>()) void woq_gemv_m1_kernel(GemvArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int KT = BITS == 4 ? 128 : 256, SPT = KT / 32, SPG = SPT / GPT;
-  constexpr int RB = lean_row_bytes(BITS);  // one fp16 row of a slice
-  constexpr int UPL = KS * KT / 8 / 64;      // 8-element staging units per lane per slice
+  constexpr int RB = lean_row_bytes(BITS, KSN);  // one fp16 row of a slice
+  constexpr int UNITS = KSN * KT / 8;             // 8-element staging units per slice
+  constexpr int UPL = UNITS >= 64 ? UNITS / 64 : 1;  // ... per lane (2-tile int4 slices: lanes < 32 hold one)
+  constexpr bool PART = UNITS < 64;
   constexpr int BIAS = BITS == 4 ? 8 : 2;
   constexpr int ESZ = AT == kActF32 ? 4 : 2;
   constexpr bool HL = AT != kActF16;  // fp32 / bf16 rows split into fp16 hi + lo (MFMA rows 0 and 8)
@@ -581,7 +585,8 @@ __global__ __launch_bounds__(gemv_max_threads<GPT>()) void woq_gemv_m1_kernel(Ge
   const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));
   const int NW = __builtin_amdgcn_readfirstlane(int(blockDim.x >> 6));
   const int nt = a.nt;
-  const int nsl = (nt + KS - 1) / KS;
+  const int nsl = (nt + KSN - 1) / KSN;
+  const bool ulane = !PART || lane < UNITS;  // this lane holds a staging unit of each slice
   NAD_TRACE(0);
   const int bid = blockIdx.x;
   const int u0 = bid * a.u_q + min(bid, a.u_r);
@@ -596,8 +601,8 @@ __global__ __launch_bounds__(gemv_max_threads<GPT>()) void woq_gemv_m1_kernel(Ge
   uint4 x[kLeanSpw * UPL][2];
 #pragma unroll
   for (int j = 0; j < kLeanSpw * UPL; j++) {
-    const int q = wave + (j / UPL) * NW, k = q * (KS * KT) + ((j % UPL) * 64 + lane) * 8;
-    const int off = (q < nsl && k < a.K) ? k * ESZ : kOOB;
+    const int q = wave + (j / UPL) * NW, k = q * (KSN * KT) + ((j % UPL) * 64 + lane) * 8;
+    const int off = (ulane && q < nsl && k < a.K) ? k * ESZ : kOOB;
     x[j][0] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(ra, off, 0, 0));
     if constexpr (ESZ == 4) x[j][1] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(ra, off + 16, 0, 0));
   }
@@ -610,16 +615,18 @@ __global__ __launch_bounds__(gemv_max_threads<GPT>()) void woq_gemv_m1_kernel(Ge
   lc.rs = lc.rt;
   lc.rz = lc.rt;
   if (!idle && nv > 0) cursor_stripe(a, lc, v0);
-  StageRegs<GPT> S0, S1, S2;
-  load_stage<GPT, ASYM>(a, S0, lc, nv, nsl, wave, NW, v0, lane, vs);
+  StageRegs<GPT, KSN> S0, S1, S2;
+  load_stage<GPT, ASYM, KSN>(a, S0, lc, nv, nsl, wave, NW, v0, lane, vs);
   NAD_TRACE(4);
 
   // 2) stage the slices into this wave's rows (LDS ops of one wave complete in order: no barrier)
-  char* wrow = smem + wave * lean_wave_lds(BITS);
+  char* wrow = smem + wave * lean_wave_lds(BITS, KSN);
 #pragma unroll
-  for (int u = 0; u < UPL; u++) *reinterpret_cast<uint4*>(wrow + (u * 64 + lane) * 16) = make_uint4(0u, 0u, 0u, 0u);
+  for (int u = 0; u < UPL; u++)
+    if (ulane) *reinterpret_cast<uint4*>(wrow + (u * 64 + lane) * 16) = make_uint4(0u, 0u, 0u, 0u);
 #pragma unroll
   for (int j = 0; j < kLeanSpw * UPL; j++) {
+    if (!ulane) break;
     h8_t hi, lo;
     if constexpr (AT == kActF16) {
       hi = __builtin_bit_cast(h8_t, x[j][0]);
@@ -636,8 +643,8 @@ __global__ __launch_bounds__(gemv_max_threads<GPT>()) void woq_gemv_m1_kernel(Ge
     *reinterpret_cast<h8_t*>(row) = hi;
     if constexpr (HL) *reinterpret_cast<h8_t*>(row + RB) = lo;
   }
-  load_stage<GPT, ASYM>(a, S1, lc, nv, nsl, wave, NW, v0, lane, vs);
-  load_stage<GPT, ASYM>(a, S2, lc, nv, nsl, wave, NW, v0, lane, vs);
+  load_stage<GPT, ASYM, KSN>(a, S1, lc, nv, nsl, wave, NW, v0, lane, vs);
+  load_stage<GPT, ASYM, KSN>(a, S2, lc, nv, nsl, wave, NW, v0, lane, vs);
   NAD_TRACE(1);
 
   // 3) the stream: MFMA row 0 = hi (lane m 0), row 8 = lo (lane m 8), every other row reads the zero row
@@ -656,15 +663,15 @@ __global__ __launch_bounds__(gemv_max_threads<GPT>()) void woq_gemv_m1_kernel(Ge
   f4_t acc = {0.f, 0.f, 0.f, 0.f};
   int cj = idle ? nv : 0, cq = wave, cs = 0;  // compute cursor: local stripe, K-slice, slice ordinal of this wave
 
-  auto compute_stage = [&](const StageRegs<GPT>& S) {
+  auto compute_stage = [&](const StageRegs<GPT, KSN>& S) {
     if (cj >= nv) return;
     const char* ab = abase + cs * slice_step;
-    f4_t accg[KS];
+    f4_t accg[KSN];
 #pragma unroll
     for (int d = 0; d < SPT; d++) {
       const int g = GPT == 1 ? 0 : d / SPG;
 #pragma unroll
-      for (int i = 0; i < KS; i++) {
+      for (int i = 0; i < KSN; i++) {
         h8_t bf;
         if constexpr (BITS == 4) {
           if constexpr (ASYM) {
@@ -682,7 +689,7 @@ __global__ __launch_bounds__(gemv_max_threads<GPT>()) void woq_gemv_m1_kernel(Ge
       }
       if ((d + 1) % SPG == 0) {  // group end: scale each tile's group partial into the stripe sum, in tile order
 #pragma unroll
-        for (int i = 0; i < KS; i++) acc += accg[i] * scale_bits_to_f32(S.sc[i][g], a.scale_t, ssh);
+        for (int i = 0; i < KSN; i++) acc += accg[i] * scale_bits_to_f32(S.sc[i][g], a.scale_t, ssh);
       }
     }
     cq += NW;
@@ -700,11 +707,11 @@ __global__ __launch_bounds__(gemv_max_threads<GPT>()) void woq_gemv_m1_kernel(Ge
 
   while (cj < nv) {
     compute_stage(S0);
-    load_stage<GPT, ASYM>(a, S0, lc, nv, nsl, wave, NW, v0, lane, vs);
+    load_stage<GPT, ASYM, KSN>(a, S0, lc, nv, nsl, wave, NW, v0, lane, vs);
     compute_stage(S1);
-    load_stage<GPT, ASYM>(a, S1, lc, nv, nsl, wave, NW, v0, lane, vs);
+    load_stage<GPT, ASYM, KSN>(a, S1, lc, nv, nsl, wave, NW, v0, lane, vs);
     compute_stage(S2);
-    load_stage<GPT, ASYM>(a, S2, lc, nv, nsl, wave, NW, v0, lane, vs);
+    load_stage<GPT, ASYM, KSN>(a, S2, lc, nv, nsl, wave, NW, v0, lane, vs);
   }
   NAD_TRACE_MAX(2);
   __syncthreads();
@@ -796,9 +803,9 @@ static hipError_t gemv_launch4(const GemvArgs& a, dim3 g, dim3 b, size_t lds, hi
   return hipGetLastError();
 }
 
-template <int BITS, int GPT, int AT, bool ASYM>
-static hipError_t gemv_m1_launch4(const GemvArgs& a, dim3 g, dim3 b, size_t lds, hipStream_t st) {
-  auto k = woq_gemv_m1_kernel<BITS, GPT, AT, ASYM>;
+template <int BITS, int GPT, int AT, bool ASYM, int KSN>
+static hipError_t gemv_m1_launch5(const GemvArgs& a, dim3 g, dim3 b, size_t lds, hipStream_t st) {
+  auto k = woq_gemv_m1_kernel<BITS, GPT, AT, ASYM, KSN>;
   static bool attr_set = false;
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -808,6 +815,11 @@ static hipError_t gemv_m1_launch4(const GemvArgs& a, dim3 g, dim3 b, size_t lds,
   }
   hipLaunchKernelGGL(k, g, b, lds, st, a);
   return hipGetLastError();
+}
+template <int BITS, int GPT, int AT, bool ASYM>
+static hipError_t gemv_m1_launch4(const GemvArgs& a, dim3 g, dim3 b, size_t lds, hipStream_t st) {
+  return a.lean_ks == 2 ? gemv_m1_launch5<BITS, GPT, AT, ASYM, 2>(a, g, b, lds, st)
+                        : gemv_m1_launch5<BITS, GPT, AT, ASYM, KS>(a, g, b, lds, st);
 }
 template <int BITS, int GPT>
 static hipError_t gemv_m1_launch2(const GemvArgs& a, dim3 g, dim3 b, size_t lds, hipStream_t st) {
@@ -861,7 +873,7 @@ static hipError_t gemv_launch1(const GemvArgs& a, int hilo, int gpt, dim3 g, dim
 size_t gemv_lds_layout(GemvArgs& a, int bits, int waves, int grid) {
   if (lean_ok(a, bits, waves)) {  // woq_gemv_m1_kernel: per-wave rows, then the partial slots [nv][waves][16]
     const int upw = (a.units + grid - 1) / grid;
-    a.part_off = waves * lean_wave_lds(bits);
+    a.part_off = waves * lean_wave_lds(bits, lean_ks(a));
     return size_t(a.part_off) + size_t(upw) * (a.dual ? 2 : 1) * waves * 16 * 4;
   }
   const int KT = bits == 4 ? 128 : (bits == 2 ? 256 : 64);
@@ -882,6 +894,25 @@ int gemv_waves(int bits, int nt, int ng, int bs) {
   const int nsl = (nt + KS - 1) / KS;
   const int spw = (nsl + maxw - 1) / maxw;  // slices per wave
   return (nsl + spw - 1) / spw;
+}
+
+void gemv_lean_slices(GemvArgs& a, int bits, int* waves, int ks_pref) {
+  a.lean_ks = KS;
+  // bench (graph-replayed token): Llama int4 g128 837 -> 853 tok/s, Mistral int2 policy 586 -> 633 (its int2 K = 4096
+  // launches go from 4 waves to 8); NAD_GEMV_KS=4 keeps 4-tile slices everywhere
+  if (ks_pref != 2 || a.M != 1 || !a.lean) return;
+  int tpg = 0;
+  const int gpt = gemv_groups_per_tile(bits, a.nt, a.ng, a.bs, &tpg);
+  const int maxw = gpt > 1 ? 8 : 16;
+  const int nsl2 = (a.nt + 1) / 2;
+  if (nsl2 > maxw || nsl2 <= *waves) return;  // 2-tile slices only where each wave gets one and there are more waves
+  if (!lean_ok(a, bits, *waves)) return;        // the 4-tile launch would not take the M = 1 kernel either
+  a.lean_ks = 2;
+  if (!lean_ok(a, bits, nsl2)) {
+    a.lean_ks = KS;
+    return;
+  }
+  *waves = nsl2;
 }
 
 int gemv_groups_per_tile(int bits, int nt, int ng, int bs, int* tpg) {

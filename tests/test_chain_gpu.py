@@ -12,6 +12,13 @@ torch = pytest.importorskip("torch")
 
 pytestmark = pytest.mark.gpu
 
+
+@pytest.fixture(autouse=True)
+def _four_tile_slices(monkeypatch):
+    # the chain streams 4-tile K-slices; the per-op M = 1 launch takes 2-tile slices at K <= 16 tiles (a different
+    # summation order), so the bit-identity reference runs the per-op launches with 4-tile slices
+    monkeypatch.setenv("NAD_GEMV_KS", "4")
+
 from neural_amd import bestla  # noqa: E402
 from neural_amd.bestla import CHAIN_GATE_UP, CHAIN_LINEAR, CHAIN_QKV, EPI_RES_ADD  # noqa: E402
 

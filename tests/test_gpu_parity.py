@@ -303,6 +303,38 @@ def test_gemv_stream_geometry(oracle, monkeypatch, cfg, geom):
     assert _rel_err(y, ref) <= TOL_DECODE
 
 
+M1_SLICES = [
+    # n, k, bs, qtype, stype, asym, act dtype: M = 1 launches that take 2-tile K-slices (K <= 16 tiles per wave count)
+    (4096, 4096, 128, S4, F16, False, "f32"),
+    (1000, 4096, 256, S4, BF16, True, "f16"),
+    (320, 2048, 64, S4, F32, True, "bf16"),  # 2 groups per tile, 8 waves
+    (520, 3968, 128, S4, F16, False, "f32"),  # K tail: 31 tiles, the last wave's slice half out of range
+    (1024, 4096, 64, S2, F16, False, "f16"),  # int2 g64 (Mistral): 4 groups per tile, 8 waves instead of 4
+    (264, 2048, 128, S2, BF16, True, "f32"),
+]
+
+
+@pytest.mark.parametrize("cfg", M1_SLICES)
+@pytest.mark.parametrize("grid", [None, "1", "7"])
+def test_gemv_m1_two_tile_slices(oracle, monkeypatch, cfg, grid):
+    """M = 1 with 2-tile K-slices (one per wave, up to 16 waves) against the oracle,
+    and within 1e-6 of the 4-tile-slice launch (NAD_GEMV_KS=4; only the partial-sum order differs).  Forced grids make
+    workgroups stream many stripes through the 3-stage ring."""
+    n, k, bs, qt, st, asym, adt = cfg
+    if grid:
+        monkeypatch.setenv("NAD_GEMV_GRID", grid)
+    blob = _blob(oracle, n, k, bs, qt, st, asym, 4, seed=n + k)
+    w = bestla.DeviceWeight(blob)
+    A = np.random.default_rng(k).uniform(-0.5, 0.5, size=(1, k)).astype(np.float32)
+    xa = torch.from_numpy(A).cuda().to(dict(f32=torch.float32, f16=torch.float16, bf16=torch.bfloat16)[adt])
+    ref = oracle.forward(xa.float().cpu().numpy(), blob, n, k)
+    y2 = w.forward(xa).cpu().numpy()
+    monkeypatch.setenv("NAD_GEMV_KS", "4")
+    y4 = w.forward(xa).cpu().numpy()
+    assert _rel_err(y2, ref) <= TOL_DECODE
+    assert _rel_err(y2, y4) <= 1e-6
+
+
 @pytest.mark.parametrize("geom", [(None, None), ("2", "3"), ("5", "16")])
 def test_gemv_stream_fused(oracle, monkeypatch, geom):
     """QKV (three weights in one stream) and the dual gate/up stream with SiLU*mul under forced geometries."""
