@@ -555,11 +555,12 @@ __global__ __launch_bounds__(gemv_max_threads<GPT>()) void woq_gemv_kernel(GemvA
 // counts (no integer division), and each wave stages only ITS K-slices of the activations into its own LDS rows
 // (hi / lo fp16, plus a zero row for the MFMA rows M = 1 leaves empty), so nothing waits on a block-wide barrier before
 // the stream; the one barrier is the final cross-wave reduction.
-constexpr int kLeanSpw = 2;  // K-slices per wave it stages (K <= waves * 2 * ks * KT)
+// K-slices per wave it stages: 2 (K <= waves * 2 * ks * KT), or 4 for long K (Mistral's down, K = 14336 at 7 waves)
 // per wave: a zero row, then per slice {hi, lo} rows of ks * KT fp16 each
 constexpr int lean_row_bytes(int bits, int ks) { return ks * (bits == 4 ? 128 : 256) * 2; }
-constexpr int lean_wave_lds(int bits, int ks) { return lean_row_bytes(bits, ks) * (1 + 2 * kLeanSpw); }
+constexpr int lean_wave_lds(int bits, int ks, int spw) { return lean_row_bytes(bits, ks) * (1 + 2 * spw); }
 static int lean_ks(const GemvArgs& a) { return a.lean_ks == 2 ? 2 : KS; }
+static int lean_spw(const GemvArgs& a) { return a.lean_spw == 4 ? 4 : 2; }
 
 static bool lean_ok(const GemvArgs& a, int bits, int waves) {
   int tpg = 0;
@@ -567,10 +568,10 @@ static bool lean_ok(const GemvArgs& a, int bits, int waves) {
   const int nsl = (a.nt + ks - 1) / ks;
   const int gpt = gemv_groups_per_tile(bits, a.nt, a.ng, a.bs, &tpg);
   const bool inst = bits == 4 ? (gpt == 1 || gpt == 2) : (bits == 2 && (gpt == 1 || gpt == 2 || (gpt == 4 && !a.asym)));
-  return a.lean && a.M == 1 && inst && a.a_fast && nsl <= waves * kLeanSpw;
+  return a.lean && a.M == 1 && inst && a.a_fast && nsl <= waves * lean_spw(a);
 }
 
-template <int BITS, int GPT, int AT, bool ASYM, int KSN>
+template <int BITS, int GPT, int AT, bool ASYM, int KSN, int SPW>
 __global__ __launch_bounds__(gemv_max_threads<GPT>()) void woq_gemv_m1_kernel(GemvArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int KT = BITS == 4 ? 128 : 256, SPT = KT / 32, SPG = SPT / GPT;
@@ -598,9 +599,9 @@ __global__ __launch_bounds__(gemv_max_threads<GPT>()) void woq_gemv_m1_kernel(Ge
 
   // 1) this wave's activation slices (q = wave + j NW), then the first weight stage
   const auto ra = rsrc(a.A, a.K * ESZ);
-  uint4 x[kLeanSpw * UPL][2];
+  uint4 x[SPW * UPL][2];
 #pragma unroll
-  for (int j = 0; j < kLeanSpw * UPL; j++) {
+  for (int j = 0; j < SPW * UPL; j++) {
     const int q = wave + (j / UPL) * NW, k = q * (KSN * KT) + ((j % UPL) * 64 + lane) * 8;
     const int off = (ulane && q < nsl && k < a.K) ? k * ESZ : kOOB;
     x[j][0] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(ra, off, 0, 0));
@@ -620,12 +621,12 @@ __global__ __launch_bounds__(gemv_max_threads<GPT>()) void woq_gemv_m1_kernel(Ge
   NAD_TRACE(4);
 
   // 2) stage the slices into this wave's rows (LDS ops of one wave complete in order: no barrier)
-  char* wrow = smem + wave * lean_wave_lds(BITS, KSN);
+  char* wrow = smem + wave * lean_wave_lds(BITS, KSN, SPW);
 #pragma unroll
   for (int u = 0; u < UPL; u++)
     if (ulane) *reinterpret_cast<uint4*>(wrow + (u * 64 + lane) * 16) = make_uint4(0u, 0u, 0u, 0u);
 #pragma unroll
-  for (int j = 0; j < kLeanSpw * UPL; j++) {
+  for (int j = 0; j < SPW * UPL; j++) {
     if (!ulane) break;
     h8_t hi, lo;
     if constexpr (AT == kActF16) {
@@ -803,9 +804,9 @@ static hipError_t gemv_launch4(const GemvArgs& a, dim3 g, dim3 b, size_t lds, hi
   return hipGetLastError();
 }
 
-template <int BITS, int GPT, int AT, bool ASYM, int KSN>
+template <int BITS, int GPT, int AT, bool ASYM, int KSN, int SPW>
 static hipError_t gemv_m1_launch5(const GemvArgs& a, dim3 g, dim3 b, size_t lds, hipStream_t st) {
-  auto k = woq_gemv_m1_kernel<BITS, GPT, AT, ASYM, KSN>;
+  auto k = woq_gemv_m1_kernel<BITS, GPT, AT, ASYM, KSN, SPW>;
   static bool attr_set = false;
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -818,8 +819,9 @@ static hipError_t gemv_m1_launch5(const GemvArgs& a, dim3 g, dim3 b, size_t lds,
 }
 template <int BITS, int GPT, int AT, bool ASYM>
 static hipError_t gemv_m1_launch4(const GemvArgs& a, dim3 g, dim3 b, size_t lds, hipStream_t st) {
-  return a.lean_ks == 2 ? gemv_m1_launch5<BITS, GPT, AT, ASYM, 2>(a, g, b, lds, st)
-                        : gemv_m1_launch5<BITS, GPT, AT, ASYM, KS>(a, g, b, lds, st);
+  if (a.lean_ks == 2) return gemv_m1_launch5<BITS, GPT, AT, ASYM, 2, 2>(a, g, b, lds, st);
+  return a.lean_spw == 4 ? gemv_m1_launch5<BITS, GPT, AT, ASYM, KS, 4>(a, g, b, lds, st)
+                         : gemv_m1_launch5<BITS, GPT, AT, ASYM, KS, 2>(a, g, b, lds, st);
 }
 template <int BITS, int GPT>
 static hipError_t gemv_m1_launch2(const GemvArgs& a, dim3 g, dim3 b, size_t lds, hipStream_t st) {
@@ -873,7 +875,7 @@ static hipError_t gemv_launch1(const GemvArgs& a, int hilo, int gpt, dim3 g, dim
 size_t gemv_lds_layout(GemvArgs& a, int bits, int waves, int grid) {
   if (lean_ok(a, bits, waves)) {  // woq_gemv_m1_kernel: per-wave rows, then the partial slots [nv][waves][16]
     const int upw = (a.units + grid - 1) / grid;
-    a.part_off = waves * lean_wave_lds(bits, lean_ks(a));
+    a.part_off = waves * lean_wave_lds(bits, lean_ks(a), lean_spw(a));
     return size_t(a.part_off) + size_t(upw) * (a.dual ? 2 : 1) * waves * 16 * 4;
   }
   const int KT = bits == 4 ? 128 : (bits == 2 ? 256 : 64);
@@ -898,6 +900,12 @@ int gemv_waves(int bits, int nt, int ng, int bs) {
 
 void gemv_lean_slices(GemvArgs& a, int bits, int* waves, int ks_pref) {
   a.lean_ks = KS;
+  a.lean_spw = 2;
+  if (a.M == 1 && a.lean && (a.nt + KS - 1) / KS > 2 * *waves) {  // long K: up to 4 slices per wave
+    a.lean_spw = 4;
+    if (!lean_ok(a, bits, *waves)) a.lean_spw = 2;
+    return;
+  }
   // bench (graph-replayed token): Llama int4 g128 837 -> 853 tok/s, Mistral int2 policy 586 -> 633 (its int2 K = 4096
   // launches go from 4 waves to 8); NAD_GEMV_KS=4 keeps 4-tile slices everywhere
   if (ks_pref != 2 || a.M != 1 || !a.lean) return;

@@ -120,6 +120,7 @@ struct GemvArgs {
   int u_q, u_r;         // units per workgroup: u_q, one more for the first u_r workgroups (host-divided)
   int lean;             // M = 1 int4 single-group-per-tile launches may take woq_gemv_m1_kernel (NAD_GEMV_LEAN)
   int lean_ks;          // woq_gemv_m1_kernel: K tiles per K-slice (4, or 2 where that gives each of up to 16 waves one slice)
+  int lean_spw;         // woq_gemv_m1_kernel: K-slices per wave at most (2, or 4 for long K)
   SkinnyWeight w[3];
 };
 

@@ -304,13 +304,17 @@ def test_gemv_stream_geometry(oracle, monkeypatch, cfg, geom):
 
 
 M1_SLICES = [
-    # n, k, bs, qtype, stype, asym, act dtype: M = 1 launches that take 2-tile K-slices (K <= 16 tiles per wave count)
+    # n, k, bs, qtype, stype, asym, act dtype: M = 1 launches of woq_gemv_m1_kernel with 2-tile K-slices (more waves)
     (4096, 4096, 128, S4, F16, False, "f32"),
     (1000, 4096, 256, S4, BF16, True, "f16"),
     (320, 2048, 64, S4, F32, True, "bf16"),  # 2 groups per tile, 8 waves
     (520, 3968, 128, S4, F16, False, "f32"),  # K tail: 31 tiles, the last wave's slice half out of range
     (1024, 4096, 64, S2, F16, False, "f16"),  # int2 g64 (Mistral): 4 groups per tile, 8 waves instead of 4
     (264, 2048, 128, S2, BF16, True, "f32"),
+    # long K: up to 4 slices per wave (Mistral's down, 4096 x 14336 int4 g64, at 7 waves)
+    (256, 14336, 64, S4, F16, False, "f16"),
+    (200, 12288, 64, S4, BF16, True, "f32"),
+    (128, 20480, 64, S2, F16, False, "bf16"),
 ]
 
 
