@@ -559,7 +559,12 @@ __global__ __launch_bounds__(gemv_max_threads<GPT>()) void woq_gemv_kernel(GemvA
 // per wave: a zero row, then per slice {hi, lo} rows of ks * KT fp16 each
 constexpr int lean_row_bytes(int bits, int ks) { return ks * (bits == 4 ? 128 : 256) * 2; }
 constexpr int lean_wave_lds(int bits, int ks, int spw) { return lean_row_bytes(bits, ks) * (1 + 2 * spw); }
-static int lean_ks(const GemvArgs& a) { return a.lean_ks == 2 ? 2 : KS; }
+static int lean_ks(const GemvArgs& a) { return a.lean_ks == 1 || a.lean_ks == 2 ? a.lean_ks : KS; }
+// narrow slices carry few stage registers: those launches may run 16 waves whatever the groups per tile
+template <int GPT, int KSN>
+constexpr int m1_max_threads() {
+  return GPT == 1 || KSN <= 2 ? 1024 : 512;
+}
 static int lean_spw(const GemvArgs& a) { return a.lean_spw == 4 ? 4 : 2; }
 
 static bool lean_ok(const GemvArgs& a, int bits, int waves) {
@@ -572,7 +577,7 @@ static bool lean_ok(const GemvArgs& a, int bits, int waves) {
 }
 
 template <int BITS, int GPT, int AT, bool ASYM, int KSN, int SPW>
-__global__ __launch_bounds__(gemv_max_threads<GPT>()) void woq_gemv_m1_kernel(GemvArgs a) {
+__global__ __launch_bounds__((m1_max_threads<GPT, KSN>())) void woq_gemv_m1_kernel(GemvArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int KT = BITS == 4 ? 128 : 256, SPT = KT / 32, SPG = SPT / GPT;
   constexpr int RB = lean_row_bytes(BITS, KSN);  // one fp16 row of a slice
@@ -819,6 +824,7 @@ static hipError_t gemv_m1_launch5(const GemvArgs& a, dim3 g, dim3 b, size_t lds,
 }
 template <int BITS, int GPT, int AT, bool ASYM>
 static hipError_t gemv_m1_launch4(const GemvArgs& a, dim3 g, dim3 b, size_t lds, hipStream_t st) {
+  if (a.lean_ks == 1) return gemv_m1_launch5<BITS, GPT, AT, ASYM, 1, 2>(a, g, b, lds, st);
   if (a.lean_ks == 2) return gemv_m1_launch5<BITS, GPT, AT, ASYM, 2, 2>(a, g, b, lds, st);
   return a.lean_spw == 4 ? gemv_m1_launch5<BITS, GPT, AT, ASYM, KS, 4>(a, g, b, lds, st)
                          : gemv_m1_launch5<BITS, GPT, AT, ASYM, KS, 2>(a, g, b, lds, st);
@@ -906,21 +912,20 @@ void gemv_lean_slices(GemvArgs& a, int bits, int* waves, int ks_pref) {
     if (!lean_ok(a, bits, *waves)) a.lean_spw = 2;
     return;
   }
-  // bench (graph-replayed token): Llama int4 g128 837 -> 853 tok/s, Mistral int2 policy 586 -> 633 (its int2 K = 4096
-  // launches go from 4 waves to 8); NAD_GEMV_KS=4 keeps 4-tile slices everywhere
-  if (ks_pref != 2 || a.M != 1 || !a.lean) return;
-  int tpg = 0;
-  const int gpt = gemv_groups_per_tile(bits, a.nt, a.ng, a.bs, &tpg);
-  const int maxw = gpt > 1 ? 8 : 16;
-  const int nsl2 = (a.nt + 1) / 2;
-  if (nsl2 > maxw || nsl2 <= *waves) return;  // 2-tile slices only where each wave gets one and there are more waves
-  if (!lean_ok(a, bits, *waves)) return;        // the 4-tile launch would not take the M = 1 kernel either
-  a.lean_ks = 2;
-  if (!lean_ok(a, bits, nsl2)) {
+  // Slices of 1 or 2 tiles, one per wave, up to 16 waves (the narrowest width that fits).  bench (graph-replayed
+  // token): 2-tile slices took Llama int4 g128 837 -> 853 tok/s and the Mistral int2 policy 586 -> 633 (its int2
+  // K = 4096 launches from 4 waves to 8).  NAD_GEMV_KS: 2 = 1- or 2-tile, 3 = 2-tile only, 4 = 4-tile everywhere.
+  if ((ks_pref != 2 && ks_pref != 3) || a.M != 1 || !a.lean) return;
+  const int ks = a.nt <= 16 && ks_pref == 2 ? 1 : 2;
+  const int nsl = (a.nt + ks - 1) / ks;
+  if (nsl > 16 || nsl <= *waves) return;  // narrow slices only where each wave gets one and there are more waves
+  if (!lean_ok(a, bits, *waves)) return;  // the 4-tile launch would not take the M = 1 kernel either
+  a.lean_ks = ks;
+  if (!lean_ok(a, bits, nsl)) {
     a.lean_ks = KS;
     return;
   }
-  *waves = nsl2;
+  *waves = nsl;
 }
 
 int gemv_groups_per_tile(int bits, int nt, int ng, int bs, int* tpg) {

@@ -119,7 +119,7 @@ struct GemvArgs {
   const float* norm_w;  //   optional per-k weight (null = 1)
   int u_q, u_r;         // units per workgroup: u_q, one more for the first u_r workgroups (host-divided)
   int lean;             // M = 1 int4 single-group-per-tile launches may take woq_gemv_m1_kernel (NAD_GEMV_LEAN)
-  int lean_ks;          // woq_gemv_m1_kernel: K tiles per K-slice (4, or 2 where that gives each of up to 16 waves one slice)
+  int lean_ks;          // woq_gemv_m1_kernel: K tiles per K-slice (4, or 1 / 2 where that gives each of up to 16 waves one)
   int lean_spw;         // woq_gemv_m1_kernel: K-slices per wave at most (2, or 4 for long K)
   SkinnyWeight w[3];
 };
@@ -192,7 +192,8 @@ int gemv_groups_per_tile(int bits, int nt, int ng, int bs, int* tpg);
 size_t gemv_lds_layout(GemvArgs& a, int bits, int waves, int grid);
 int gemv_waves(int bits, int nt, int ng, int bs);
 // M = 1: K-slices of 2 tiles for woq_gemv_m1_kernel when that gives more waves (one slice each); sets a.lean_ks and
-// *waves when taken (ks_pref = NAD_GEMV_KS: 2 wherever that gives more waves, 4 never)
+// *waves when taken (ks_pref = NAD_GEMV_KS: 2 = 1- or 2-tile slices wherever that gives more waves, 3 = 2-tile only,
+// 4 = never)
 void gemv_lean_slices(GemvArgs& a, int bits, int* waves, int ks_pref);
 hipError_t launch_gemv(const GemvArgs& a, int bits, int waves, int grid, size_t lds, hipStream_t stream);
 
