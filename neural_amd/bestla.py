@@ -30,17 +30,17 @@ COMP_UNDEF, COMP_F32, COMP_BF16, COMP_F16, COMP_INT8 = 0, 1, 2, 3, 4
 ACT_F32, ACT_F16, ACT_BF16 = 0, 1, 2
 EPI_NONE, EPI_BIAS, EPI_SILU_MUL, EPI_GELU_MUL, EPI_GELU, EPI_ADD_GELU, EPI_SILU, EPI_RES_ADD = range(8)
 
-S3, S5, S6, S7 = 3 | 0x100, 5 | 0x100, 6 | 0x100, 7 | 0x100
+S1, S3, S5, S6, S7 = 1 | 0x100, 3 | 0x100, 5 | 0x100, 6 | 0x100, 7 | 0x100
 F4_E2M1, F4_BNB, F4_NF4 = 4, 4 | (1 << 16), 4 | (2 << 16)
 F8_E4M3, F8_E5M2, F8_E8M0 = 8, 8 | (1 << 16), 8 | (3 << 16)
 # quant_config.h:22-57 parse_bits ("int1" is not supported here); "fp4_bnb" names the F4_BNB type the reference packs
 # but has no command-line name for
-_WEIGHT_DTYPES = {"int4": S4, "int8": S8, "int2": S2, "int3": S3, "int5": S5, "int6": S6, "int7": S7,
+_WEIGHT_DTYPES = {"int4": S4, "int8": S8, "int2": S2, "int1": S1, "int3": S3, "int5": S5, "int6": S6, "int7": S7,
                   "fp4_e2m1": F4_E2M1, "fp4": F4_E2M1, "nf4": F4_NF4, "fp4_bnb": F4_BNB,
                   "fp8_e4m3": F8_E4M3, "fp8": F8_E4M3, "fp8_e5m2": F8_E5M2}
 _SCALE_DTYPES = {"fp32": F32, "bf16": BF16, "fp16": F16, "fp8": F8_E8M0}
 _COMP = {"int8": COMP_INT8, "bf16": COMP_BF16, "fp16": COMP_F16, "fp32": COMP_F32, "auto": COMP_UNDEF}
-BITS = {S4: 4, S2: 2, S8: 8, S3: 3, S5: 5, S6: 6, S7: 7, F4_E2M1: 4, F4_BNB: 4, F4_NF4: 4, F8_E4M3: 8, F8_E5M2: 8}
+BITS = {S4: 4, S2: 2, S8: 8, S1: 1, S3: 3, S5: 5, S6: 6, S7: 7, F4_E2M1: 4, F4_BNB: 4, F4_NF4: 4, F8_E4M3: 8, F8_E5M2: 8}
 
 
 def _ptr(a):

@@ -262,8 +262,8 @@ bool Blob::parse(const void* buf, std::string* err) {
   if (prologue == 2) {
     if (f4_kind(qtype) < 0 && !is_f8(qtype))
       return fail("NFloat weight dtype must be F4_BNB, F4_E2M1, F4_NF4, F8_E4M3 or F8_E5M2");
-  } else if (!dtype_is_int(qtype) || dtype_bits(qtype) < 2 || dtype_bits(qtype) > 8) {
-    return fail("weight dtype must be an integer type S2_CLIP .. S8 (S1 is not supported)");
+  } else if (!dtype_is_int(qtype) || dtype_bits(qtype) < 1 || dtype_bits(qtype) > 8) {
+    return fail("weight dtype must be an integer type S1_CLIP .. S8");
   }
   if (scale_t != kF32 && scale_t != kBF16 && scale_t != kF16 && !(scale_t == kF8E8M0 && is_f8(qtype)))
     return fail("scale dtype must be F32, BF16 or F16 (F8_E8M0 with F8 weights)");
@@ -446,11 +446,13 @@ static inline size_t ilv_index(int k, int n, int kpad, int ntile, int pr) {
   return size_t(n / ntile) * ntile * kpad + size_t(k / pr) * ntile * pr + size_t(n % ntile) * pr + (k % pr);
 }
 
+static inline int8_t read_q(const Blob& b, const uint8_t* qp, const CoreInfo& ci, int kk, int nn);
+
 bool pack_quantized(Blob& b, int8_t* base, const int8_t* Q, int ldq, const float* S, const int8_t* Z,
                     const int* g_idx, std::string* err) {
   const CoreInfo ci = core_info(b.core_id);
   const int bits = dtype_bits(b.qtype);
-  if (bits < 2 || bits > 8) {
+  if (bits < 1 || bits > 8) {
     if (err) *err = "unsupported weight bits";
     return false;
   }
@@ -481,16 +483,20 @@ bool pack_quantized(Blob& b, int8_t* base, const int8_t* Q, int ldq, const float
   // reorderWeight + compressWeight: walk the interleaved order directly, packing as we go
   uint8_t* qp = reinterpret_cast<uint8_t*>(base + b.q_off);
   const int ntile = ci.ntile, pr = ci.packrow, kpad = b.kpad;
-  if (bits == 3 || bits == 5 || bits == 6 || bits == 7) {  // bit planes (compressBitNWeight, bestla_prologue_b.h:512-546)
+  if (bits == 1 || bits == 3 || bits == 5 || bits == 6 || bits == 7) {  // bit planes (compressBitNWeight,
+    // bestla_prologue_b.h:512-546 / compressBit1Weight :566-581)
     const size_t nel = size_t(b.npad) * kpad;
     std::memset(qp, 0, b.q_size);
-    const bool has4 = bits >= 5, has2 = bits == 3 || bits >= 6, has1 = bits == 3 || bits == 5 || bits == 7;
+    const bool has4 = bits >= 5, has2 = bits == 3 || bits >= 6, has1 = bits == 1 || bits == 3 || bits == 5 || bits == 7;
     const size_t o2 = has4 ? nel / 2 : 0, o1 = o2 + (has2 ? nel / 4 : 0);
     // one task per group of 8 elements so no two tasks write the same byte of any plane
     parallel_for(int(nel / 8 / 64 + 1), [&](int task) {
       for (size_t e8 = size_t(task) * 64; e8 < std::min(nel / 8, size_t(task + 1) * 64); e8++)
         for (size_t e = e8 * 8; e < e8 * 8 + 8; e++) {
-          const size_t st = e / (size_t(ntile) * kpad), el = e % (size_t(ntile) * kpad);
+          // compress_1bit (kernel_ref.h:343-361) fills the slot of element 8i + 4 from srcptr[8i + FullRange] =
+          // srcptr[8i + 1]; the blob keeps that, so it matches the reference's byte for byte
+          const size_t es = bits == 1 && (e & 7) == 4 ? e - 3 : e;
+          const size_t st = es / (size_t(ntile) * kpad), el = es % (size_t(ntile) * kpad);
           const int kk = int(el / (size_t(ntile) * pr)) * pr + int(el % pr);
           const int nn = int(st) * ntile + int((el / pr) % ntile);
           const int8_t v = (kk < b.k && nn < b.n) ? Q[size_t(kk) * ldq + nn] : 0;
@@ -540,7 +546,8 @@ bool pack_quantized(Blob& b, int8_t* base, const int8_t* Q, int ldq, const float
         float s = load_scale(sp, size_t(g) * b.cstep + n, b.scale_t);
         int z = b.asym ? (base + b.z_off)[size_t(g) * b.cstep + n] : 0;
         float t = 0.f;
-        for (int kk = k0; kk < k1; kk++) t += float(Q[size_t(kk) * ldq + n] - z) * s;
+        for (int kk = k0; kk < k1; kk++)  // from the stored codes (unpackWeight): S1 keeps compress_1bit's slot 4
+          t += float((bits == 1 ? read_q(b, qp, ci, kk, n) : Q[size_t(kk) * ldq + n]) - z) * s;
         rp[size_t(g) * b.cstep + n] = f32_to_bf16_rne(t);
       }
     });
@@ -552,9 +559,9 @@ static inline int8_t read_q(const Blob& b, const uint8_t* qp, const CoreInfo& ci
   size_t e = ilv_index(kk, nn, b.kpad, ci.ntile, ci.packrow);
   int bits = dtype_bits(b.qtype);
   if (bits == 8) return int8_t(qp[e]);
-  if (bits == 3 || bits == 5 || bits == 6 || bits == 7) {
+  if (bits == 1 || bits == 3 || bits == 5 || bits == 6 || bits == 7) {
     const size_t nel = size_t(b.npad) * b.kpad;
-    const bool has4 = bits >= 5, has2 = bits == 3 || bits >= 6, has1 = bits == 3 || bits == 5 || bits == 7;
+    const bool has4 = bits >= 5, has2 = bits == 3 || bits >= 6, has1 = bits == 1 || bits == 3 || bits == 5 || bits == 7;
     const size_t o2 = has4 ? nel / 2 : 0, o1 = o2 + (has2 ? nel / 4 : 0);
     uint32_t u = 0;
     int sh = 0;

@@ -29,8 +29,9 @@ namespace nad {
 
 // ------------------------------------------------------------------------------------------------ repack
 // signed integer q of blob element e (interleaved order).  S2/S4: crumb / nibble = q + 2^(b-1); S8: the byte;
-// S3/S5/S6/S7: u = q + 2^(b-1) split over a nibble plane [nel/2], a crumb plane [nel/4] and a bit plane [nel/8]
-// (3 = crumb|bit, 5 = nibble|bit, 6 = nibble|crumb, 7 = nibble|crumb|bit; kernel_ref.h:178-341).
+// S1/S3/S5/S6/S7: u = q + 2^(b-1) split over a nibble plane [nel/2], a crumb plane [nel/4] and a bit plane [nel/8]
+// (1 = bit, 3 = crumb|bit, 5 = nibble|bit, 6 = nibble|crumb, 7 = nibble|crumb|bit; kernel_ref.h:178-361).  S1
+// repacks into the int2 tile layout (q in {-1, 0}).
 __device__ __forceinline__ int blob_q(const RepackArgs& a, uint64_t e) {
   const uint8_t* q = a.src_q;
   switch (a.src_bits) {
@@ -44,7 +45,7 @@ __device__ __forceinline__ int blob_q(const RepackArgs& a, uint64_t e) {
       break;
   }
   const int b = a.src_bits;
-  const bool has4 = b >= 5, has2 = b == 3 || b >= 6, has1 = b == 3 || b == 5 || b == 7;
+  const bool has4 = b >= 5, has2 = b == 3 || b >= 6, has1 = b == 1 || b == 3 || b == 5 || b == 7;
   uint64_t off = 0;
   uint32_t u = 0;
   int sh = 0;

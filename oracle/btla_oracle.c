@@ -1065,15 +1065,18 @@ int orc_q4_0_forward(const float* A, const uint8_t* W, float* C, int m, int n, i
   return 0;
 }
 
-/* ------------------------------------------------------------------ 3/5/6/7-bit planes */
+/* ------------------------------------------------------------------ 1/3/5/6/7-bit planes */
 /* kernel_ref.h:178-341 compress_{7,6,5,3}bit with the plane layout of compressBitNWeight (bestla_prologue_b.h:512-546):
    stored u = q + 2^(bits-1) split into a nibble plane (bit4x2: element 2i in the low nibble of byte i), a crumb plane
    (bit2x4: element 4i + j at bits 2j of byte i) and a bit plane (bit1x8: element 8i + j at bit j of byte i):
    3 = crumb [n/4] | bit [n/8];  5 = nibble [n/2] | bit [n/8];  6 = nibble [n/2] | crumb [n/4];
-   7 = nibble [n/2] | crumb [n/4] | bit [n/8]; the high part of u sits in the later plane(s). */
+   7 = nibble [n/2] | crumb [n/4] | bit [n/8]; the high part of u sits in the later plane(s).
+   1 = bit [n/8] (compress_1bit, kernel_ref.h:343-361), which stores element 8i + 4 from srcptr[8i + FullRange] =
+   srcptr[8i + 1]: reproduced, so blobs match the reference byte for byte (golden compress_bit1). */
 static void planes(int bits, size_t n, size_t* o4, size_t* o2, size_t* o1) {
   *o4 = *o2 = *o1 = (size_t)-1;
   switch (bits) {
+    case 1: *o1 = 0; break;
     case 3: *o2 = 0; *o1 = n / 4; break;
     case 5: *o4 = 0; *o1 = n / 2; break;
     case 6: *o4 = 0; *o2 = n / 2; break;
@@ -1087,7 +1090,7 @@ int orc_compress_planes(int bits, const int8_t* src, uint8_t* dst, size_t n) {
   if (o2 == (size_t)-1 && o1 == (size_t)-1) return -1;
   memset(dst, 0, n * bits / 8);
   for (size_t e = 0; e < n; e++) {
-    unsigned u = (unsigned)(src[e] + (1 << (bits - 1)));
+    unsigned u = (unsigned)(src[bits == 1 && (e & 7) == 4 ? e - 3 : e] + (1 << (bits - 1)));
     int sh = 0;
     if (o4 != (size_t)-1) {
       dst[o4 + e / 2] |= (uint8_t)((u & 15u) << (4 * (e & 1)));
@@ -1101,7 +1104,7 @@ int orc_compress_planes(int bits, const int8_t* src, uint8_t* dst, size_t n) {
   }
   return 0;
 }
-/* decompress_s{3,5,6,7}_s8 (kernel_ref.h:412-520) */
+/* decompress_s{1,3,5,6,7}_s8 (kernel_ref.h:412-525) */
 int orc_decompress_planes(int bits, const uint8_t* src, int8_t* dst, size_t n) {
   size_t o4, o2, o1;
   planes(bits, n, &o4, &o2, &o1);

@@ -315,6 +315,20 @@ static void case_compress_planes(const char* cs, size_t n) {
   }
 }
 
+// kernel_ref.h:343-361 compress_1bit / :511-525 decompress_s1_s8 (S1_CLIP, one bit plane).  compress_1bit reads
+// element 4 of every 8 from srcptr[j + FullRange] = srcptr[j + 1]: the golden records what the reference stores.
+static void case_compress_bit1(const char* cs, size_t n) {
+  std::vector<int8_t> tmp(64), src(n), dec(n);
+  for (auto& v : src) v = (int8_t)((int)(rnd() % 2u) - 1);
+  std::vector<uint8_t> packed(n / 8);
+  auto* b1 = reinterpret_cast<utils::bit1x8*>(packed.data());
+  kernel::ref::compress_1bit(src.data(), b1, n);
+  kernel::ref::decompress_s1_s8(b1, dec.data(), n, tmp.data(), tmp.size());
+  dump(cs, "s1", "i1", src.data(), n);
+  dump(cs, "c1", "u1", packed.data(), packed.size());
+  dump(cs, "d1", "i1", dec.data(), n);
+}
+
 // NFloat 4-bit: kernel_ref.h:1800-1822 quantize_f32_f4_rowblock, f4_dequantize (the unpack trees) and the
 // bestla_utils.h:749-790 LUTs the SIMD kernels use
 template <BTLA_DTYPE F4_T>
@@ -413,6 +427,9 @@ int main(int argc, char** argv) {
   case_f8<BTLA_DTYPE::F8_E5M2>("f8_e5m2_e8m0_g64", 128, 9, 64, BTLA_DTYPE::F8_E8M0, 100.f);
   case_f8<BTLA_DTYPE::F8_E4M3>("f8_e4m3_f32_g32", 96, 7, 32, BTLA_DTYPE::F32, 0.5f);
   case_f8<BTLA_DTYPE::F8_E5M2>("f8_e5m2_f32_g128", 256, 5, 128, BTLA_DTYPE::F32, 1.f);
+  case_compress_bit1("compress_bit1", 4096);
+  case_quant("quant_s1_sym_g32", 128, 37, 32, BTLA_DTYPE::S1_CLIP, false, 1);
+  case_quant("quant_s1_asym_g64", 128, 13, 64, BTLA_DTYPE::S1_CLIP, true, 0);
   fclose(g_man);
   return 0;
 }

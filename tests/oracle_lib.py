@@ -11,10 +11,10 @@ GOLDEN = os.path.join(REPO, "tests", "golden")
 
 F32, F16, BF16 = 32, 16, 16 | (1 << 16)
 S8, S4, S2 = 8 | 0x100, 4 | 0x100, 2 | 0x100
-S3, S5, S6, S7 = 3 | 0x100, 5 | 0x100, 6 | 0x100, 7 | 0x100
+S1, S3, S5, S6, S7 = 1 | 0x100, 3 | 0x100, 5 | 0x100, 6 | 0x100, 7 | 0x100
 F4_E2M1, F4_BNB, F4_NF4 = 4, 4 | (1 << 16), 4 | (2 << 16)
 F8_E4M3, F8_E5M2, F8_E8M0 = 8, 8 | (1 << 16), 8 | (3 << 16)
-BITS_TO_QTYPE = {8: S8, 7: S7, 6: S6, 5: S5, 4: S4, 3: S3, 2: S2}
+BITS_TO_QTYPE = {8: S8, 7: S7, 6: S6, 5: S5, 4: S4, 3: S3, 2: S2, 1: S1}
 
 _p = C.c_void_p
 

@@ -6,7 +6,7 @@ import numpy as np
 import pytest
 
 from neural_amd import _lib, bestla
-from tests.oracle_lib import F32, BF16, F16, F4_BNB, F4_E2M1, F4_NF4, F8_E4M3, F8_E5M2, F8_E8M0, S2, S3, S4, S5, S6, S7, S8
+from tests.oracle_lib import F32, BF16, F16, F4_BNB, F4_E2M1, F4_NF4, F8_E4M3, F8_E5M2, F8_E8M0, S1, S2, S3, S4, S5, S6, S7, S8
 
 
 def test_library_exports_every_header_symbol():
@@ -40,6 +40,8 @@ CFGS = [
     (48, 256, 32, S5, F32, True, bestla.COMP_F32),      # 5-bit: nibble + bit planes
     (48, 256, 64, S6, F16, False, bestla.COMP_INT8),    # 6-bit: nibble + crumb planes
     (40, 128, 32, S7, F32, False, bestla.COMP_F32),     # 7-bit: nibble + crumb + bit planes
+    (64, 256, 32, S1, F32, False, bestla.COMP_F32),     # 1-bit: one bit plane (compress_1bit's slot-4 quirk)
+    (50, 256, 64, S1, BF16, True, bestla.COMP_INT8),    # ... reduce buffer from the stored codes
     (64, 256, 32, F4_NF4, F32, False, bestla.COMP_F32),  # NFloat (prologue WeightKBlockNFloat): no zp / reduce
     (50, 256, 64, F4_E2M1, BF16, False, bestla.COMP_BF16),
     (48, 128, 32, F4_BNB, F32, False, bestla.COMP_INT8),  # int8 compute falls through to a float core
@@ -61,7 +63,7 @@ def test_quant_pack_bit_exact_vs_oracle(oracle, cfg):
     if qt in (F8_E4M3, F8_E5M2) and st == F32:
         blob = bestla.quant_pack(W, bs, qt, st, asym, comp)
     else:
-        blob = bestla.quantize(W, group_size=bs, weight_dtype={S4: "int4", S2: "int2", S8: "int8", S3: "int3", S5: "int5", S6: "int6",
+        blob = bestla.quantize(W, group_size=bs, weight_dtype={S4: "int4", S2: "int2", S8: "int8", S1: "int1", S3: "int3", S5: "int5", S6: "int6",
                                                            S7: "int7", F4_NF4: "nf4", F4_E2M1: "fp4_e2m1",
                                                            F4_BNB: "fp4_bnb", F8_E4M3: "fp8_e4m3", F8_E5M2: "fp8_e5m2"}[qt],
                            scale_dtype={F32: "fp32", BF16: "bf16", F16: "fp16", F8_E8M0: "fp8"}[st],
@@ -151,7 +153,7 @@ def test_unsupported_inputs_fail_loudly():
     assert L.nad_device_weight_size(bad.ctypes.data_as(C.c_void_p)) == 0
     assert "WeightKBlockNInteger" in _lib.last_error() or "corrupt" in _lib.last_error()
     with pytest.raises(ValueError):
-        bestla.quantize(np.zeros((16, 64), np.float32), 32, "int1")  # S1 weights: not supported (loudly)
+        bestla.quantize(np.zeros((16, 64), np.float32), 32, "int9")  # no such weight dtype (loudly)
     with pytest.raises(RuntimeError):  # F8_E8M0 scales with integer weights: rejected by the pack API
         bestla.quant_pack(np.zeros((16, 64), np.float32), 32, S4, F8_E8M0, False, bestla.COMP_F32)
 

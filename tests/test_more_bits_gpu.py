@@ -1,8 +1,8 @@
-"""GPU parity for the 3/5/6/7-bit integer weights and the NFloat 4-bit weights (F4_NF4 / F4_E2M1 / F4_BNB,
+"""GPU parity for the 1/3/5/6/7-bit integer weights and the NFloat 4-bit weights (F4_NF4 / F4_E2M1 / F4_BNB,
 bestla_prologue_b.h:1005-1342: codes in the int4 tile layout, dequantized through the bestla_utils.h:749-790 LUT whose
 entries are rounded to fp16 for the MFMA B operand -- <= 2^-12 relative per weight, hence the 1e-3 bar) and the
 3/5/6/7-bit integer weights (quant_config.h:22-57 "int3".."int7"; planes of
-bestla_prologue_b.h:512-546).  The repack stores S3 in the int4 tile layout and S5-S7 in the int8 one (exact: the
+bestla_prologue_b.h:512-546).  The repack stores S1 in the int2 tile layout, S3 in the int4 one and S5-S7 in the int8 one (exact: the
 integers fit), so every forward kernel serves them; checked against the oracle's fp64 forward of the same blob, the
 repacked integers bit-exact, and the int8-compute mode against the oracle's kblock GEMM.  NFloat 8-bit weights (F8_E4M3 /
 F8_E5M2 with F8_E8M0 or F32 scales, bestla_prologue_b.h:1198-1208, kernel_ref.h:984-1026) sit as raw codes in the int8
@@ -11,7 +11,7 @@ import numpy as np
 import pytest
 
 from tests.conftest import gpu_available
-from tests.oracle_lib import BF16, F16, F32, F4_BNB, F4_E2M1, F4_NF4, F8_E4M3, F8_E5M2, F8_E8M0, S3, S5, S6, S7
+from tests.oracle_lib import BF16, F16, F32, F4_BNB, F4_E2M1, F4_NF4, F8_E4M3, F8_E5M2, F8_E8M0, S1, S3, S5, S6, S7
 from tests.test_gpu_parity import _blob, _rel_err
 
 pytestmark = pytest.mark.gpu
@@ -28,6 +28,9 @@ CASES = [
     (128, 1024, 32, S6, F16, False, 4),
     (64, 512, 128, S7, F32, False, 1),
     (48, 300, 1024, S3, F32, False, 1),     # per-channel, K tail
+    (256, 1024, 64, S1, F16, False, 1),     # 1-bit (S1_CLIP, q in {-1, 0}) in the int2 tile layout
+    (200, 768, 32, S1, BF16, True, 4),
+    (72, 300, 128, S1, F32, False, 2),      # K tail
     (256, 1024, 32, F4_NF4, F32, False, 1),
     (128, 512, 64, F4_E2M1, BF16, False, 2),
     (96, 512, 32, F4_BNB, F16, False, 1),
@@ -46,7 +49,7 @@ def test_repack_exact(oracle, cfg):
     n, k, bs, qt, st, asym, comp = cfg
     blob = _blob(oracle, n, k, bs, qt, st, asym, comp, seed=n + k)
     w = bestla.DeviceWeight(blob)
-    assert w.bits == (4 if qt in (S3,) + F4 else 8)
+    assert w.bits == (2 if qt == S1 else (4 if qt in (S3,) + F4 else 8))
     assert np.array_equal(w.unpack().view(np.uint32), oracle.unpack_fp32(blob).view(np.uint32))
 
 

@@ -224,6 +224,23 @@ def test_compress_planes_bit_exact(oracle):
         assert np.array_equal(d, g[f"d{bits}"]) and np.array_equal(d, src), bits
 
 
+def test_compress_bit1_bit_exact(oracle):
+    """1-bit weights (S1_CLIP): kernel_ref.h compress_1bit / decompress_s1_s8 against the reference's own outputs.  The
+    reference's compressor stores element 8i + 1 in the slot of element 8i + 4 (srcptr[j + FullRange]); the oracle
+    reproduces that, so the decompressed golden differs from its source exactly there."""
+    g = G["compress_bit1"]
+    src = np.ascontiguousarray(g["s1"])
+    n = src.size
+    c = np.zeros(n // 8, np.uint8)
+    assert oracle.lib.orc_compress_planes(1, src.ctypes.data, c.ctypes.data, n) == 0
+    assert np.array_equal(c, g["c1"])
+    d = np.zeros(n, np.int8)
+    assert oracle.lib.orc_decompress_planes(1, np.ascontiguousarray(g["c1"]).ctypes.data, d.ctypes.data, n) == 0
+    assert np.array_equal(d, g["d1"])
+    quirk = np.arange(n) % 8 == 4
+    assert np.array_equal(d[~quirk], src[~quirk]) and np.array_equal(d[quirk], src[np.nonzero(quirk)[0] - 3])
+
+
 @pytest.mark.parametrize("case,kind", [("f4_bnb_g32", 0), ("f4_e2m1_g64", 1), ("f4_nf4_g32", 2),
                                        ("f4_nf4_perchannel", 2)])
 def test_f4_quantizer_and_lut_bit_exact(oracle, case, kind):
