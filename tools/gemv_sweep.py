@@ -32,13 +32,14 @@ import torch  # noqa: E402
 from neural_amd import _lib, bestla  # noqa: E402
 
 G = int(os.environ.get("SWEEP_GROUP", "128"))  # quantization group of the synthetic weights
+BITS = int(os.environ.get("SWEEP_BITS", "4"))  # weight bits (4, or 2 for the Mistral int2 policy)
 SHAPES = {  # name: (n, k, weights per launch)
     "qkv": (4096, 4096, 3), "o": (4096, 4096, 1), "gate_up": (11008, 4096, 2), "down": (4096, 11008, 1),
     "lm_head": (32000, 4096, 1)}
 
 
 def wbytes(n, k):
-    return n * k // 2 + n * (k // G) * 2
+    return n * k * BITS // 8 + n * (k // G) * 2
 
 
 def set_env(cfg):
@@ -68,7 +69,7 @@ def main():
         copies = max(2, math.ceil(600e6 / per))
         if os.environ.get("SWEEP_COPIES"):  # e.g. 1-2: weights stay in the Infinity Cache (warm-MALL experiment)
             copies = int(os.environ["SWEEP_COPIES"])
-        ws = [[bestla.DeviceWeight.synthetic(4, n, k, G, "fp16", False, seed=1000 * i + j) for j in range(nw)]
+        ws = [[bestla.DeviceWeight.synthetic(BITS, n, k, G, "fp16", False, seed=1000 * i + j) for j in range(nw)]
               for i in range(copies)]
         xa = x[:, :k].contiguous()
         out = torch.empty((3, 1, n), device=dev)
