@@ -58,6 +58,22 @@ def weight_bytes(n, k, bits, g, sbytes=2, asym=False):
     return n * k * bits // 8 + groups * sbytes + (groups if asym else 0)
 
 
+def shard_table(cfg, world):
+    """Per-rank tensor-parallel shards of the model geometry (what Stack builds on each rank; no GPU): head-aligned
+    Q/K/V columns, O's K rows = that rank's heads, gate/up columns = down's K rows in whole quantization groups, vocab
+    columns of lm_head in whole 16-column stripes."""
+    H, F, g, hd = cfg["hidden"], cfg["ffn"], cfg["group"], cfg["head"]
+    rows = []
+    for r in range(world):
+        q = shard(H, world, r, hd)
+        kv = shard(cfg["kv"], world, r, hd)
+        f = shard(F, world, r, g)
+        v = shard(cfg["vocab"], world, r, 16)
+        rows.append({"rank": r, "q_cols": q, "kv_cols": kv, "o_k_rows": q, "gate_up_cols": f, "down_k_rows": f,
+                     "down_k_groups": (f[1] - f[0]) // g, "heads": (q[1] - q[0]) // hd, "lm_head_cols": v})
+    return rows
+
+
 class Stack:
     """Synthetic linear weights of one TP rank for a model geometry (random codes, scales U[0.001, 0.01])."""
 
@@ -286,7 +302,11 @@ def cpu_baseline(budget_s=12.0):
     decoder layer's shapes + lm_head (int4 g128), repeated for ~budget_s seconds, extrapolated to a 32-layer token."""
     from tests.oracle_lib import Oracle, S4, F16
     orc = Oracle.get()
-    threads = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)))
+    # every host core this process may use: its affinity set, capped by the box's CPU share when the launcher sets
+    # one (the GPU box exports OMP_NUM_THREADS = its share of the machine; os.cpu_count() is the whole machine)
+    usable = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    threads = max(1, min(usable, share) if share > 0 else usable)
     rng = np.random.default_rng(0)
     core = orc.core("avx512f")
     H, F, Lr, V, G = 4096, 11008, 32, 32000, 128
@@ -319,7 +339,9 @@ def cpu_baseline(budget_s=12.0):
     except OSError:
         pass
     return {"value": round(1.0 / total, 4), "unit": "tokens/s", "cores": threads, "kind": "port",
-            "cpu_model": cpu_model,
+            "cpu_model": cpu_model, "host_cpus": os.cpu_count(), "usable_cpus": usable,
+            "cores_note": "all CPUs this process may use (affinity), capped by the launcher's CPU share "
+                          "(OMP_NUM_THREADS) when set",
             "sample": f"oracle GEMV (kernel_ref.h gemv_4bit_fp32_fp32 order, scalar code, NTILE column blocks over "
                       f"{threads} OpenMP threads) on one decoder layer (QKV 12288x4096, O 4096x4096, gate+up "
                       f"22016x4096, down 4096x11008) + lm_head 32000x4096 int4 g128, {len(times[0])} rounds "
@@ -327,6 +349,21 @@ def cpu_baseline(budget_s=12.0):
             "reference_published": REFERENCE_PUBLISHED,
             "note": "scalar restatement, not the reference's AVX512/AMX kernels (unbuildable offline: xbyak); compare "
                     "against reference_published, not this value"}
+
+
+def latest_pmc():
+    """The newest round's decode PMC traffic file: profiles/rNN_pmc_traffic_decode*.json with the highest round, the
+    file listed last in that round's profiles/rNN_pmc_latest.txt when present (tools/pmc_traffic.py writes both)."""
+    import glob
+    import re
+    prof = os.path.join(REPO, "profiles")
+    best = None
+    for f in glob.glob(os.path.join(prof, "r*_pmc_latest.txt")):
+        rnd = int(re.match(r"r(\d+)_", os.path.basename(f)).group(1))
+        names = [ln.strip() for ln in open(f) if ln.strip()]
+        if names and os.path.exists(os.path.join(prof, names[-1])) and (best is None or rnd > best[0]):
+            best = (rnd, os.path.join(prof, names[-1]))
+    return best[1] if best else os.path.join(prof, "pmc_traffic.json")
 
 
 def _free_port():
@@ -361,7 +398,8 @@ def main(argv=None):
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         if args.dry_run:
-            print(json.dumps({"relaunch": True, "nproc_per_node": args.gpus}))
+            print(json.dumps({"relaunch": True, "nproc_per_node": args.gpus,
+                              "shards": shard_table(LLAMA, args.gpus)}))
             return 0
         return relaunch(argv, args.gpus)
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -370,7 +408,8 @@ def main(argv=None):
     if world != args.gpus:
         raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: refusing to report a wrong n_gpus")
     if args.dry_run:
-        print(json.dumps({"relaunch": False, "world": world, "rank": rank, "local_rank": local}))
+        print(json.dumps({"relaunch": False, "world": world, "rank": rank, "local_rank": local,
+                          "shards": shard_table(LLAMA, world)[rank:rank + 1]}))
         return 0
 
     import torch
@@ -455,7 +494,7 @@ def main(argv=None):
             tot_bytes / n_per_op_launches, per_op_time / n_per_op_launches
     achieved = bytes_per_launch / launch_s / 1e9
     traffic = None
-    pmc = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    pmc = latest_pmc()
     if os.path.exists(pmc):
         try:
             rec = json.load(open(pmc))["woq_chain_kernel" if chain is not None else "woq_gemv_m1_kernel"]
@@ -499,6 +538,7 @@ def main(argv=None):
             "prefill_ms_per_2048_tokens": round(pdt / args.prefill_steps * 1e3, 3),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
+                         "traffic_source": os.path.basename(pmc) if traffic is not None else None,
                          "kernel": kernel, "bytes_per_launch": int(bytes_per_launch),
                          "avg_launch_us": round(launch_s * 1e6, 3)},
             "decode_chain_tokens_per_s": None if chain_tok_s is None else round(chain_tok_s, 2),

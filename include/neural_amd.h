@@ -128,7 +128,8 @@ int nad_pc_allreduce_f32(parallel_context* p, const float* send, float* recv, si
 int nad_pc_set_stream(parallel_context* p, void* stream);   /* stream of the reference entry points (default NULL) */
 double nad_pc_max_f64(parallel_context* p, double v);        /* max over ranks (host value; bench timing) */
 int nad_pc_status(parallel_context* p);   /* 0 ok, 1 a one-shot all-reduce gave up waiting for a peer */
-int nad_pc_info(parallel_context* p);     /* bit0 GPU transport, bit1 one-shot IPC path, bit2 RCCL communicator */
+int nad_pc_info(parallel_context* p);     /* bit0 GPU transport, bit1 one-shot IPC path, bit2 RCCL communicator,
+                                             bit3 one-shot buffer is uncached fine-grained memory (else hipMalloc) */
 const char* nad_pc_last_error(parallel_context* p);
 void nad_pc_destroy(parallel_context* p);
 
@@ -185,9 +186,20 @@ int nad_synthetic_weight(void* devstor, void* deviceptr, size_t capacity, int bi
                          int scale_t, int asym, uint64_t seed, void* queue);
 /* device bytes of nad_synthetic_weight's layout */
 size_t nad_synthetic_weight_size(int bits, int n, int k, int blocksize, int scale_t, int asym);
-/* drop every device copy the host-pointer ABI cached (weights are keyed by blob address + content fingerprint and
- * re-uploaded when a pack entry rewrites a blob) */
+/* The host-pointer ABI (bestla_f32f32_forward & co., inner_product.cpp:28-36 called per node at ne_layers.c:7313)
+ * keeps one device copy per blob address.  Per call the key check is O(1): the 64-byte header, the blob size and 64
+ * dwords sampled at fixed positions; every pack entry of this library (BTLAGemmQuantPackB, BTLAGemmPackB,
+ * bestla_packweight_copyattr, nad_blob_split) drops the copy of the buffer it writes, so a rewrite through the pack
+ * API is always seen.  The cache is bounded (least recently used first out) by NAD_HOST_CACHE_MB, default 64 GiB. */
 void nad_host_cache_clear(void);
+/* drop the device copy of one blob (call before freeing or rewriting it outside the pack API) */
+void nad_host_cache_evict(const void* blob);
+/* cap on the cached device bytes (0 = the default); returns the previous cap */
+size_t nad_host_cache_set_limit(size_t bytes);
+/* entries and device bytes currently cached */
+int nad_host_cache_stats(size_t* entries, size_t* bytes);
+/* the per-call key of a host blob (what the cache compares on every forward); 0 if the blob does not parse */
+unsigned long long nad_host_blob_key(const void* blob);
 /* ===== int8-compute mode: the reference's comp_int8 arithmetic for weights packed for an integer core (blobs that
  * carry the bf16 reduce).  0 (default): fp16 MFMA on the exact weights.  1: activations quantized to u8 per (row,
  * weight block) as kernel_ref.h:1824-1883, s32 block dot products, the kblock core's fp32 combine
@@ -195,6 +207,14 @@ void nad_host_cache_clear(void);
  * reduce keep the fp path; a fused call mixing the two kinds fails. */
 int nad_set_compute_mode(int mode);
 int nad_get_compute_mode(void);
+/* per-thread override of the process mode (-1 clears it); thread-safe, takes precedence over nad_set_compute_mode */
+int nad_set_thread_compute_mode(int mode);
+/* per-weight arithmetic, as the reference selects it per blob core (bestla_gemm.cpp:516-616): -1 follow the
+ * thread / process mode, 0 fp, 1 int8 (integer-core blobs and GGUF Q4_0; other weights stay fp).  Takes precedence
+ * over both; a fused call whose weights resolve to different arithmetic runs each weight in its own. */
+int nad_device_set_compute(void* devstor, int mode);
+/* the arithmetic a forward of this weight takes now: 0 fp, 1 int8, -1 not a device weight */
+int nad_device_get_compute(const void* devstor);
 /* kernel::wrapper::QuantizeU8ColBlock::forward (kernel_wrapper.h:571-590) on device pointers: act [m][lda] in
  * act_dtype, q [m][ldq] u8, scales / zps [m][ld_scale] per block, blkreduce (may be NULL) = sum(round(x/s)) * s. */
 int nad_quant_u8_colblock(const void* act, int act_dtype, int m, int k, int lda, int blocksize, uint8_t* q, int ldq,

@@ -75,8 +75,15 @@ SIGNATURES = {
     "nad_synthetic_weight_size": (_sz, [_i, _i, _i, _i, _i, _i]),
     "nad_device_unpack_fp32": (_i, [_p, _p, _p]),
     "nad_host_cache_clear": (None, []),
+    "nad_host_cache_evict": (None, [_p]),
+    "nad_host_cache_set_limit": (_sz, [_sz]),
+    "nad_host_cache_stats": (_i, [_p, _p]),
+    "nad_host_blob_key": (C.c_ulonglong, [_p]),
     "nad_set_compute_mode": (_i, [_i]),
     "nad_get_compute_mode": (_i, []),
+    "nad_set_thread_compute_mode": (_i, [_i]),
+    "nad_device_set_compute": (_i, [_p, _i]),
+    "nad_device_get_compute": (_i, [_p]),
     "nad_quant_u8_colblock": (_i, [_p, _i, _i, _i, _i, _i, _p, _i, _p, _p, _i, _p, _p]),
     "nad_q4_0_device_size": (_sz, [_i, _i]),
     "nad_q4_0_device_load": (_i, [_p, _i, _i, _p, _p, _sz, _p]),

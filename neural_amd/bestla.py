@@ -258,6 +258,17 @@ class DeviceWeight:
 
     __call__ = forward
 
+    def set_compute(self, mode):
+        """Per-weight arithmetic (nad_device_set_compute): None / -1 follow the thread / process mode, COMPUTE_FP or
+        COMPUTE_INT8 (integer-core blobs and GGUF Q4_0 only; other weights stay fp)."""
+        check(lib().nad_device_set_compute(self.desc, -1 if mode is None else int(mode)), "nad_device_set_compute")
+        return self
+
+    @property
+    def compute(self):
+        """the arithmetic a forward takes now: COMPUTE_FP or COMPUTE_INT8"""
+        return lib().nad_device_get_compute(self.desc)
+
     def unpack(self, stream=None):
         """dequantized fp32 [K][N] read back from the device tile layout (repack exactness check)."""
         out = np.zeros((self.k, self.n), np.float32)
@@ -279,6 +290,11 @@ def set_compute_mode(mode):
 
 def get_compute_mode():
     return lib().nad_get_compute_mode()
+
+
+def set_thread_compute_mode(mode):
+    """Per-thread override of the process mode (None / -1 clears it)."""
+    check(lib().nad_set_thread_compute_mode(-1 if mode is None else int(mode)), "nad_set_thread_compute_mode")
 
 
 def quant_u8_colblock(x, blocksize, stream=None):

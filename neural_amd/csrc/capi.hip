@@ -2,6 +2,7 @@
 // MI355X.  Host-side orchestration only; all arithmetic on the hot path runs in woq_kernels.hip.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <climits>
 #include <cstdarg>
 #include <cstdio>
@@ -420,6 +421,7 @@ static int try_gemv(const void* act, int act_t, int lda, int m, int k, int nw, c
 }
 
 static bool int8_compute(const DeviceWeight& w);
+static bool is_q4_0(const DeviceWeight& w);
 static int run_i8(const void* act, int act_t, int lda, int m, int k, int nw, const DeviceWeight* const* ws,
                   float* const* outs, const int* ldos, bool dual, int epi, const float* bias, int bias_ld,
                   const float* res, int ld_res, const float* aux, int ld_aux, hipStream_t st);
@@ -427,6 +429,22 @@ static int run_i8(const void* act, int act_t, int lda, int m, int k, int nw, con
 static int run_skinny(const void* act, int act_t, int lda, int m, int k, int nw, const DeviceWeight* const* ws,
                       float* const* outs, const int* ldos, int epi, const float* bias, int bias_ld, const float* res,
                       int ld_res, float* aux, int ld_aux, hipStream_t st) {
+  if (nw > 1) {  // weights of one fused call whose arithmetic differs (per-weight compute modes) run one by one
+    bool mixed = false;
+    for (int i = 1; i < nw; i++)
+      mixed |= int8_compute(*ws[i]) != int8_compute(*ws[0]) || is_q4_0(*ws[i]) != is_q4_0(*ws[0]);
+    if (mixed) {
+      if (epi == kEpiSiluMul || epi == kEpiGeluMul) {
+        set_err("gate/up weights of one FFN must resolve to the same arithmetic (nad_device_set_compute)");
+        return -1;
+      }
+      for (int i = 0; i < nw; i++)
+        if (run_skinny(act, act_t, lda, m, k, 1, ws + i, outs + i, ldos + i, epi, bias, bias_ld, res, ld_res, aux,
+                       ld_aux, st))
+          return -1;
+      return 0;
+    }
+  }
   if (int8_compute(*ws[0]))
     return run_i8(act, act_t, lda, m, k, nw, ws, outs, ldos, nw == 2 && (epi == kEpiSiluMul || epi == kEpiGeluMul),
                   epi, bias, bias_ld, res, ld_res, aux, ld_aux, st);
@@ -532,16 +550,28 @@ static void* workspace_for(size_t bytes, hipStream_t st) {
 // reduce).  Off by default: the fp16-MFMA path on exact weights is the more accurate one.  Mode 1 (nad_set_compute_mode
 // or NAD_COMPUTE_INT8=1) reproduces the reference: u8 activations per (row, block), s32 block dots, the kblock core's
 // fp32 combine.
-static int g_compute_mode = -1;
+// The arithmetic is chosen per call, in order: the weight's own setting (nad_device_set_compute: the reference picks
+// it per blob core, bestla_gemm.cpp:516-616), else the calling thread's (nad_set_thread_compute_mode), else the
+// process default (nad_set_compute_mode, initialised from NAD_COMPUTE_INT8).  Mode 1 applies to blobs packed for an
+// integer core only -- exactly those that carry the reduce -- and to GGUF Q4_0; every other weight stays fp.
+static std::atomic<int> g_compute_mode{-1};
+static thread_local int t_compute_mode = -1;
 static int compute_mode() {
-  if (g_compute_mode < 0) g_compute_mode = env_int("NAD_COMPUTE_INT8", 0) ? 1 : 0;
-  return g_compute_mode;
+  if (t_compute_mode >= 0) return t_compute_mode;
+  int m = g_compute_mode.load(std::memory_order_relaxed);
+  if (m < 0) {
+    int init = env_int("NAD_COMPUTE_INT8", 0) ? 1 : 0, expect = -1;
+    g_compute_mode.compare_exchange_strong(expect, init);
+    m = g_compute_mode.load(std::memory_order_relaxed);
+  }
+  return m;
 }
 // a GGUF Q4_0 matrix (nad_q4_0_device_load) carries this in src_core_id: its int8 arithmetic is Q8_0 x Q4_0
 constexpr uint64_t kGgufQ4_0 = 0x3054344655474700ull;  // "\0GGUF4Q0"
 static bool is_q4_0(const DeviceWeight& w) { return w.src_core_id == kGgufQ4_0; }
+static int effective_mode(const DeviceWeight& w) { return w.compute > 0 ? w.compute - 1 : compute_mode(); }
 static bool int8_compute(const DeviceWeight& w) {
-  return compute_mode() == 1 && (w.reduce != nullptr || is_q4_0(w));
+  return effective_mode(w) == 1 && (w.reduce != nullptr || is_q4_0(w));
 }
 
 extern "C" int nad_set_compute_mode(int mode) {
@@ -549,10 +579,40 @@ extern "C" int nad_set_compute_mode(int mode) {
     set_err("compute mode must be 0 (fp) or 1 (int8 for integer-core weights), got %d", mode);
     return -1;
   }
-  g_compute_mode = mode;
+  g_compute_mode.store(mode, std::memory_order_relaxed);
   return 0;
 }
 extern "C" int nad_get_compute_mode(void) { return compute_mode(); }
+extern "C" int nad_set_thread_compute_mode(int mode) {
+  if (mode < -1 || mode > 1) {
+    set_err("thread compute mode must be -1 (follow the process default), 0 or 1, got %d", mode);
+    return -1;
+  }
+  t_compute_mode = mode;
+  return 0;
+}
+extern "C" int nad_device_set_compute(void* devstor, int mode) {
+  DeviceWeight* w = static_cast<DeviceWeight*>(devstor);
+  if (!w || w->magic != kWeightMagic) {
+    set_err("nad_device_set_compute: not a device weight");
+    return -1;
+  }
+  if (mode < -1 || mode > 1) {
+    set_err("weight compute mode must be -1 (follow the thread/process setting), 0 (fp) or 1 (int8), got %d", mode);
+    return -1;
+  }
+  w->compute = mode + 1;
+  return 0;
+}
+// the arithmetic a forward of this weight takes right now: 0 fp, 1 int8
+extern "C" int nad_device_get_compute(const void* devstor) {
+  const DeviceWeight* w = static_cast<const DeviceWeight*>(devstor);
+  if (!w || w->magic != kWeightMagic) {
+    set_err("nad_device_get_compute: not a device weight");
+    return -1;
+  }
+  return int8_compute(*w) ? 1 : 0;
+}
 
 struct I8Act {
   const int8_t* aq = nullptr;
@@ -990,10 +1050,17 @@ extern "C" int nad_device_qkv_forward(const void* act, int act_dtype, const void
     if (prepare_a16(pre, act, act_dtype, lda, m, k, *ws[0], st) < 0) return -1;
     pp = &pre;
   }
-  for (int i = 0; i < 3; i++)
-    if (run_gemm(act, act_dtype, lda, m, k, *ws[i], outs[i], ldos[i], kEpiNone, nullptr, 0, nullptr, 0, nullptr, 0,
-                 st, pp))
+  for (int i = 0; i < 3; i++) {
+    const DeviceWeight& w = *ws[i];
+    // a weight that cannot reuse the shared fp16 copy (other K tile, act-order, int8 arithmetic) writes its own
+    // conversion / u8 codes at the start of the same workspace: the copy is gone for the weights after it
+    const bool reuses = pp && !int8_compute(w) && pipelined_gemm(w, m) && !w.shuffle && pp->kp == w.nt * k_tile(w);
+    const bool clobbers = !reuses && (int8_compute(w) || pipelined_gemm(w, m));
+    if (run_gemm(act, act_dtype, lda, m, k, w, outs[i], ldos[i], kEpiNone, nullptr, 0, nullptr, 0, nullptr, 0, st,
+                 reuses ? pp : nullptr))
       return -1;
+    if (clobbers && pp && pp->p != act) pp = nullptr;
+  }
   return 0;
 }
 
@@ -1376,12 +1443,18 @@ struct CachedWeight {
   DeviceWeight w;
   void* mem;
   uint64_t size;
-  uint64_t fingerprint;
+  uint64_t key;
+  uint64_t bytes;     // device bytes held
+  uint64_t last_use;  // LRU tick
 };
 struct HostCtx {
   std::mutex mu;
   NadDevice* dev = nullptr;
   std::unordered_map<const void*, CachedWeight> cache;
+  uint64_t cached_bytes = 0;
+  uint64_t limit = 0;       // 0: NAD_HOST_CACHE_MB or the default
+  uint64_t tick = 0;
+  uint64_t call_start = 0;  // entries used since this tick belong to the running call: never evicted by it
   void* stage = nullptr;
   size_t stage_bytes = 0;
   int threads = 0;
@@ -1395,18 +1468,31 @@ NadDevice* host_device() {
   if (!c.dev) c.dev = static_cast<NadDevice*>(bestla_create_device(false));
   return c.dev;
 }
-// FNV-1a over the blob header, the whole correction section (scales / zero points: 1/32 of an int4 blob) and every
-// 4 KiB-th dword of the packed codes: a re-pack into the same buffer changes the scales, so it changes the key
-uint64_t blob_fingerprint(const Blob& b, const uint8_t* base) {
+uint64_t cache_limit() {
+  HostCtx& c = hctx();
+  if (c.limit) return c.limit;
+  const uint64_t mb = uint64_t(env_int("NAD_HOST_CACHE_MB", 64 * 1024));
+  return (mb ? mb : 1) << 20;
+}
+// one host-ABI call (holds the context lock): the weights it fetches stay cached until it returns
+struct HostCall {
+  std::lock_guard<std::mutex> lk;
+  HostCall() : lk(hctx().mu) { hctx().call_start = hctx().tick + 1; }
+};
+// O(1) per-call key: FNV-1a over the 64-byte header, the blob size and 64 dwords at fixed positions spread over the
+// whole blob (codes and scales).  Rewrites through this library's pack entries are caught exactly (they drop the
+// entry, invalidate_host_weight); the samples catch a re-pack of another matrix into the same buffer.
+uint64_t blob_key(const Blob& b, const uint8_t* base) {
   uint64_t h = 1469598103934665603ull;
   auto mix = [&](const uint8_t* p, size_t n) {
     for (size_t i = 0; i < n; i++) h = (h ^ p[i]) * 1099511628211ull;
   };
   mix(base, 64);
-  mix(base + b.s_off, b.s_size);
-  if (b.asym) mix(base + b.z_off, b.z_size);
-  for (uint64_t o = 0; o + 4 <= b.q_size; o += 4096) mix(base + b.q_off + o, 4);
   mix(reinterpret_cast<const uint8_t*>(&b.size), sizeof(b.size));
+  if (b.size >= 8) {
+    const uint64_t span = (b.size - 4) & ~uint64_t(3);
+    for (uint64_t i = 0; i < 64; i++) mix(base + (span * i / 63 & ~uint64_t(3)), 4);
+  }
   return h;
 }
 void drop_cached(const void* blob) {
@@ -1415,9 +1501,26 @@ void drop_cached(const void* blob) {
   if (it == c.cache.end()) return;
   if (c.dev) (void)hipStreamSynchronize(c.dev->stream);
   (void)hipFree(it->second.mem);
+  c.cached_bytes -= it->second.bytes;
   c.cache.erase(it);
 }
-// device copy of a host blob, created on first use and refreshed when the blob's bytes change
+// least recently used entries out until the cache fits its cap (not those of the running call)
+void evict_to_limit() {
+  HostCtx& c = hctx();
+  const uint64_t lim = cache_limit();
+  while (c.cached_bytes > lim) {
+    const void* victim = nullptr;
+    uint64_t oldest = UINT64_MAX;
+    for (auto& kv : c.cache)
+      if (kv.second.last_use < c.call_start && kv.second.last_use < oldest) {
+        oldest = kv.second.last_use;
+        victim = kv.first;
+      }
+    if (!victim) break;
+    drop_cached(victim);
+  }
+}
+// device copy of a host blob, created on first use and refreshed when the blob's key changes
 const DeviceWeight* cached_weight(void* blob) {
   HostCtx& c = hctx();
   Blob b;
@@ -1426,9 +1529,12 @@ const DeviceWeight* cached_weight(void* blob) {
     set_err("%s", err.c_str());
     return nullptr;
   }
-  const uint64_t fp = blob_fingerprint(b, static_cast<const uint8_t*>(blob));
+  const uint64_t key = blob_key(b, static_cast<const uint8_t*>(blob));
   auto it = c.cache.find(blob);
-  if (it != c.cache.end() && it->second.size == b.size && it->second.fingerprint == fp) return &it->second.w;
+  if (it != c.cache.end() && it->second.size == b.size && it->second.key == key) {
+    it->second.last_use = ++c.tick;
+    return &it->second.w;
+  }
   drop_cached(blob);
   NadDevice* d = host_device();
   if (!d) return nullptr;
@@ -1446,8 +1552,12 @@ const DeviceWeight* cached_weight(void* blob) {
   }
   cw.mem = mem;
   cw.size = b.size;
-  cw.fingerprint = fp;
+  cw.key = key;
+  cw.bytes = need;
+  cw.last_use = ++c.tick;
+  c.cached_bytes += need;
   auto res = c.cache.emplace(blob, cw);
+  evict_to_limit();
   return &res.first->second.w;
 }
 bool is_device_ptr(const void* p) {
@@ -1537,7 +1647,7 @@ extern "C" unsigned long long bestla_fusion_FFN_f32f32_get_workspace_size(int se
 
 static int host_forward(float* act, void* wblob, float* out, int m, int n, int k, int lda, int ldo, int epi,
                         const float* bias, int bias_ld) {
-  std::lock_guard<std::mutex> lk(hctx().mu);
+  HostCall call;
   const DeviceWeight* w = cached_weight(wblob);
   if (!w) return -1;
   NadDevice* d = host_device();
@@ -1598,7 +1708,7 @@ extern "C" void bestla_fusion_QKV_f32f32_forward(float* activation, void* wqptr,
                                                  float* output, int _m, int _n, int _k, int lda, int ldo,
                                                  void* workspace) {
   // ip_fusion_qkv.cpp:22-40: Q, K, V written to output, output + M*ldo, output + 2*M*ldo
-  std::lock_guard<std::mutex> lk(hctx().mu);
+  HostCall call;
   const DeviceWeight* w[3] = {cached_weight(wqptr), cached_weight(wkptr), cached_weight(wvptr)};
   if (!w[0] || !w[1] || !w[2]) {
     report("bestla_fusion_QKV_f32f32_forward");
@@ -1640,7 +1750,7 @@ extern "C" bool bestla_fusion_FFN_Gelu_Mul_f32f32_support(void* w1ptr, void* w2p
 
 static void host_ffn3(float* act, void* w1p, void* w2p, void* w3p, float* tmp1, float* tmp2, float* out, int seq,
                       int fin, int fmid, int fout, int epi, const char* name) {
-  std::lock_guard<std::mutex> lk(hctx().mu);
+  HostCall call;
   const DeviceWeight* w1 = cached_weight(w1p);
   const DeviceWeight* w2 = cached_weight(w2p);
   const DeviceWeight* w3 = cached_weight(w3p);
@@ -1692,7 +1802,7 @@ extern "C" bool bestla_fusion_FFN_Add_GeLu_f32f32_support(void* w1ptr, void* w2p
 
 static void host_ffn2(float* act, void* w1p, void* w2p, const float* b1, const float* b2, float* tmp1, float* out,
                       int seq, int fin, int fmid, int fout, bool add, bool bcast, const char* name) {
-  std::lock_guard<std::mutex> lk(hctx().mu);
+  HostCall call;
   const DeviceWeight* w1 = cached_weight(w1p);
   const DeviceWeight* w2 = cached_weight(w2p);
   if (!w1 || !w2) {
@@ -1746,6 +1856,37 @@ extern "C" void nad_host_cache_clear(void) {
   if (c.dev) (void)hipStreamSynchronize(c.dev->stream);
   for (auto& kv : c.cache) (void)hipFree(kv.second.mem);
   c.cache.clear();
+  c.cached_bytes = 0;
+}
+
+extern "C" void nad_host_cache_evict(const void* blob) { invalidate_host_weight(blob); }
+
+extern "C" size_t nad_host_cache_set_limit(size_t bytes) {
+  HostCtx& c = hctx();
+  std::lock_guard<std::mutex> lk(c.mu);
+  const size_t prev = cache_limit();
+  c.limit = bytes;
+  c.call_start = c.tick + 1;
+  evict_to_limit();
+  return prev;
+}
+
+extern "C" int nad_host_cache_stats(size_t* entries, size_t* bytes) {
+  HostCtx& c = hctx();
+  std::lock_guard<std::mutex> lk(c.mu);
+  if (entries) *entries = c.cache.size();
+  if (bytes) *bytes = c.cached_bytes;
+  return 0;
+}
+
+extern "C" unsigned long long nad_host_blob_key(const void* blob) {
+  Blob b;
+  std::string err;
+  if (!blob || !b.parse(blob, &err)) {
+    set_err("%s", err.c_str());
+    return 0;
+  }
+  return blob_key(b, static_cast<const uint8_t*>(blob));
 }
 
 // ------------------------------------------------------------------------------------------------ pack API
@@ -1963,6 +2104,7 @@ extern "C" size_t nad_blob_split(const void* src, int axis, int rank, int world,
     gidx.resize(b.k);
     for (int p = 0; p < b.k; p++) gidx[shf[p]] = p / b.blocksize;
   }
+  invalidate_host_weight(dst);
   o.write_header(static_cast<int8_t*>(dst));
   if (!pack_quantized(o, static_cast<int8_t*>(dst), Q2.data(), n2, S2.data(), b.asym ? Z2.data() : nullptr,
                       b.has_shuffle ? gidx.data() : nullptr, &err)) {

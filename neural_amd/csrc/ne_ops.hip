@@ -471,10 +471,15 @@ extern "C" int bestla_backend_support(struct ne_tensor* src0p, struct ne_tensor*
 }
 
 extern "C" size_t nad_device_workspace_size(int m, int k) {
-  if (m <= 16) return 0;  // decode GEMV stages its activations in LDS
+  // K padded to the largest device K tile (256: int2), so the bound holds for every weight format
+  const size_t kp = (size_t(k) + 255) / 256 * 256;
+  auto a256 = [](size_t x) { return (x + 255) / 256 * 256; };
+  // m <= 16: the fp decode GEMV stages its activations in LDS; a weight in the int8-compute mode quantizes them into
+  // u8 codes [m][kp] + per-(row, block) {scale, zp} (block >= 32)
+  if (m <= 16) return a256(size_t(m) * kp) + a256(size_t(m) * (kp / 32) * 8) + 256;
   // fp16 copy of A (tile padded), then the split-K partials of a GEMM with few output tiles (bound for any N)
   const size_t nbm = (size_t(m) + 255) / 256;
-  return (size_t(m) * ((size_t(k) + 127) / 128 * 128) * 2 + 255) / 256 * 256 + size_t(m) * 4 * 256 * 128 / nbm + 256;
+  return a256(size_t(m) * kp * 2) + size_t(m) * 4 * 256 * 128 / nbm + 256;
 }
 
 // ne_bestla.cpp:205-249 + the device workspace of this backend's prefill GEMM (the reference's SYCL path reports 0)

@@ -257,6 +257,7 @@ struct parallel_context {
   PeerPtrs peers{};
   uint32_t* ctl = nullptr;
   bool oneshot = false;
+  bool oneshot_uncached = false;  // the one-shot buffer is fine-grained uncached memory (else the hipMalloc fallback)
   // host staging
   float* stage = nullptr;
   size_t stage_bytes = 0;
@@ -313,6 +314,7 @@ bool oneshot_init(parallel_context* p) {
     }
     if (hipIpcGetMemHandle(&h, p->own) == hipSuccess) {
       have = true;
+      p->oneshot_uncached = attempt == 0;
     } else {
       (void)hipGetLastError();
       (void)hipFree(p->own);
@@ -539,8 +541,15 @@ extern "C" void broadcast(parallel_context* p, float* buffer, size_t count) {
 extern "C" void alltoall(parallel_context* p, float* send_buffer, float* recv_buffer, size_t count) {
   if (!p) return;
   std::lock_guard<std::mutex> lk(p->mu);
-  if (p->world == 1) {
-    if (send_buffer != recv_buffer) std::memmove(recv_buffer, send_buffer, count * 4);
+  if (p->world == 1) {  // as reduce_add: device buffers are copied on the context's stream, never by the host
+    if (send_buffer != recv_buffer) {
+      if (p->gpu && (is_dev(send_buffer) || is_dev(recv_buffer))) {
+        if (hipMemcpyAsync(recv_buffer, send_buffer, count * 4, hipMemcpyDefault, p->stream) != hipSuccess)
+          set_pc_err(p, "alltoall (world 1) copy failed");
+      } else {
+        std::memmove(recv_buffer, send_buffer, count * 4);
+      }
+    }
     return;
   }
   const size_t tot = count * size_t(p->world);
@@ -600,10 +609,11 @@ extern "C" int nad_pc_status(parallel_context* p) {
   return int(c[2]);
 }
 
-// bit 0: GPU transport, bit 1: one-shot IPC all-reduce available, bit 2: RCCL communicator up
+// bit 0: GPU transport, bit 1: one-shot IPC all-reduce available, bit 2: RCCL communicator up, bit 3: the one-shot
+// buffer is uncached fine-grained memory (hipExtMallocWithFlags(hipDeviceMallocUncached)), not the hipMalloc fallback
 extern "C" int nad_pc_info(parallel_context* p) {
   if (!p) return -1;
-  return (p->gpu ? 1 : 0) | (p->oneshot ? 2 : 0) | (p->comm ? 4 : 0);
+  return (p->gpu ? 1 : 0) | (p->oneshot ? 2 : 0) | (p->comm ? 4 : 0) | (p->oneshot && p->oneshot_uncached ? 8 : 0);
 }
 
 extern "C" const char* nad_pc_last_error(parallel_context* p) { return p ? p->err.c_str() : "no parallel context"; }

@@ -81,8 +81,13 @@ __global__ __launch_bounds__(256) void quant_u8_kernel(QuantU8Args a) {
 template <int BITS>
 __device__ __forceinline__ void b_step(const u4_t& b, int d, uint32_t bias, uint32_t& lo, uint32_t& hi) {
   if constexpr (BITS == 8) {
-    lo = b[2 * d] ^ 0x80808080u;  // byte - 128 (symmetric only)
-    hi = b[2 * d + 1] ^ 0x80808080u;
+    // byte = q + 128 (S5..S8); q - zp fits s8 for every format the int8 core takes (S8 is symmetric there,
+    // bestla_gemm.cpp:250), so add bias = (-zp) mod 256 per byte without carries between bytes (SWAR byte add)
+    auto add_bytes = [](uint32_t x, uint32_t y) {
+      return ((x & 0x7f7f7f7fu) + (y & 0x7f7f7f7fu)) ^ ((x ^ y) & 0x80808080u);
+    };
+    lo = add_bytes(b[2 * d] ^ 0x80808080u, bias);
+    hi = add_bytes(b[2 * d + 1] ^ 0x80808080u, bias);
     return;
   } else {
     constexpr int SH = BITS;                    // field stride between the two elements sharing a byte pair

@@ -55,6 +55,8 @@ struct DeviceWeight {
   int32_t blob_bs;    // the blob's own block size (per-channel: may exceed K; the int8-compute quantizer uses it)
   int32_t f4kind;     // NFloat weight: 0 F4_BNB, 1 F4_E2M1, 2 F4_NF4 (codes in the int4 layout, LUT dequant),
                       // 3 F8_E4M3, 4 F8_E5M2 (raw codes in the int8 layout); -1 = integer
+  int32_t compute;    // per-weight arithmetic (nad_device_set_compute): 0 follow the thread / process mode, 1 fp,
+                      // 2 int8 (integer-core blobs and Q4_0 only)
 };
 
 // Tile (s, t) and scale row (s, g) positions.  K-major interleaves the stripes at every K position, so the waves of a
@@ -94,6 +96,7 @@ inline uint64_t layout_geometry(DeviceWeight& w, int bits, int n, int k, int blo
   w.red_ld = reduce ? w.ns * 16 : 0;
   w.blob_bs = blocksize;
   w.f4kind = -1;
+  w.compute = 0;
   uint64_t rbytes = uint64_t(w.ng) * w.red_ld * 2;
   return align256(tiles) + align256(sbytes) + align256(zbytes) + align256(shf) + align256(rbytes);
 }

@@ -37,7 +37,8 @@ class ParallelContext:
 
     def info(self):
         v = self.L.nad_pc_info(self.p)
-        return {"gpu": bool(v & 1), "oneshot": bool(v & 2), "rccl": bool(v & 4)}
+        return {"gpu": bool(v & 1), "oneshot": bool(v & 2), "rccl": bool(v & 4),
+                "oneshot_alloc": ("uncached" if v & 8 else "hipMalloc") if v & 2 else None}
 
     def _err(self, what):
         e = self.L.nad_pc_last_error(self.p)

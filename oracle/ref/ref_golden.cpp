@@ -374,6 +374,21 @@ static void case_f8(const char* cs, int row, int col, int bs, BTLA_DTYPE sdt, fl
   dump(cs, "dec", "f4", dec.data(), 256);
 }
 
+// kernel_ref.h:2199-2240 layernorm<float> as BTLALayerNorm drives it (bestla_gemm.cpp:751-776: no scale / bias,
+// simplified = isrms), one row at a time -- the reference of bestla_layernormalization (ne_bestla.cpp:113-116)
+static void case_layernorm(const char* cs, int rows, int size, bool isrms, float eps, float amp, float offset) {
+  std::vector<float> src((size_t)rows * size), dst((size_t)rows * size);
+  for (auto& v : src) v = offset + urand(-amp, amp);
+  for (int r = 0; r < rows; r++)
+    kernel::ref::layernorm<float>(src.data() + (size_t)r * size, nullptr, nullptr, eps, size,
+                                  dst.data() + (size_t)r * size, nullptr, nullptr, isrms);
+  int meta[3] = {rows, size, isrms ? 1 : 0};
+  dump(cs, "meta", "i4", meta, 3);
+  dump(cs, "eps", "f4", &eps, 1);
+  dump(cs, "src", "f4", src.data(), src.size());
+  dump(cs, "dst", "f4", dst.data(), dst.size());
+}
+
 int main(int argc, char** argv) {
   if (argc < 2) {
     fprintf(stderr, "usage: %s <outdir>\n", argv[0]);
@@ -430,6 +445,10 @@ int main(int argc, char** argv) {
   case_compress_bit1("compress_bit1", 4096);
   case_quant("quant_s1_sym_g32", 128, 37, 32, BTLA_DTYPE::S1_CLIP, false, 1);
   case_quant("quant_s1_asym_g64", 128, 13, 64, BTLA_DTYPE::S1_CLIP, true, 0);
+  case_layernorm("layernorm_rms_4096", 5, 4096, true, 1e-5f, 2.f, 0.f);
+  case_layernorm("layernorm_ln_300", 7, 300, false, 1e-6f, 1.f, 0.75f);
+  case_layernorm("layernorm_rms_11008", 2, 11008, true, 1e-6f, 40.f, 0.f);
+  case_layernorm("layernorm_ln_4096", 3, 4096, false, 1e-5f, 3.f, -1.5f);
   fclose(g_man);
   return 0;
 }

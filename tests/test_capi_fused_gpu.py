@@ -13,7 +13,7 @@ import numpy as np
 import pytest
 
 from tests.conftest import gpu_available
-from tests.oracle_lib import F16, S4
+from tests.oracle_lib import F16, F32, S2, S4
 from tests.test_gpu_parity import _blob, _rel_err
 
 pytestmark = pytest.mark.gpu
@@ -200,3 +200,102 @@ def test_device_forward_uses_caller_workspace_and_capture_contract(oracle):
     torch.cuda.synchronize()
     assert _rel_err(y2.cpu().numpy(), ref) <= 1e-3
     L.nad_bind_workspace(C.c_void_p(st2.cuda_stream), None, 0)
+
+
+def test_host_cache_code_only_rewrite_and_lru_bound(oracle):
+    """(1) a rewrite that changes only the CODES and keeps every scale, through the pack API
+    (BTLAGemmPackB into the same buffer) or by another writer followed by nad_host_cache_evict, is seen by the next
+    forward; (2) the cache is bounded by device bytes, least recently used first out, and results stay exact when
+    entries are evicted and re-uploaded."""
+    L = _lib.lib()
+    n, k, m = 128, 512, 2
+    rng = np.random.default_rng(3)
+    A = rng.uniform(-1, 1, size=(m, k)).astype(np.float32)
+    s = rng.uniform(0.001, 0.01, size=(k // 128, n)).astype(np.float32)
+    size = L.BTLAGemmPackBSize(n, k, 128, S4, F32, False, 4, None)
+    buf = bestla._aligned_buffer(size)
+    L.nad_host_cache_clear()
+
+    def fwd(b):
+        out = np.zeros((m, n), np.float32)
+        L.bestla_f32f32_forward(vp(A), vp(b), vp(out), m, n, k, k, n, None)
+        assert _lib.last_error() == ""
+        return out
+    for seed in (1, 2):  # same scales, new codes, through the pack API
+        q = np.random.default_rng(seed).integers(-8, 8, size=(k, n), dtype=np.int8)
+        assert L.BTLAGemmPackB(vp(buf), vp(q), vp(s), None, n, k, n, 128, S4, F32, False, 4, None, None)
+        assert _rel_err(fwd(buf), oracle.forward(A, buf, n, k)) <= 2e-5, seed
+    # another writer flips ONE code byte (no API call): evict, and the forward follows it
+    info = bestla.blob_info(buf)
+    buf[info["q_off"] + 7] ^= 0x11
+    L.nad_host_cache_evict(vp(buf))
+    assert _rel_err(fwd(buf), oracle.forward(A, buf, n, k)) <= 2e-5
+    # LRU bound: room for two of these weights -> at most two entries, every forward still exact
+    e, b = C.c_size_t(0), C.c_size_t(0)
+    L.nad_host_cache_stats(C.byref(e), C.byref(b))
+    one = b.value
+    assert e.value == 1 and one > 0
+    prev = L.nad_host_cache_set_limit(2 * one + 16)
+    try:
+        blobs = [_wb(oracle, n, k, 40 + i) for i in range(4)]
+        for rnd in range(2):
+            for bl in blobs:
+                assert _rel_err(fwd(bl), oracle.forward(A, bl, n, k)) <= 2e-5
+                L.nad_host_cache_stats(C.byref(e), C.byref(b))
+                assert e.value <= 2 and b.value <= 2 * one + 16
+    finally:
+        L.nad_host_cache_set_limit(prev)
+        L.nad_host_cache_clear()
+
+
+def test_qkv_prefill_mixed_formats_keep_their_activations(oracle):
+    """the shared fp16 activation copy of a QKV prefill must not be reused after a weight that rewrote the
+    workspace (other K tile: int4 / int2 / int4; or an int8-compute weight in the middle)."""
+    m, k = 64, 1024
+    bq = _blob(oracle, 256, k, 128, S4, F16, False, 1, seed=71)
+    bk = _blob(oracle, 128, k, 64, S2, F16, False, 1, seed=72)
+    bv = _blob(oracle, 128, k, 128, S4, F16, False, 1, seed=73)
+    bi = _blob(oracle, 128, k, 32, S4, F32, False, 4, seed=74)      # integer core: int8-capable
+    x = torch.from_numpy(np.random.default_rng(9).uniform(-1, 1, size=(m, k)).astype(np.float32)).cuda()
+    xa = x.cpu().numpy()
+    wq, wk, wv, wi = (bestla.DeviceWeight(b) for b in (bq, bk, bv, bi))
+    oq, ok, ov = bestla.qkv_forward(x, wq, wk, wv)
+    for o, b, n in ((oq, bq, 256), (ok, bk, 128), (ov, bv, 128)):
+        assert _rel_err(o.cpu().numpy(), oracle.forward(xa, b, n, k)) <= 1e-3
+    wi.set_compute(bestla.COMPUTE_INT8)
+    assert wi.compute == bestla.COMPUTE_INT8 and wq.compute == bestla.COMPUTE_FP
+    oq, oi, ov = bestla.qkv_forward(x, wq, wi, wv)
+    assert _rel_err(oq.cpu().numpy(), oracle.forward(xa, bq, 256, k)) <= 1e-3
+    assert _rel_err(oi.cpu().numpy(), oracle.forward_int8(xa, bi, 128, k)) <= 1e-5
+    assert _rel_err(ov.cpu().numpy(), oracle.forward(xa, bv, 128, k)) <= 1e-3
+
+
+@pytest.mark.parametrize("m", [1, 4, 64])
+def test_per_weight_compute_mode(oracle, m):
+    """the int8-compute arithmetic is chosen per weight (the reference: per blob core,
+    bestla_gemm.cpp:516-616) and per thread, not only by a process-global switch; a fused decode QKV whose weights
+    resolve to different arithmetic runs each in its own."""
+    k = 512
+    b8 = [_blob(oracle, 128, k, 32, S4, F32, False, 4, seed=80 + i) for i in range(3)]   # integer-core blobs
+    ws = [bestla.DeviceWeight(b) for b in b8]
+    A = np.random.default_rng(m).uniform(-1, 1, size=(m, k)).astype(np.float32)
+    x = torch.from_numpy(A).cuda()
+    assert bestla.get_compute_mode() == bestla.COMPUTE_FP
+    assert all(w.compute == bestla.COMPUTE_FP for w in ws)
+    ws[1].set_compute(bestla.COMPUTE_INT8)
+    outs = bestla.qkv_forward(x, *ws)
+    for i, (o, b) in enumerate(zip(outs, b8)):
+        ref = oracle.forward_int8(A, b, 128, k) if i == 1 else oracle.forward(A, b, 128, k)
+        assert _rel_err(o.cpu().numpy(), ref) <= (1e-5 if i == 1 else (2e-5 if m <= 16 else 1e-3)), i
+    # the thread override switches the weights that follow it; the per-weight setting still wins
+    ws[0].set_compute(bestla.COMPUTE_FP)
+    bestla.set_thread_compute_mode(bestla.COMPUTE_INT8)
+    try:
+        assert [w.compute for w in ws] == [bestla.COMPUTE_FP, bestla.COMPUTE_INT8, bestla.COMPUTE_INT8]
+        y2 = ws[2].forward(x).cpu().numpy()
+        assert _rel_err(y2, oracle.forward_int8(A, b8[2], 128, k)) <= 1e-5
+    finally:
+        bestla.set_thread_compute_mode(None)
+    assert ws[2].compute == bestla.COMPUTE_FP
+    ws[1].set_compute(None)
+    assert ws[1].compute == bestla.COMPUTE_FP

@@ -10,7 +10,7 @@ import numpy as np
 import pytest
 
 from tests.conftest import gpu_available
-from tests.oracle_lib import BF16, F16, F32, S2, S4, S8, load_ref_golden
+from tests.oracle_lib import BF16, F16, F32, S2, S4, S5, S6, S7, S8, load_ref_golden
 from tests.test_gpu_parity import _blob, _rel_err
 
 pytestmark = pytest.mark.gpu
@@ -69,6 +69,10 @@ I8_CASES = [
     (128, 512, 32, S8, F32, False, False),      # int8 sym
     (64, 512, 128, S4, F32, True, True),        # act-order shuffle (gather before quantization)
     (48, 300, 32, S4, F32, False, False),       # K tail inside a tile and a block
+    # 5/6/7-bit asym (int8 device layout q + 128 with separate zero points; ADVICE r2: the zp was dropped there)
+    (96, 512, 32, S5, F32, True, False),
+    (64, 768, 64, S6, BF16, True, False),
+    (80, 512, 128, S7, F32, True, False),
 ]
 
 

@@ -147,3 +147,43 @@ def test_llama_int4_g128_asym(oracle, shape):
     if name != "lm_head":
         _check(oracle, blob, n, k, 2048, "fp32", seed=13)
         _check(oracle, blob, n, k, 2048, "fp16", seed=14)
+
+
+def _llama_sym(oracle, n, k, seed):
+    return _qblob(oracle, n, k, 128, 4, False, stype=F16, seed=seed)
+
+
+def test_llama_sym_headline_qkv_three_weight_launch(oracle):
+    """the headline's fused QKV launch at full width -- ONE woq_gemv_m1_kernel launch streaming three
+    4096 x 4096 int4 g128 sym weights (fp16 scales, as the bench's synthetic stack) with fp32 activations at M = 1 --
+    against the oracle, each output."""
+    H = 4096
+    blobs = [_llama_sym(oracle, H, H, seed=900 + i) for i in range(3)]
+    ws = [bestla.DeviceWeight(b) for b in blobs]
+    A = np.random.default_rng(21).uniform(-0.5, 0.5, size=(1, H)).astype(np.float32)
+    outs = bestla.qkv_forward(torch.from_numpy(A).cuda(), *ws)
+    for o, b in zip(outs, blobs):
+        assert _rel_err(o.cpu().numpy(), oracle.forward(A, b, H, H)) <= TOL[("decode", "fp32")]
+
+
+def test_llama_sym_headline_gate_up_dual_launch(oracle):
+    """The headline's dual gate/up launch at N = 11008 (SiLU(x.W1) * (x.W3) formed in registers) vs the oracle."""
+    H, F = 4096, 11008
+    b1, b3 = _llama_sym(oracle, F, H, seed=910), _llama_sym(oracle, F, H, seed=911)
+    w1, w3 = bestla.DeviceWeight(b1), bestla.DeviceWeight(b3)
+    A = np.random.default_rng(22).uniform(-0.5, 0.5, size=(1, H)).astype(np.float32)
+    t = bestla.ffn_gate_up(torch.from_numpy(A).cuda(), w1, w3, act="silu").cpu().numpy()
+    g = oracle.forward(A, b1, F, H).astype(np.float64)
+    u = oracle.forward(A, b3, F, H).astype(np.float64)
+    ref = g / (1.0 + np.exp(-g)) * u
+    assert _rel_err(t, ref) <= 1e-4          # product of two 2e-5 GEMMs through SiLU
+
+
+@pytest.mark.parametrize("shape", [("down", 4096, 11008), ("lm_head", 32000, 4096), ("o", 4096, 4096)],
+                         ids=["down", "lm_head", "o"])
+def test_llama_sym_headline_single_launches(oracle, shape):
+    """down (K = 11008: 86 K tiles, 43 two-tile slices), lm_head (N = 32000) and O at M = 1, fp32 activations, sym
+    fp16-scale weights: the exact instantiations the headline token runs."""
+    name, n, k = shape
+    blob = _llama_sym(oracle, n, k, seed=920 + n + k)
+    _check(oracle, blob, n, k, 1, "fp32", seed=23)

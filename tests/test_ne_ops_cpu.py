@@ -27,13 +27,37 @@ def test_support_mul_mat_workspaces():
         # host weight: the reference's workspace contract M * padto(K, 128) * 4 (inner_product.cpp:20-25)
         assert ok and node.n_tasks == 1 and ws == m * 4096 * 4 and dws == 0
     w.backend = BACKEND_DEVICE
-    for m, want in ((1, 0), (16, 0), (2048, L.nad_device_workspace_size(2048, 4096))):
+    for m in (1, 16, 2048):
+        want = L.nad_device_workspace_size(m, 4096)
         x = tensor([4096, m])
         node = tensor([4096, m], op=OP["MUL_MAT"], backend=BACKEND_DEVICE)
         node.src0, node.src1 = C.pointer(w), C.pointer(x)
         ok, ws, dws = _support(node)
         assert ok and ws == 0 and dws == want
     assert L.nad_device_workspace_size(2048, 4096) >= 2048 * 4096 * 2      # fp16 copy of A
+
+
+def _a256(x):
+    return -(-x // 256) * 256
+
+
+def test_workspace_bound_covers_every_k_tile():
+    """nad_device_workspace_size bounds what the forward places in the workspace for any weight format: the fp16 copy
+    of A padded to the weight's K tile (int2: 256, so K mod 256 in 1..128 needs more than a 128-rounded bound) plus the
+    split-K partials behind it; at m <= 16 the int8-compute mode's u8 codes + per-block {scale, zp}."""
+    L = _lib.lib()
+    for k in (4096, 4097, 4160, 4224, 4300, 11008, 300, 33):
+        for m in (1, 5, 16):
+            kp = -(-k // 256) * 256
+            need = _a256(m * kp) + _a256(m * (kp // 32) * 8)          # i8_act_bytes at the smallest group (32)
+            assert L.nad_device_workspace_size(m, k) >= need, (m, k)
+        for m in (17, 300, 2048):
+            for ktile in (64, 128, 256):
+                kp = -(-k // ktile) * ktile
+                a16 = _a256(m * kp * 2)
+                # split-K partials: ks runs x m x ldp fp32, ks x ceil(m/256) x ceil(N/128) <= 256 -> N-independent
+                part = 4 * m * 256 * 128 // -(-m // 256)
+                assert L.nad_device_workspace_size(m, k) >= a16 + part, (m, k, ktile)
 
 
 def test_support_elementwise_rules():

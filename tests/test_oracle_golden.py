@@ -276,3 +276,20 @@ def test_f8_quantizer_and_decode_bit_exact(oracle, case, t):
     oracle.lib.orc_quantize_f8_rowblock(src.ctypes.data, q.ctypes.data, row, col, col, col, s.ctypes.data, bs, t, e8m0)
     assert np.array_equal(s.ravel().view(np.uint32), g["s"].view(np.uint32))
     assert np.array_equal(q.ravel(), g["q"])
+
+
+def test_layernorm_golden_is_the_stated_formula():
+    """The layernorm goldens (kernel_ref.h:2199-2240 via oracle/ref/ref_golden.cpp) are what the numpy restatement used
+    by the device-op tests says: x / sqrt(mean(x^2) + eps) (RMS) or (x - mean) / sqrt(mean(x^2) - mean^2 + eps)."""
+    G = load_ref_golden()
+    for case in ("layernorm_rms_4096", "layernorm_ln_300", "layernorm_rms_11008", "layernorm_ln_4096"):
+        g = G[case]
+        rows, size, rms = (int(v) for v in g["meta"])
+        eps = float(g["eps"][0])
+        x = g["src"].reshape(rows, size).astype(np.float64)
+        mean = x.mean(-1, keepdims=True)
+        ms = np.sqrt((x ** 2).mean(-1, keepdims=True) + eps) if rms else \
+            np.sqrt((x ** 2).mean(-1, keepdims=True) - mean ** 2 + eps)
+        ref = x / ms if rms else (x - mean) / ms
+        d = g["dst"].reshape(rows, size).astype(np.float64)
+        assert np.abs(d - ref).max() / np.abs(ref).max() <= 2e-5, case

@@ -47,8 +47,9 @@ def _worker(rank, world, port, q):
         from neural_amd.parallel_context import ParallelContext
         ctx = ParallelContext()
         assert ctx.get_tp_size() == world and ctx.get_tp_rank() == rank
+        info = ctx.info()
         if world > 1:
-            assert ctx.info()["oneshot"], "one-shot IPC all-reduce unavailable"
+            assert info["oneshot"], "one-shot IPC all-reduce unavailable"
         spec = {"wq": (".attention.wq.weight", D, D), "wo": (".attention.wo.weight", D, D),
                 "w1": (".feed_forward.w1.weight", F, D), "w3": (".feed_forward.w3.weight", F, D),
                 "w2": (".feed_forward.w2.weight", D, F)}
@@ -58,6 +59,7 @@ def _worker(rank, world, port, q):
             shard, rng_ = tp.shard_blob(b, tp.split_type("layers.0" + name), rank, world, unit=GS)
             W[key] = bestla.DeviceWeight(shard)
             FULL[key] = bestla.DeviceWeight(b)
+            info["range_" + key] = rng_
         out, ref = {}, {}
         for m in (1, 48):
             x = torch.from_numpy(np.random.default_rng(m).uniform(-1, 1, size=(m, D)).astype(np.float32)).cuda()
@@ -97,7 +99,7 @@ def _worker(rank, world, port, q):
         assert ctx.status() == 0
         ctx.barrier()
         ctx.destroy()
-        q.put((rank, out, graph_ok, ref))
+        q.put((rank, out, graph_ok, ref, info))
     except Exception as e:
         import traceback
         q.put((rank, "ERR", traceback.format_exc() + str(e)))
@@ -119,14 +121,13 @@ def _run(world):
     return sorted(res, key=lambda r: r[0])
 
 
-@pytest.mark.skipif(not gpu_available(), reason="needs a GPU")
-def test_tp2_hip_kernels_match_tp1():
+def _check_tp(world):
     single = _run(1)[0]
-    multi = _run(2)
+    multi = _run(world)
     for m in (1, 48):   # TP=1 computed in the world-1 run and in each rank agree bit for bit
         np.testing.assert_array_equal(single[1][m], single[3][m])
         np.testing.assert_array_equal(multi[0][3][m], single[3][m])
-    for _, out, graph_ok, _ in multi:
+    for _, out, graph_ok, _, _ in multi:
         assert graph_ok, "graph-replayed one-shot all-reduce gave a wrong sum"
         for m in (1, 48):
             ref = single[1][m].astype(np.float64)
@@ -134,9 +135,30 @@ def test_tp2_hip_kernels_match_tp1():
             # M=48 rounds each GEMM input to fp16: a 1e-7 change of h from the all-reduce order can move an element
             # across an fp16 rounding boundary (one ulp = 1e-3 of that element) -> allow 2e-4 there
             assert err <= (1e-5 if m == 1 else 2e-4), (m, err)
-    # both ranks hold the identical reduced result (rank-order summation)
+    # every rank holds the identical reduced result (rank-order summation)
     for m in (1, 48):
-        np.testing.assert_array_equal(multi[0][1][m], multi[1][1][m])
+        for r in range(1, world):
+            np.testing.assert_array_equal(multi[0][1][m], multi[r][1][m])
+    return multi
+
+
+@pytest.mark.skipif(not gpu_available(), reason="needs a GPU")
+def test_tp2_hip_kernels_match_tp1():
+    _check_tp(2)
+
+
+@pytest.mark.skipif(not gpu_available(), reason="needs a GPU")
+def test_tp4_uneven_k_shards_match_tp1():
+    """World 4 on the one GPU: F = 2816 = 22 groups of 128 -> the row-parallel down weight gets
+    UNEVEN K shards 6/6/5/5 groups (model_files.h:134-235 requires even splits; here whole groups, exact), the gate/up
+    column shards line up with them, and which one-shot allocation actually ran is recorded."""
+    multi = _check_tp(4)
+    ranges = [r[4]["range_w2"] for r in multi]
+    assert ranges == [(0, 768), (768, 1536), (1536, 2176), (2176, 2816)], ranges
+    assert [r[4]["range_w1"] for r in multi] == ranges                 # gate/up N shard == down K shard
+    allocs = {r[4]["oneshot_alloc"] for r in multi}
+    assert len(allocs) == 1 and allocs <= {"uncached", "hipMalloc"}, allocs
+    print(f"\nTP=4 one-shot all-reduce buffer: {allocs.pop()} (nad_pc_info bit 3); down K shards {ranges}")
 
 
 def _rccl_worker(q):

@@ -57,6 +57,13 @@ def main():
                     "dispatches": n, "traffic_over_algorithmic": round((fb + wb) / a, 4)}
         print(fam, rec[fam])
     json.dump(rec, open(out, "w"), indent=1)
+    # bench.py reads the newest round's last-listed file (bench.latest_pmc)
+    import os
+    import re
+    m = re.match(r"(r\d+)_", os.path.basename(out))
+    if m:
+        with open(os.path.join(os.path.dirname(os.path.abspath(out)), f"{m.group(1)}_pmc_latest.txt"), "a") as f:
+            f.write(os.path.basename(out) + "\n")
 
 
 if __name__ == "__main__":
