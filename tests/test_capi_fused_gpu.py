@@ -218,6 +218,7 @@ def test_host_cache_code_only_rewrite_and_lru_bound(oracle):
 
     def fwd(b):
         out = np.zeros((m, n), np.float32)
+        L.nad_clear_error()
         L.bestla_f32f32_forward(vp(A), vp(b), vp(out), m, n, k, k, n, None)
         assert _lib.last_error() == ""
         return out

@@ -226,7 +226,8 @@ LN_GOLDEN = ["layernorm_rms_4096", "layernorm_ln_300", "layernorm_rms_11008", "l
 def test_layernorm_matches_reference_golden(case, where):
     """bestla_layernormalization pinned to the REFERENCE's own output: tests/golden/ref/layernorm_* were produced by
     kernel_ref.h:2199-2240 layernorm<float> driven as BTLALayerNorm drives it (oracle/ref/ref_golden.cpp).  The
-    device kernel sums the row in a tree instead of left to right, so the bar is fp32 reduction-order noise, 2e-6."""
+    device kernel sums the row in a tree instead of left to right, so the bar is fp32 reduction-order noise: 1e-5
+    (the non-RMS form's mean(x^2) - mean^2 cancels, amplifying that noise where |mean| ~ rms)."""
     from tests.oracle_lib import load_ref_golden
     g = load_ref_golden()[case]
     rows, size, rms = (int(v) for v in g["meta"])
@@ -241,4 +242,4 @@ def test_layernorm_matches_reference_golden(case, where):
     else:
         out = np.zeros_like(x)
         _lib.lib().bestla_layernormalization(rows, size, bool(rms), eps, x.ctypes.data, out.ctypes.data)
-    assert _rel(out, g["dst"].reshape(rows, size)) <= 2e-6
+    assert _rel(out, g["dst"].reshape(rows, size)) <= TOL
