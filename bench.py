@@ -171,39 +171,52 @@ class Runner:
 
 
 class ChainRunner:
-    """The decode step as ONE persistent launch (nad_chain_*): every WOQ matmul of the token with its real data
-    dependencies -- x -> RMSNorm -> QKV -> (attention at position 0 is the identity on V) -> O + x -> RMSNorm ->
-    gate/up + SiLU*mul -> down + h -> next layer, then RMSNorm -> lm_head.  RoPE at position 0 is the identity too;
-    only the attention over a KV history (out of scope) is not modelled."""
+    """The decode step on the weight-stream engine (nad_chain_*, woq_chain.hip) with its real data dependencies:
+    x -> RMSNorm -> QKV -> (attention) -> O + x -> RMSNorm -> gate/up SiLU*mul -> down + h -> next layer ...
+    -> RMSNorm -> lm_head.  cut=True (the headline): one launch per segment between attention nodes -- the form the
+    reference graph dispatches (ne_layers.c:11915-12028; llama.cpp op order) -- i.e. [QKV_0], then per layer
+    [O, gate/up, down, next QKV] (the last: [O, gate/up, down, lm_head]): 33 launches per Llama-2-7B token.  The
+    attention between launches is outside the WOQ path; its output here is V, which is exact for a
+    single-token context (softmax over one key).  cut=False: the whole token as ONE launch (printed beside it)."""
 
-    def __init__(self, stack, m, device):
+    def __init__(self, stack, device, cut=True):
         import torch
         from neural_amd import bestla
-        H = stack.cfg["hidden"]
+        H, L = stack.cfg["hidden"], len(stack.layers)
         f = dict(dtype=torch.float32, device=device)
         g = torch.Generator(device="cpu").manual_seed(7)
-        self.xs = [(torch.rand((m, H), generator=g) - 0.5).to(device), torch.empty((m, H), **f)]
-        self.q, self.k, self.v = (torch.empty((m, stack.nq), **f) for _ in range(3))
-        self.h = torch.empty((m, H), **f)
-        self.t = torch.empty((m, stack.nf), **f)
-        self.logits = torch.empty((m, stack.nv), **f)
-        ops = []
-        for li, L in enumerate(stack.layers):
-            x, xn = self.xs[li % 2], self.xs[(li + 1) % 2]
-            ops.append(dict(kind=bestla.CHAIN_QKV, w=[L["wq"], L["wk"], L["wv"]], act=x, out=[self.q, self.k, self.v],
+        self.xs = [((torch.rand((1, H), generator=g) - 0.5)).to(device)] + [torch.empty((1, H), **f) for _ in range(L)]
+        self.q = [torch.empty((1, stack.nq), **f) for _ in range(L)]
+        self.k = [torch.empty((1, stack.nkv), **f) for _ in range(L)]
+        self.v = [torch.empty((1, stack.nkv), **f) for _ in range(L)]
+        self.h = [torch.empty((1, H), **f) for _ in range(L)]
+        self.t = [torch.empty((1, stack.nf), **f) for _ in range(L)]
+        self.logits = torch.empty((1, stack.nv), **f)
+        ops, cuts = [], [1]
+        for li, Lw in enumerate(stack.layers):
+            x = self.xs[li]
+            ops.append(dict(kind=bestla.CHAIN_QKV, w=[Lw["wq"], Lw["wk"], Lw["wv"]], act=x,
+                            out=[self.q[li], self.k[li], self.v[li]], norm=True))
+            ops.append(dict(kind=bestla.CHAIN_LINEAR, w=[Lw["wo"]], act=self.v[li], out=[self.h[li]],
+                            epi=bestla.EPI_RES_ADD, res=x))
+            ops.append(dict(kind=bestla.CHAIN_GATE_UP, w=[Lw["w1"], Lw["w3"]], act=self.h[li], out=[self.t[li]],
                             norm=True))
-            ops.append(dict(kind=bestla.CHAIN_LINEAR, w=[L["wo"]], act=self.v, out=[self.h], epi=bestla.EPI_RES_ADD,
-                            res=x))
-            ops.append(dict(kind=bestla.CHAIN_GATE_UP, w=[L["w1"], L["w3"]], act=self.h, out=[self.t], norm=True))
-            ops.append(dict(kind=bestla.CHAIN_LINEAR, w=[L["w2"]], act=self.t, out=[xn], epi=bestla.EPI_RES_ADD,
-                            res=self.h))
-        ops.append(dict(kind=bestla.CHAIN_LINEAR, w=[stack.lm_head], act=self.xs[len(stack.layers) % 2],
-                        out=[self.logits], norm=True))
-        self.chain = bestla.Chain(ops, m)
+            ops.append(dict(kind=bestla.CHAIN_LINEAR, w=[Lw["w2"]], act=self.t[li], out=[self.xs[li + 1]],
+                            epi=bestla.EPI_RES_ADD, res=self.h[li]))
+            cuts.append(len(ops) + 1)
+        ops.append(dict(kind=bestla.CHAIN_LINEAR, w=[stack.lm_head], act=self.xs[L], out=[self.logits], norm=True))
+        cuts[-1] = len(ops)
+        bounds = [0] + cuts if cut else [0, len(ops)]
+        self.chains = [bestla.Chain(ops[a:b], 1) for a, b in zip(bounds, bounds[1:])]
         self.n_ops = len(ops)
+        self.n_launches = len(self.chains)
 
     def step(self, stream=None):
-        self.chain.run(stream=stream)
+        for c in self.chains:
+            c.run(stream=stream)
+
+    def status(self):
+        return max(c.status() for c in self.chains)
 
 
 def graph_time(fn, reps, torch):
@@ -453,16 +466,22 @@ def main(argv=None):
             dt = pc.max_over_ranks(dt)
         return dt
 
-    # ---- decode (headline): M = 1.  One GPU: the faster of the whole token as one persistent chain launch
-    # (nad_chain_*) and per-op launches; tensor parallel: per-op launches + C-ABI all-reduce after O and down.
+    # ---- decode (headline): M = 1.  One GPU: the faster of the weight-stream engine cut at the attention nodes (33
+    # launches per token) and per-op launches; the whole token as one engine launch is measured beside it.
+    # Tensor parallel: per-op launches + C-ABI all-reduce after O and down.
     use_graph = not args.no_graph
     chain = None
-    chain_tok_s = None
+    chain_tok_s = uncut_tok_s = None
     if world == 1 and not args.per_op:
-        chain = ChainRunner(stack, 1, "cuda")
+        chain = ChainRunner(stack, "cuda", cut=True)
         dt_chain = timed(chain, args.steps, args.warmup, use_graph)
-        assert chain.chain.status() == 0, "decode chain hand-off timed out"
+        assert chain.status() == 0, "decode engine hand-off timed out"
         chain_tok_s = args.steps / dt_chain
+        uncut = ChainRunner(stack, "cuda", cut=False)
+        dt_uncut = timed(uncut, args.steps, args.warmup, use_graph)
+        assert uncut.status() == 0, "decode engine hand-off timed out"
+        uncut_tok_s = args.steps / dt_uncut
+        del uncut
     dec = Runner(stack, 1, pc, "cuda")
     dt_op = timed(dec, args.steps, args.warmup, use_graph)
     per_op_tok_s = args.steps / dt_op
@@ -486,9 +505,10 @@ def main(argv=None):
     per_op_time = sum(per[n] * c for n, _, _, c in L1)
     n_per_op_launches = sum(c for *_, c in L1)
     if chain is not None:
-        chain_us = graph_time(lambda s: chain.step(stream=s), 20, torch)
-        kernel, bytes_per_launch, launch_s = "woq_chain_kernel (whole decode step, one persistent launch)", tot_bytes, \
-            chain_us
+        token_s = graph_time(lambda s: chain.step(stream=s), 20, torch)
+        kernel, bytes_per_launch, launch_s = (f"woq_engine_kernel (weight-stream engine, {chain.n_launches} launches per "
+                                              f"token cut at the attention nodes)", tot_bytes / chain.n_launches,
+                                              token_s / chain.n_launches)
     else:
         kernel, bytes_per_launch, launch_s = "woq_gemv_m1_kernel (decode GEMV, one launch per matmul)", \
             tot_bytes / n_per_op_launches, per_op_time / n_per_op_launches
@@ -497,7 +517,7 @@ def main(argv=None):
     pmc = latest_pmc()
     if os.path.exists(pmc):
         try:
-            rec = json.load(open(pmc))["woq_chain_kernel" if chain is not None else "woq_gemv_m1_kernel"]
+            rec = json.load(open(pmc))["woq_engine_kernel" if chain is not None else "woq_gemv_m1_kernel"]
             traffic = int(rec["traffic_over_algorithmic"] * bytes_per_launch)
         except Exception:
             traffic = None
@@ -528,12 +548,14 @@ def main(argv=None):
             "dtype": "f16",
             "data": "synthetic: random int4 codes + fp16 group scales U[0.001,0.01] in Llama-2-7B shapes (no checkpoint)",
             "config": {"workload": "Llama-2-7B int4-g128 sym decode step, M=1: 32 x [RMSNorm, fused QKV, O + residual, "
-                                   "RMSNorm, gate/up + SiLU*mul, down + residual] + RMSNorm + lm_head, fp32 activations "
-                                   "(attention at position 0 = V)" if chain is not None else
+                                   "RMSNorm, gate/up + SiLU*mul, down + residual] + RMSNorm + lm_head, fp32 activations; "
+                                   "one engine launch per segment between attention nodes (attention output = V, exact "
+                                   "for a single-token context)" if chain is not None else
                                    "Llama-2-7B int4-g128 sym decode linear stack, M=1 (32 x [QKV, O, gate/up+SiLU*mul, "
                                    "down] + lm_head), fp32 activations", "group_size": LLAMA["group"], "batch": 1,
                        "tp": world, "parallelism": f"tp{world}", "hip_graph": use_graph,
-                       "decode_path": "chain (1 launch per token)" if chain is not None else "per-op launches"},
+                       "decode_path": f"weight-stream engine ({chain.n_launches} launches per token)"
+                       if chain is not None else "per-op launches"},
             "prefill_tflops": round(prefill_tflops, 2),
             "prefill_ms_per_2048_tokens": round(pdt / args.prefill_steps * 1e3, 3),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
@@ -541,7 +563,8 @@ def main(argv=None):
                          "traffic_source": os.path.basename(pmc) if traffic is not None else None,
                          "kernel": kernel, "bytes_per_launch": int(bytes_per_launch),
                          "avg_launch_us": round(launch_s * 1e6, 3)},
-            "decode_chain_tokens_per_s": None if chain_tok_s is None else round(chain_tok_s, 2),
+            "decode_engine_cut_tokens_per_s": None if chain_tok_s is None else round(chain_tok_s, 2),
+            "decode_engine_whole_token_tokens_per_s": None if uncut_tok_s is None else round(uncut_tok_s, 2),
             "per_op_launches": {"tokens_per_s": round(per_op_tok_s, 2),
                                 "gemv_achieved_GBps": round(tot_bytes / per_op_time / 1e9, 1),
                                 "per_shape_us": {k: round(v * 1e6, 3) for k, v in per.items()}},

@@ -152,8 +152,8 @@ void nad_clear_error(void);
 size_t nad_device_weight_size(const void* hostblob);
 /* bestla_device_load_storage with an explicit capacity check and a status return */
 int nad_device_load(const void* hostblob, void* devstor, void* deviceptr, size_t capacity, void* queue);
-/* 64-byte descriptor summary: [magic, bits, n, k, blocksize, ns, nt, ng, scale_t, asym, has_shuffle, bytes] */
-int nad_weight_info(const void* devstor, int64_t* out12);
+/* descriptor summary: [magic, bits, n, k, blocksize, ns, nt, ng, scale_t, asym, has_shuffle, bytes, fold_ok] */
+int nad_weight_info(const void* devstor, int64_t* out13);
 /* blob header summary (same fields as the oracle's orc_blob_info) */
 int nad_blob_info(const void* hostblob, int64_t* out27);
 /* Y = epi(X . W^T): X in fp32/fp16/bf16 (act_dtype), Y fp32.  bias: bias[m*bias_ld + n] (bias_ld 0 = broadcast);

@@ -209,10 +209,10 @@ class DeviceWeight:
         else:
             self.mem = _mem
             C.memmove(self.desc, _desc, len(self.desc))
-        o = np.zeros(12, np.int64)
+        o = np.zeros(13, np.int64)
         check(L.nad_weight_info(self.desc, _ptr(o)), "nad_weight_info")
         (_, self.bits, self.n, self.k, self.blocksize, self.ns, self.nt, self.ng, self.scale_t, self.asym,
-         self.has_shuffle, self.bytes) = (int(v) for v in o)
+         self.has_shuffle, self.bytes, self.fold_ok) = (int(v) for v in o)
 
     @classmethod
     def synthetic(cls, bits, n, k, group_size=128, scale_dtype="fp16", asym=False, seed=0, device=None, stream=None):

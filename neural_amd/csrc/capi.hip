@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <atomic>
+#include <cmath>
 #include <climits>
 #include <cstdarg>
 #include <cstdio>
@@ -145,6 +146,41 @@ extern "C" size_t nad_device_weight_size(const void* hostblob) {
                          b.has_reduce);
 }
 
+// largest |q - zp| of the device layout (int4 / int2 / int8 codes, sym or asym)
+static float fold_qmax(int bits, bool asym) {
+  if (bits == 4) return asym ? 15.f : 8.f;
+  if (bits == 2) return asym ? 3.f : 2.f;
+  return asym ? 255.f : 128.f;
+}
+// every scale s: s == 0, or s >= 2^-14 (the smallest nonzero |q| s is an fp16 normal) and qmax |s| <= 65504
+static bool scale_in_fold_range(float s, float qmax) {
+  const float a = std::fabs(s);
+  return a == 0.f || (a >= 6.103515625e-05f && a * qmax <= 65504.f);
+}
+static bool blob_fold_ok(const Blob& b, const uint8_t* base, int dev_bits) {
+  if (b.scale_t == kF8E8M0 || nfloat_kind(b.qtype) >= 0) return false;  // F4 / F8 weights never take gemm3 / gemm4
+  const float qmax = fold_qmax(dev_bits, b.asym);
+  const uint8_t* p = base + b.s_off;
+  const size_t es = b.scale_bytes(), n = b.s_size / es;
+  for (size_t i = 0; i < n; i++) {
+    float s;
+    if (es == 4) {
+      std::memcpy(&s, p + 4 * i, 4);
+    } else {
+      uint16_t h;
+      std::memcpy(&h, p + 2 * i, 2);
+      if (b.scale_t == kBF16) {
+        const uint32_t u = uint32_t(h) << 16;
+        std::memcpy(&s, &u, 4);
+      } else {
+        s = float(__builtin_bit_cast(_Float16, h));
+      }
+    }
+    if (!scale_in_fold_range(s, qmax)) return false;
+  }
+  return true;
+}
+
 extern "C" int nad_device_load(const void* hostblob, void* devstor, void* deviceptr, size_t capacity, void* queue) {
   Blob b;
   std::string err;
@@ -174,6 +210,7 @@ extern "C" int nad_device_load(const void* hostblob, void* devstor, void* device
   w.blob_bs = b.blocksize;
   // F4 codes go through the int4 repack unchanged (blob_q returns code - 8, + 8 back); F8 codes are stored raw
   w.f4kind = nfloat_kind(b.qtype);
+  w.fold_ok = blob_fold_ok(b, static_cast<const uint8_t*>(hostblob), w.bits) ? 1 : 0;
   // stage the raw blob buffers on the device, repack there
   const uint8_t* base = static_cast<const uint8_t*>(hostblob);
   uint8_t* stage = nullptr;
@@ -240,8 +277,8 @@ extern "C" int nad_weight_info(const void* devstor, int64_t* o) {
     set_err("not a neural_amd device weight descriptor");
     return -1;
   }
-  int64_t v[12] = {w->magic, w->bits, w->n, w->k, w->blocksize, w->ns, w->nt, w->ng, w->scale_t, w->asym,
-                   w->has_shuffle, int64_t(w->bytes)};
+  int64_t v[13] = {w->magic, w->bits, w->n, w->k, w->blocksize, w->ns, w->nt, w->ng, w->scale_t, w->asym,
+                   w->has_shuffle, int64_t(w->bytes), w->fold_ok};
   std::memcpy(o, v, sizeof(v));
   return 0;
 }
@@ -780,6 +817,16 @@ extern "C" int nad_q4_0_device_load(const void* blocks, int n, int k, void* devs
   layout_assign(w, deviceptr);
   w.src_core_id = kGgufQ4_0;
   w.owner = nullptr;
+  {  // block_q4_0: fp16 d, then 16 bytes of nibbles; q in [-8, 7]
+    const uint8_t* bp = static_cast<const uint8_t*>(blocks);
+    bool ok = true;
+    for (size_t i = 0; ok && i < size_t(n) * (k / 32); i++) {
+      uint16_t h;
+      std::memcpy(&h, bp + 18 * i, 2);
+      ok = scale_in_fold_range(float(__builtin_bit_cast(_Float16, h)), 8.f);
+    }
+    w.fold_ok = ok ? 1 : 0;
+  }
   // padding columns / K tiles: nibble 8 = q 0, scale 0
   HIP_OK(hipMemsetAsync(w.tiles, 0x88, size_t(w.ns) * w.nt * 1024, st));
   HIP_OK(hipMemsetAsync(w.scales, 0, size_t(w.ns) * w.ng * 16 * 2, st));
@@ -920,6 +967,7 @@ static int run_gemm(const void* act, int act_t, int lda, int m, int k, const Dev
   a.ld_aux = ld_aux;
   a.prio = env_int("NAD_GEMM3_PRIO", 0);
   a.stagger = env_int("NAD_GEMM3_STAGGER", 1);  // measured +3-7 % (profiles/r02_gemm3_stagger.txt)
+  a.fold = w.fold_ok && env_int("NAD_GEMM_FOLD", 1) ? 1 : 0;
   a.w = view(w, out, ldo, bias, bias_ld);
   const int pg = pipelined_gemm(w, m);
   if (h16) {
@@ -1160,99 +1208,221 @@ extern "C" int nad_device_ffn_forward(const void* act, int act_dtype, const void
 }
 
 // ------------------------------------------------------------------------------------------------ decode chain
-// A decode step's WOQ matmuls as one persistent launch (woq_chain.hip).  Each op is what nad_device_forward /
-// nad_device_qkv_forward / nad_device_ffn_gate_up would run at M <= 16; ops execute in order and every op may read
-// any earlier op's output.  All ops must be int4, groups of >= 128 that tile K (one group per K tile or coarser),
-// no act-order shuffle, stripe-major layout, one activation dtype.
+// A segment of a decode step's WOQ matmuls as ONE persistent launch on the weight-stream engine (woq_chain.hip).
+// Ops run in order; an op whose input (act) or residual (res) is exactly an earlier op's output receives it through
+// that op's granules inside the launch, anything else is an external vector written before the launch.  Eligible:
+// M = 1, fp32 activations, every op int4 (or every op int2) with the same groups-per-tile class and symmetry,
+// stripe-major layout, no act-order shuffle, fp arithmetic; LINEAR epilogues NONE / RES_ADD, GATE_UP SILU_MUL /
+// GELU_MUL.  The reference graph cuts such a segment at every attention node (ne_layers.c:11915-12028).
 struct NadChain {
-  GemvArgs* dev_ops = nullptr;
-  unsigned* ctl = nullptr;  // [0, grid) per-workgroup arrival flags, [1024] status
-  int n_ops = 0, waves = 0, grid = 0, hilo = 0, asym = 0;
-  size_t lds = 0;
+  EngOp* dev_ops = nullptr;
+  unsigned* ctl = nullptr;              // [0] generation, [1] status
+  unsigned long long* gran = nullptr;   // granule arrays of the results read inside the launch
+  int n_ops = 0, grid = 0, bump = 0;
+  EngGeometry g{};
 };
 
+namespace {
+struct ChainOut {
+  const float* p;
+  int n, op, wi;
+};
+}  // namespace
+
 extern "C" void* nad_chain_create(const nad_chain_op* ops, int n_ops, int m) {
-  if (!ops || n_ops <= 0 || m <= 0 || m > 8) {
-    set_err("nad_chain_create: need 1 <= m <= 8 and at least one op");
+  if (!ops || n_ops <= 0 || n_ops > 255 || m != 1) {
+    set_err("nad_chain_create: the decode engine takes m = 1 and 1..255 ops (got m = %d, %d ops)", m, n_ops);
     return nullptr;
   }
-  std::vector<GemvArgs> host(static_cast<size_t>(n_ops));
-  const int grid = std::min(device_cus(), 256);  // the flag sweep covers 64 lanes x 4 flags
-  int waves = 0, act_t = ops[0].act_dtype, asym = -1;
+  const int grid = device_cus();
+  std::vector<EngOp> host(static_cast<size_t>(n_ops));
+  std::vector<ChainOut> outs;                       // every result of the launch, in op order
+  std::vector<std::vector<int>> need_gran(static_cast<size_t>(n_ops), std::vector<int>(3, 0));
+  EngGeometry g{};
+  g.bits = 0;
+  int kp = 0;
+  size_t sd_bytes = 0;
+  bool bump = false;
+  // the LATEST earlier op writing exactly this vector (a buffer may be rewritten by later layers of one launch)
+  auto find_out = [&](const float* p, int upto, int len, const char* what, int i, int* op, int* wi) -> int {
+    int found = 0;
+    for (const ChainOut& c : outs) {
+      if (c.op >= upto) break;
+      if (c.p == p) {
+        if (c.n != len) {
+          set_err("nad_chain_create: op %d reads %s from op %d's result of length %d, expected %d", i, what, c.op, c.n,
+                  len);
+          return -1;
+        }
+        *op = c.op;
+        *wi = c.wi;
+        found = 1;
+      } else if (p < c.p + c.n && c.p < p + len) {
+        set_err("nad_chain_create: op %d's %s overlaps op %d's result without being it", i, what, c.op);
+        return -1;
+      }
+    }
+    return found;
+  };
   for (int i = 0; i < n_ops; i++) {
     const nad_chain_op& o = ops[i];
+    EngOp& e = host[size_t(i)];
     const int nw = o.kind == NAD_CHAIN_QKV ? 3 : (o.kind == NAD_CHAIN_GATE_UP ? 2 : 1);
     const DeviceWeight* ws[3] = {nullptr, nullptr, nullptr};
     for (int j = 0; j < nw; j++)
       if (!(ws[j] = as_weight(o.w[j]))) return nullptr;
     const DeviceWeight& w0 = *ws[0];
-    for (int j = 0; j < nw; j++)
-      if (int8_compute(*ws[j])) {
-        set_err("nad_chain_create: op %d runs in the int8-compute mode, which the chain does not implement", i);
+    int tpg = 0;
+    const int gpt = gemv_groups_per_tile(w0.bits, w0.nt, w0.ng, w0.blocksize, &tpg);
+    for (int j = 0; j < nw; j++) {
+      const DeviceWeight& w = *ws[j];
+      if ((w.bits != 4 && w.bits != 2) || w.f4kind >= 0 || w.has_shuffle || w.kmajor || int8_compute(w) ||
+          w.k != w0.k || w.nt != w0.nt || w.ng != w0.ng || w.blocksize != w0.blocksize || w.bits != w0.bits ||
+          w.scale_t != w0.scale_t || w.asym != w0.asym) {
+        set_err("nad_chain_create: op %d weight %d is not an engine weight (int4 / int2, stripe-major, no act-order, "
+                "fp arithmetic, one geometry per op)", i, j);
         return nullptr;
       }
-    if (w0.bits != 4 || w0.f4kind >= 0 || w0.has_shuffle || w0.kmajor || w0.blocksize % 128 != 0 || o.act_dtype != act_t ||
-        (asym >= 0 && asym != w0.asym)) {
-      set_err("nad_chain_create: op %d is not a chain op (int4, group >= 128, no shuffle, one act dtype/symmetry)", i);
+    }
+    if (gpt == 0 || (w0.bits == 4 && gpt > 2)) {
+      set_err("nad_chain_create: op %d's group size %d does not tile the K tiles", i, w0.blocksize);
       return nullptr;
     }
-    asym = w0.asym;
+    if (g.bits == 0) {
+      g.bits = w0.bits;
+      g.gpt = gpt;
+      g.asym = w0.asym;
+    } else if (g.bits != w0.bits || g.gpt != gpt || g.asym != w0.asym) {
+      set_err("nad_chain_create: op %d's format (bits %d, %d groups per tile, asym %d) differs from op 0's", i,
+              w0.bits, gpt, w0.asym);
+      return nullptr;
+    }
+    if (o.act_dtype != kActF32 || !o.act) {
+      set_err("nad_chain_create: op %d: the engine takes fp32 activations", i);
+      return nullptr;
+    }
     int epi = o.epi;
-    if (o.kind == NAD_CHAIN_GATE_UP && epi != kEpiSiluMul && epi != kEpiGeluMul) epi = kEpiSiluMul;
-    float* outs[3] = {o.out[0], o.out[1], o.out[2]};
-    int ldos[3] = {o.ldo[0], o.ldo[1], o.ldo[2]};
     if (o.kind == NAD_CHAIN_GATE_UP) {
-      outs[1] = outs[0];
-      ldos[1] = ldos[0];
-    }
-    int wv = 0, gr = 0, gpt = 0;
-    GemvArgs& a = host[size_t(i)];
-    if (!prepare_gemv(a, wv, gr, gpt, o.act, o.act_dtype, o.lda, m, w0.k, nw, ws, outs, ldos, epi, o.bias,
-                      o.bias_ld, o.res, o.ld_res, o.aux, o.ld_aux, false) ||
-        gpt != 1) {
-      set_err("nad_chain_create: op %d not eligible for the stripe stream", i);
+      if (epi != kEpiSiluMul && epi != kEpiGeluMul) epi = kEpiSiluMul;
+    } else if (epi != kEpiNone && epi != kEpiResAdd) {
+      set_err("nad_chain_create: op %d: epilogue %d is not an engine epilogue (NONE / RES_ADD)", i, epi);
       return nullptr;
     }
-    a.nwa = wv;
-    a.norm = o.norm;
-    a.norm_eps = o.norm_eps;
-    a.norm_w = o.norm_w;
-    waves = std::max(waves, wv);
-  }
-  waves = std::max(waves, m);
-  if (waves > 12) {  // woq_chain_kernel is built for <= 768 threads (168 VGPRs, no spills)
-    set_err("nad_chain_create: %d waves per workgroup exceed the chain kernel's 12", waves);
-    return nullptr;
-  }
-  size_t lds = 80 * 1024 + 16;  // > half the LDS: exactly one workgroup per CU, all co-resident
-  for (int i = 0; i < n_ops; i++) {
-    GemvArgs& a = host[size_t(i)];
-    const int ku = a.nt * 128 / 8;
-    if (m * ku > 3 * waves * 64) {
-      set_err("nad_chain_create: op %d activations exceed the staging registers (m * K too large)", i);
+    const int KT = w0.bits == 4 ? 128 : 256;
+    e.nw = nw;
+    e.dual = o.kind == NAD_CHAIN_GATE_UP ? 1 : 0;
+    e.K = w0.k;
+    e.nt = w0.nt;
+    e.ng = w0.ng;
+    e.tpg_shift = (gpt == 1 && tpg > 0) ? __builtin_ctz(unsigned(tpg)) : 31;
+    e.scale_t = w0.scale_t;
+    e.norm = o.norm;
+    e.norm_eps = o.norm_eps;
+    e.norm_w = o.norm_w;
+    e.epi = epi;
+    e.aux = o.kind == NAD_CHAIN_GATE_UP ? o.aux : nullptr;
+    e.tag = unsigned(i + 1);
+    int stripes = 0;
+    for (int j = 0; j < 4; j++) e.stripe_base[j] = INT_MAX;
+    for (int j = 0; j < nw; j++) {
+      EngWeight& W = e.w[j];
+      W.tiles = ws[j]->tiles;
+      W.scales = ws[j]->scales;
+      W.zps = ws[j]->zps;
+      W.ns = ws[j]->ns;
+      W.n = ws[j]->n;
+      W.out = (o.kind == NAD_CHAIN_GATE_UP && j == 1) ? nullptr : o.out[j];
+      e.stripe_base[j] = stripes;
+      stripes += ws[j]->ns;
+    }
+    if (e.dual && (ws[1]->n != w0.n)) {
+      set_err("nad_chain_create: op %d: gate and up differ in N", i);
       return nullptr;
     }
-    lds = std::max(lds, chain_lds_layout(a, waves, grid));
+    e.units = e.dual ? w0.ns : stripes;
+    e.u_q = e.units / grid;
+    e.u_r = e.units % grid;
+    if ((e.u_q + (e.u_r ? 1 : 0)) * (e.dual ? 2 : 1) > kEngMaxStripes) {
+      set_err("nad_chain_create: op %d has more than %d stripes per CU", i, kEngMaxStripes);
+      return nullptr;
+    }
+    // input / residual: an earlier result of this launch, or external
+    int pop, pwi;
+    int r = find_out(static_cast<const float*>(o.act), i, e.K, "its input", i, &pop, &pwi);
+    if (r < 0) return nullptr;
+    if (r) {
+      e.act_tag = unsigned(pop + 1);
+      need_gran[size_t(pop)][size_t(pwi)] = 1;
+      bump = true;
+    }
+    e.act = static_cast<const float*>(o.act);
+    if (epi == kEpiResAdd) {
+      if (!o.res || nw != 1) {
+        set_err("nad_chain_create: op %d: RES_ADD needs a residual and one weight", i);
+        return nullptr;
+      }
+      r = find_out(o.res, i, w0.n, "its residual", i, &pop, &pwi);
+      if (r < 0) return nullptr;
+      if (r) {
+        e.res_tag = unsigned(pop + 1);
+        need_gran[size_t(pop)][size_t(pwi)] = 1;
+        bump = true;
+      }
+      e.res = o.res;
+    }
+    for (int j = 0; j < nw; j++)
+      if (e.w[j].out) outs.push_back(ChainOut{e.w[j].out, e.w[j].n, i, j});
+    kp = std::max(kp, w0.nt * KT);
+    // scale (+ zero point) bytes of one fill of 16 tiles
+    const int ssz = w0.scale_t == kScaleF32 ? 4 : 2;
+    const size_t groups = gpt == 1 ? size_t((16 + std::max(tpg, 1) - 1) / std::max(tpg, 1) + 1) : size_t(16) * gpt;
+    sd_bytes = std::max(sd_bytes, std::min(groups, size_t(w0.ng)) * 16 * ssz);
   }
-  if (lds > 160 * 1024) {
-    set_err("nad_chain_create: LDS need %zu exceeds 160 KiB", lds);
+  g.sd = int((sd_bytes + 1023) / 1024);
+  if (g.sd < 1) g.sd = 1;
+  if (g.sd > 2 || !engine_geometry(g, kp)) {
+    set_err("nad_chain_create: the engine's LDS ring does not fit (K up to %d, %zu scale bytes per fill)", kp,
+            sd_bytes);
     return nullptr;
   }
+  // granule arrays for the results read inside the launch
+  size_t ngran = 0;
+  for (int i = 0; i < n_ops; i++)
+    for (int j = 0; j < host[size_t(i)].nw; j++)
+      if (need_gran[size_t(i)][size_t(j)]) ngran += size_t(host[size_t(i)].w[j].n);
   NadChain* c = new NadChain();
   c->n_ops = n_ops;
-  c->waves = waves;
   c->grid = grid;
-  c->lds = lds;
-  c->hilo = act_t == kActF16 ? 0 : 1;
-  c->asym = asym;
-  if (hipMalloc(&c->dev_ops, sizeof(GemvArgs) * size_t(n_ops)) != hipSuccess ||
-      hipMalloc(&c->ctl, 8192) != hipSuccess ||
-      hipMemcpy(c->dev_ops, host.data(), sizeof(GemvArgs) * size_t(n_ops), hipMemcpyHostToDevice) != hipSuccess ||
-      hipMemset(c->ctl, 0, 8192) != hipSuccess) {
+  c->bump = bump ? 1 : 0;
+  c->g = g;
+  if (hipMalloc(&c->dev_ops, sizeof(EngOp) * size_t(n_ops)) != hipSuccess || hipMalloc(&c->ctl, 256) != hipSuccess ||
+      hipMemset(c->ctl, 0, 256) != hipSuccess ||
+      (ngran && (hipMalloc(&c->gran, ngran * 8) != hipSuccess || hipMemset(c->gran, 0, ngran * 8) != hipSuccess))) {
     set_err("nad_chain_create: device allocation failed");
-    if (c->dev_ops) (void)hipFree(c->dev_ops);
-    if (c->ctl) (void)hipFree(c->ctl);
-    delete c;
+    nad_chain_destroy(c);
+    return nullptr;
+  }
+  size_t off = 0;
+  std::vector<std::vector<unsigned long long*>> gp(static_cast<size_t>(n_ops), std::vector<unsigned long long*>(3));
+  for (int i = 0; i < n_ops; i++)
+    for (int j = 0; j < host[size_t(i)].nw; j++)
+      if (need_gran[size_t(i)][size_t(j)]) {
+        host[size_t(i)].w[j].gran = c->gran + off;
+        gp[size_t(i)][size_t(j)] = c->gran + off;
+        off += size_t(host[size_t(i)].w[j].n);
+      }
+  // resolve the readers' granule pointers
+  for (int i = 0; i < n_ops; i++) {
+    EngOp& e = host[size_t(i)];
+    for (const ChainOut& o : outs) {
+      if (o.op >= i) break;
+      if (e.act_tag && unsigned(o.op + 1) == e.act_tag && o.p == e.act) e.act_gran = gp[size_t(o.op)][size_t(o.wi)];
+      if (e.res_tag && unsigned(o.op + 1) == e.res_tag && o.p == e.res) e.res_gran = gp[size_t(o.op)][size_t(o.wi)];
+    }
+  }
+  if (hipMemcpy(c->dev_ops, host.data(), sizeof(EngOp) * size_t(n_ops), hipMemcpyHostToDevice) != hipSuccess) {
+    set_err("nad_chain_create: op table upload failed");
+    nad_chain_destroy(c);
     return nullptr;
   }
   return c;
@@ -1261,12 +1431,7 @@ extern "C" void* nad_chain_create(const nad_chain_op* ops, int n_ops, int m) {
 extern "C" int nad_chain_run(void* chain, void* queue) {
   NadChain* c = static_cast<NadChain*>(chain);
   if (!c) return -1;
-  hipStream_t st = static_cast<hipStream_t>(queue);
-  if (hipMemsetAsync(c->ctl, 0, sizeof(unsigned) * size_t(c->grid), st) != hipSuccess) {
-    set_err("nad_chain_run: flag reset failed");
-    return -1;
-  }
-  hipError_t e = launch_chain(c->dev_ops, c->n_ops, c->hilo, c->asym, c->waves, c->grid, c->lds, c->ctl, c->ctl + 1024, env_int("NAD_CHAIN_PRE", 1), st);
+  hipError_t e = launch_engine(c->dev_ops, c->n_ops, c->g, c->ctl, c->grid, c->bump, static_cast<hipStream_t>(queue));
   if (e != hipSuccess) {
     set_err("nad_chain_run: launch failed: %s", hipGetErrorString(e));
     return -1;
@@ -1278,15 +1443,16 @@ extern "C" int nad_chain_status(void* chain) {
   NadChain* c = static_cast<NadChain*>(chain);
   if (!c) return -1;
   unsigned s = 0;
-  if (hipMemcpy(&s, c->ctl + 1024, sizeof(unsigned), hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  if (hipMemcpy(&s, c->ctl + 1, sizeof(unsigned), hipMemcpyDeviceToHost) != hipSuccess) return -1;
   return int(s);
 }
 
 extern "C" void nad_chain_destroy(void* chain) {
   NadChain* c = static_cast<NadChain*>(chain);
   if (!c) return;
-  (void)hipFree(c->dev_ops);
-  (void)hipFree(c->ctl);
+  if (c->dev_ops) (void)hipFree(c->dev_ops);
+  if (c->ctl) (void)hipFree(c->ctl);
+  if (c->gran) (void)hipFree(c->gran);
   delete c;
 }
 
@@ -1339,6 +1505,7 @@ extern "C" int nad_synthetic_weight(void* devstor, void* deviceptr, size_t capac
   }
   layout_assign(w, deviceptr);
   w.src_core_id = 0;
+  w.fold_ok = 1;  // scales U[0.001, 0.01] (nad_fill_scales_kernel): every q * s is an fp16 normal
   hipStream_t st = static_cast<hipStream_t>(queue);
   uint64_t nd = uint64_t(w.ns) * w.nt * 256;
   hipLaunchKernelGGL(nad_fill_u32_kernel, dim3(4096), dim3(256), 0, st, static_cast<uint32_t*>(w.tiles), nd, seed);

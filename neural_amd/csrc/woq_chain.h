@@ -1,13 +1,68 @@
-// woq_chain.h -- the persistent decode chain (woq_chain.hip): a list of decode GEMV ops run in one launch.
+// woq_chain.h -- the decode weight-stream engine (woq_chain.hip): a list of M = 1 WOQ matmuls in ONE persistent
+// launch, one workgroup per CU, each CU's weights streamed by one LDS-DMA loader wave into an LDS ring while eight
+// consumer waves compute, hand-offs between ops as data-tagged 8-byte granules.
 #pragma once
 #include <hip/hip_runtime.h>
+
+#include <cstdint>
 
 #include "woq_kernels.h"
 
 namespace nad {
-// LDS bytes one op needs inside the chain (sets a.part_off)
-size_t chain_lds_layout(GemvArgs& a, int waves, int grid);
-// dev_ops: n_ops GemvArgs in device memory; flags[grid] must be 0 at launch; status[0] set on a barrier timeout
-hipError_t launch_chain(const GemvArgs* dev_ops, int n_ops, int hilo, int asym, int waves, int grid, size_t lds,
-                        unsigned* flags, unsigned* status, int npre, hipStream_t st);
+
+struct EngWeight {
+  const void* tiles;            // stripe-major tile layout (woq_layout.h)
+  const void* scales;
+  const int8_t* zps;            // asym only
+  int ns, n;
+  float* out;                   // [n] fp32 result (plain stores; read by kernels after this launch)
+  unsigned long long* gran;     // [n] {value, tag} granules for ops of this launch that read the result (or null)
+};
+
+struct EngOp {
+  EngWeight w[3];
+  int nw;                       // weights (QKV: 3); dual: w[0] = gate, w[1] = up
+  int dual;                     // units are {w[0] stripe u, w[1] stripe u}: out = act(x.w0) * (x.w1) into w[0]
+  int units, u_q, u_r;          // units (virtual stripes, or stripe pairs); per workgroup u_q, +1 for the first u_r
+  int stripe_base[4];           // non-dual: first virtual stripe of each weight (unused = INT_MAX)
+  int K, nt, ng, tpg_shift;     // shared geometry: K, K tiles, groups, log2(tiles per group) (31: one group)
+  int scale_t;
+  // input: an external fp32 vector [K] (written before this launch), or the granules of an earlier op
+  const float* act;
+  const unsigned long long* act_gran;
+  unsigned act_tag;
+  int norm;                     // RMS-normalise the input: x / sqrt(mean(x^2) + eps) * (norm_w ? norm_w : 1)
+  float norm_eps;
+  const float* norm_w;
+  int epi;                      // kEpiNone, kEpiResAdd, dual: kEpiSiluMul / kEpiGeluMul
+  const float* res;             // residual: external [n] ...
+  const unsigned long long* res_gran;  // ... or an earlier op's granules
+  unsigned res_tag;
+  float* aux;                   // dual: act(x.w0) (optional)
+  unsigned tag;                 // this op's index in the launch + 1
+};
+
+// Engine geometry: 8 consumer waves + 1 loader wave, fills of 16 tiles, 3 fills in flight
+constexpr int kEngConsumers = 8;
+constexpr int kEngThreads = (kEngConsumers + 1) * 64;
+constexpr int kEngFillTiles = 16;
+constexpr int kEngInflight = 3;
+constexpr int kEngMaxStripes = 16;   // virtual stripes of one op per workgroup (partial-sum slots)
+constexpr int kEngMaxK = 16384;      // input length (gather registers)
+
+struct EngGeometry {
+  int bits, gpt, asym, sd;      // kernel instantiation: bits 4 / 2, groups per tile 1 / 2 / 4, scale DMAs per fill
+  int slots;                    // ring slots
+  int kp;                       // activation row length (max over ops of nt * KT)
+  size_t lds;                   // dynamic LDS bytes
+  size_t slot_bytes;
+};
+
+// fills g.kp/slots/lds from g.bits/gpt/asym/sd and the ops' largest padded K; false if the ring does not fit
+bool engine_geometry(EngGeometry& g, int kp);
+// ops: device array; ctl: [0] launch generation (tags), [1] status (0 ok, else the first give-up code); bump: some op
+// reads a result of this launch (the generation then moves on after the launch)
+hipError_t launch_engine(const EngOp* ops, int n_ops, const EngGeometry& g, unsigned* ctl, int grid, int bump,
+                         hipStream_t st);
+
 }  // namespace nad

@@ -1,28 +1,42 @@
-// woq_chain.hip -- a whole decode step's WOQ matmuls in ONE persistent launch (the decode chain).
+// woq_chain.hip -- the decode weight-stream engine: a list of M = 1 WOQ matmuls in ONE persistent launch.
 //
-// What it replaces: the sequence of device WOQ nodes one decode token runs through the ne graph
+// What it replaces: the device WOQ nodes one decode step runs between two attention nodes
 // (ne_compute_forward_mul_mat_q_f32_bestla -> bestla_device_f32f32_forward, neural_speed/core/ne_layers.c:7219-7316;
-// fused QKV / FFN nodes, ne_layers.c:8050-8170), i.e. what BTLAGemmBatchDriver (core/layers/bestla_gemm.cpp:508-624)
-// does for a batch of independent GEMMs, extended with the data dependencies between consecutive matmuls.
+// the fused QKV / FFN nodes, ne_layers.c:8050-8170; op order llama.cpp:212-237,590-619,690-718), i.e. what
+// BTLAGemmBatchDriver (core/layers/bestla_gemm.cpp:508-624) does for independent GEMMs, extended with the data
+// dependencies between consecutive matmuls (the O -> gate/up -> down -> next QKV segment of a decoder layer).
 //
-// Why: measured on MI355X (profiles/r01_decode_calibration.md) every separate decode launch pays ~5 us during which
-// HBM is mostly idle -- the kernel boundary (~1.8 us), the prologue (cold instruction cache, activation staging,
-// first weight loads ~2.5-3 us) and the epilogue (~0.7 us).  Over 129 launches per Llama-2-7B token that is about
-// half of the token time.  Here one workgroup per CU stays resident for the whole step and, for every op:
-//   1. issues the first three weight stages of the op (they do not depend on the activations) -- these loads stream
-//      from HBM while the workgroup waits for the previous op;
-//   2. wave 0 polls the per-workgroup arrival flags (one 16-B sc1 load per lane) until every workgroup has
-//      published the previous op;
-//   3. stages the op's activations (optionally RMS-normalised) into LDS as MFMA-ready fp16 hi/lo rows;
-//   4. runs the stripe stream of woq_gemv.hip (same tiles, same dequant, same MFMA and reduction order, so every
-//      op's output is bit-identical to the single-op launch);
-//   5. publishes its outputs with write-through (sc1) stores, waits for them, and sets its own flag to op + 1.
-// Hand-off protocol (MI355X_MICROARCH.md, "Hand-offs measured with sc1 loads", row 1): every load of chain-produced
-// data (activations, residuals) is an sc1 load, every store of it an sc1 store, each storing wave waits vmcnt(0)
-// before the workgroup barrier that precedes the one-lane sc1 flag store; the polling wave's loads follow its
-// matching poll, the other waves' follow the barrier it then joins.  All workgroups must be co-resident: the grid is
-// one workgroup per CU and the LDS request (> 80 KiB) admits no second one.  Every spin is bounded; a timeout sets
-// status[0] and the launch still terminates.
+// Why: a separate decode launch is bounded by its own fixed chain (kernel boundary ~1.2 us, first weight load issued
+// ~0.5 us in, ~1.5 us of HBM latency before the stream runs, ~0.6 us reduce + epilogue), so one
+// launch at a time cannot pass ~0.33-0.57 of the 8 TB/s roofline whatever its body does.  The weights of a decode step
+// do not depend on the activations: here each CU's weight stream runs ahead of every data dependency.
+//
+// Shape (MI355X_MICROARCH.md rows ldsdma-fill, prefetch-credit, handoff-1to1, allgather; the engine-vs-launches row
+// measured the same structure at 0.87-0.89x of separate launches for a bf16 layer):
+//   * one workgroup per CU (the LDS request admits no second one), all co-resident; 9 waves: 8 consumers + 1 loader;
+//   * every op's units (16-column stripes; {gate, up} stripe pairs for the dual SiLU*mul op) are split into balanced
+//     runs per workgroup, exactly as the single-op stripe stream splits them;
+//   * the LOADER wave walks the workgroup's fills for ALL ops of the launch in order -- a fill is 16 consecutive
+//     1 KiB K tiles of one stripe + their group scales (+ zero points) -- and moves each by LDS-DMA
+//     (buffer_load_dwordx4 ... lds, non-temporal: read once per token) into a ring of LDS slots: at most 3 fills in
+//     flight (counted s_waitcnt vmcnt), a FULL word per slot published when its fill has landed, a slot re-filled only
+//     when all 8 consumers have released it (FREE counter).  It never waits for activations, so it keeps streaming the
+//     next op's weights while the consumers wait for that op's input;
+//   * the 8 CONSUMER waves: per op, stage the input vector into LDS as MFMA-ready fp16 hi/lo rows (hi = fp16(x),
+//     lo = fp16(x - hi): fp32-accurate products), optionally RMS-normalised; then for each fill consumer c takes tiles
+//     c and c + 8: ds_read of the 1 KiB tile (the same 16 B per lane a global load would bring), 0x6400 magic
+//     dequantisation, v_mfma_f32_16x16x32_f16 with hi in MFMA rows 0-7 and lo in rows 8-15, the group scale applied to
+//     an fp32 group accumulator; partial sums per (stripe, consumer) in LDS, summed in a fixed order, fused epilogue
+//     (residual add, SiLU / GELU * up);
+//   * hand-offs between ops (MI355X_MICROARCH.md "Hand-offs measured with sc1 loads", granule form R2; Guideline 16):
+//     each result element is published as ONE 8-byte {fp32 value, tag} granule by an agent-scope relaxed 64-bit store
+//     (write-through sc1), tag = launch generation * 256 + op index + 1; a consumer reads the whole input vector with
+//     sc1 buffer loads and re-reads every granule whose tag is not yet the expected one -- the data is the flag, no
+//     fence, no counter.  The generation is a per-chain device word bumped by workgroup 0 at its end, so stale
+//     granules of the previous run never match (graph replay safe, nothing to reset per call);
+//   * every spin is bounded (~1 s); a give-up records a code in ctl[1] and the launch still terminates.
+// Arithmetic per op is the same for every position of the op in a launch: a one-op launch of it gives bit-identical
+// outputs (tests/test_chain_gpu.py).
 #include <hip/hip_runtime.h>
 
 #include <climits>
@@ -33,129 +47,172 @@
 #include "woq_kernels.h"
 
 namespace nad {
-namespace chain {
+namespace eng {
 
-// Development instrumentation (make chaintrace): per-(op, workgroup) wall-clock stamps of the chain's phases.
-#ifdef NAD_CHAIN_TRACE
-constexpr int kTrOps = 160, kTrWg = 256, kTrSlots = 6;
-__device__ unsigned long long nad_chain_trace[kTrSlots][kTrOps][kTrWg];
-#define CTRACE(slot)                                                                                      \
-  do {                                                                                                    \
-    if (threadIdx.x == 0 && op < kTrOps && blockIdx.x < kTrWg) nad_chain_trace[slot][op][blockIdx.x] = wall_clock64(); \
-  } while (0)
-#else
-#define CTRACE(slot) \
-  do {               \
-  } while (0)
-#endif
+constexpr int NC = kEngConsumers;
+constexpr int FT = kEngFillTiles;
+constexpr int D = kEngInflight;
+constexpr int PJ = 8;                       // granule pairs per consumer lane per gather pass
+constexpr int kOOB = 0x7FFF0000;            // buffer offset past every resource: no memory access, returns 0
+constexpr int kSC1 = 16;                    // buffer-load aux: sc1 (bypass this CU's L1)
+constexpr int kNT = 2;                      // buffer-load aux: non-temporal (weights, read once per token)
+constexpr unsigned kSpinMax = 1u << 24;     // ~1 s of s_sleep(1) polls
+// LDS control words (u32 index): FULL[8], FREE[8], consumer barrier, RMS partial sums[8]
+constexpr int kFull = 0, kFree = 8, kBar = 16, kNsum = 20, kCtlBytes = 128;
+constexpr int kPartBytes = kEngMaxStripes * NC * 16 * 4;
 
-constexpr int kOOB = 0x7FFF0000;  // buffer offset past every resource: the load returns 0 and touches no memory
-constexpr int kSC1 = 16;          // cache-policy aux bit of buffer loads: sc1 (bypass the CU's L1)
-constexpr int KS = 4;             // tiles per K-slice (woq_gemv.hip)
+typedef __attribute__((address_space(3))) void lds_void_t;
 
-__device__ __forceinline__ void vstripe(const GemvArgs& a, int v, int& w, int& s) {
-  if (a.dual) {
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, bytes, 0x00020000);
+}
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return uint32_t(reinterpret_cast<uintptr_t>((const __attribute__((address_space(3))) char*)p));
+}
+// LDS words shared between the loader and the consumers, in inline asm: hipcc puts vmcnt(0) in front of every LDS
+// access it can see while an LDS-DMA is in flight, which would drain the loader's pipeline at every poll
+__device__ __forceinline__ unsigned lds_ld(uint32_t a) {
+  unsigned r;
+  asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(r) : "v"(a) : "memory");
+  return __builtin_amdgcn_readfirstlane(r);
+}
+__device__ __forceinline__ void lds_st(uint32_t a, unsigned v) {
+  asm volatile("ds_write_b32 %0, %1" ::"v"(a), "v"(v) : "memory");
+}
+__device__ __forceinline__ void lds_add(uint32_t a, unsigned v) {
+  asm volatile("ds_add_u32 %0, %1" ::"v"(a), "v"(v) : "memory");
+}
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+__device__ __forceinline__ void give_up(unsigned* ctl, unsigned code) {
+  __hip_atomic_store(ctl + 1, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// virtual stripe -> (weight, stripe within it)
+__device__ __forceinline__ void vstripe(const EngOp& o, int v, int& w, int& s) {
+  if (o.dual) {
     w = v & 1;
     s = v >> 1;
   } else {
-    w = (v >= a.stripe_base[1] ? 1 : 0) + (v >= a.stripe_base[2] ? 1 : 0);
-    s = v - (w == 0 ? 0 : (w == 1 ? a.stripe_base[1] : a.stripe_base[2]));
+    w = (v >= o.stripe_base[1] ? 1 : 0) + (v >= o.stripe_base[2] ? 1 : 0);
+    s = v - o.stripe_base[w];
+  }
+}
+__device__ __forceinline__ void unit_range(const EngOp& o, int bid, int& v0, int& nv) {
+  const int u0 = bid * o.u_q + min(bid, o.u_r);
+  const int nu = o.u_q + (bid < o.u_r ? 1 : 0);
+  const int vpu = o.dual ? 2 : 1;
+  v0 = u0 * vpu;
+  nv = nu * vpu;
+}
+// groups of one fill (chunk c of a stripe): first group and count
+template <int GPT>
+__device__ __forceinline__ void fill_groups(const EngOp& o, int t0, int& g0, int& ngc) {
+  const int t1 = min(t0 + FT, o.nt);
+  if constexpr (GPT == 1) {
+    g0 = t0 >> o.tpg_shift;
+    ngc = ((t1 - 1) >> o.tpg_shift) - g0 + 1;
+  } else {
+    g0 = t0 * GPT;
+    ngc = (t1 - t0) * GPT;
   }
 }
 
-template <class T>
-__device__ __forceinline__ T sel3(int w, T x0, T x1, T x2) {
-  return w == 0 ? x0 : (w == 1 ? x1 : x2);
-}
-
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, int bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, bytes, 0x00020000);
-}
-
-__device__ __forceinline__ float ld_sc1(const float* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_sc1(float* p, float v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-struct StageCursor {
-  int j, q, s;
-  __amdgpu_buffer_rsrc_t rt, rs, rz;
-};
-
-__device__ __forceinline__ void cursor_stripe(const GemvArgs& a, StageCursor& c, int v0) {
-  int w, s;
-  vstripe(a, v0 + c.j, w, s);
-  const int ns = sel3(w, a.w[0].ns, a.w[1].ns, a.w[2].ns);
-  const int ssz = a.scale_t == kScaleF32 ? 4 : 2;
-  c.s = s;
-  c.rt = rsrc(sel3(w, a.w[0].tiles, a.w[1].tiles, a.w[2].tiles), ns * a.nt * 1024);
-  c.rs = rsrc(sel3(w, a.w[0].scales, a.w[1].scales, a.w[2].scales), ns * a.ng * 16 * ssz);
-  c.rz = rsrc(sel3(w, a.w[0].zps, a.w[1].zps, a.w[2].zps), ns * a.ng * 16);
-}
-
-template <bool ASYM>
-struct StageRegs {
-  u4_t b[KS];
-  uint32_t sc[KS];
-  int zp[KS];
-};
-
-// one stage = KS tiles of one (stripe, K-slice) + their group scales (never predicated: out-of-range offsets)
-template <bool ASYM>
-__device__ __forceinline__ void load_stage(const GemvArgs& a, StageRegs<ASYM>& S, StageCursor& c, int nv, int nsl,
-                                           int wave, int NW, int v0, int lane, int vs) {
-  if (c.j >= nv) {
+// ------------------------------------------------------------------------------------------------ loader
+template <int GPT, bool ASYM, int SD>
+__device__ void loader(const EngOp* ops, int n_ops, char* ring, int S, int slot_bytes, uint32_t ctl_a, unsigned* ctl,
+                       int lane) {
+  constexpr int IPF = FT + SD + (ASYM ? 1 : 0);  // DMA instructions per fill: constant, so vmcnt counts are exact
+  const uint32_t full_a = ctl_a + kFull * 4, free_a = ctl_a + kFree * 4;
+  int f = 0, fpub = 0, slot = 0, pslot = 0;
+  unsigned round = 0;
+  bool failed = false;
+  auto publish_one = [&]() {
+    lds_st(full_a + pslot * 4, unsigned(fpub + 1));
+    fpub++;
+    pslot = pslot + 1 == S ? 0 : pslot + 1;
+  };
+  for (int op = 0; op < n_ops; op++) {
+    const EngOp& o = ops[op];
+    const int nt = o.nt, ng = o.ng, nch = (nt + FT - 1) / FT;
+    const int ssz = o.scale_t == kScaleF32 ? 4 : 2;
+    int v0, nv;
+    unit_range(o, blockIdx.x, v0, nv);
+    for (int jl = 0; jl < nv; jl++) {
+      int wsel, s;
+      vstripe(o, v0 + jl, wsel, s);
+      const EngWeight& W = o.w[wsel];
+      const auto rt = rsrc(W.tiles, unsigned(W.ns) * nt * 1024u);
+      const auto rs = rsrc(W.scales, unsigned(W.ns) * ng * 16u * ssz);
+      const auto rz = rsrc(ASYM ? static_cast<const void*>(W.zps) : W.tiles, ASYM ? unsigned(W.ns) * ng * 16u : 0u);
+      const int tbase = s * nt * 1024 + lane * 16;
+      for (int c = 0; c < nch; c++) {
+        if (f - fpub == D) {  // keep at most D fills in flight: the oldest has landed -> publish it
+          wait_vm<(D - 1) * IPF>();
+          publish_one();
+        }
+        if (round > 0) {  // this slot's previous fill must have been released by every consumer
+          const unsigned need = NC * round;
+          if (lds_ld(free_a + slot * 4) < need) {
+            wait_vm<0>();  // about to wait anyway: publish everything in flight first
+            while (fpub < f) publish_one();
+            unsigned spins = 0;
+            while (!failed && lds_ld(free_a + slot * 4) < need) {
+              __builtin_amdgcn_s_sleep(1);
+              if (++spins > kSpinMax) {
+                give_up(ctl, 2);
+                failed = true;
+              }
+            }
+          }
+        }
+        char* sb = ring + slot * slot_bytes;
+        const int t0 = c * FT;
 #pragma unroll
-    for (int i = 0; i < KS; i++) {
-      S.b[i] = __builtin_bit_cast(u4_t, __builtin_amdgcn_raw_buffer_load_b128(c.rt, kOOB, 0, 2));
-      S.sc[i] = __builtin_amdgcn_raw_buffer_load_b32(c.rs, kOOB, 0, 0);
-      S.zp[i] = ASYM ? int(int8_t(__builtin_amdgcn_raw_buffer_load_b8(c.rz, kOOB, 0, 0))) : 0;
+        for (int i = 0; i < FT; i++)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rt, (lds_void_t*)(sb + i * 1024), 16,
+                                                   t0 + i < nt ? tbase + (t0 + i) * 1024 : kOOB, 0, 0, kNT);
+        int g0, ngc;
+        fill_groups<GPT>(o, t0, g0, ngc);
+        const int sbytes = ngc * 16 * ssz, soff = (s * ng + g0) * 16 * ssz;
+#pragma unroll
+        for (int j = 0; j < SD; j++) {
+          const int b = j * 1024 + lane * 16;
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)(sb + FT * 1024 + j * 1024), 16,
+                                                   b < sbytes ? soff + b : kOOB, 0, 0, 0);
+        }
+        if constexpr (ASYM) {
+          const int b = lane * 16;
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rz, (lds_void_t*)(sb + FT * 1024 + SD * 1024), 16,
+                                                   b < ngc * 16 ? (s * ng + g0) * 16 + b : kOOB, 0, 0, 0);
+        }
+        f++;
+        if (++slot == S) {
+          slot = 0;
+          round++;
+        }
+      }
     }
-    return;
   }
-  const int nt = a.nt;
-  const int t0 = c.q * KS;
-  const int tb = (c.s * nt + t0) * 1024;
-  const int rowb = a.scale_t == kScaleF32 ? 64 : 32;
-#pragma unroll
-  for (int i = 0; i < KS; i++) {
-    const bool live = t0 + i < nt;
-    S.b[i] = __builtin_bit_cast(u4_t, __builtin_amdgcn_raw_buffer_load_b128(c.rt, (live ? tb + i * 1024 : kOOB) + lane * 16, 0, 2));
-    const int row = c.s * a.ng + ((t0 + i) >> a.tpg_shift);
-    S.sc[i] = __builtin_amdgcn_raw_buffer_load_b32(c.rs, (live ? row * rowb : kOOB) + vs, 0, 0);
-    if constexpr (ASYM)
-      S.zp[i] = int(int8_t(__builtin_amdgcn_raw_buffer_load_b8(c.rz, (live ? row * 16 : kOOB) + (lane & 15), 0, 0)));
-    else
-      S.zp[i] = 0;
-  }
-  c.q += NW;
-  if (c.q >= nsl) {
-    c.q = wave;
-    c.j++;
-    if (c.j < nv)
-      cursor_stripe(a, c, v0);
-    else
-      c.rt = c.rs = c.rz = rsrc(a.w[0].tiles, 0);
-  }
+  wait_vm<0>();
+  while (fpub < f) publish_one();
 }
 
-// (x & m) | c in one VOP3
+// ------------------------------------------------------------------------------------------------ consumers
 __device__ __forceinline__ uint32_t and_or(uint32_t x, uint32_t m, uint32_t c) {
   uint32_t r;
   asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "s"(m), "v"(c));
   return r;
 }
-
 __device__ __forceinline__ h2_t splat(float v) {
   h2_t r;
   r[0] = _Float16(v);
   r[1] = _Float16(v);
   return r;
 }
-
-// int4: 0x6400 | nibble<<0 = 1024 + q, 0x6400 | nibble<<4 = 1024 + 16 q (exact fp16), one shift per dword
+// int4: 0x6400 | nibble = 1024 + q and 0x6400 | nibble << 4 = 1024 + 16 q (exact fp16): one shift per dword
 __device__ __forceinline__ h8_t dequant4(uint32_t w, uint32_t m0, uint32_t m1, uint32_t mag, h2_t s16, h2_t c0,
                                          h2_t c1) {
   const uint32_t w8 = w >> 8;
@@ -174,373 +231,346 @@ __device__ __forceinline__ h8_t dequant4(uint32_t w, uint32_t m0, uint32_t m1, u
   r[7] = p3[1];
   return r;
 }
-
-__device__ __forceinline__ float scale_bits_to_f32(uint32_t x, int st, int sh) {
-  const uint32_t h = (x >> sh) & 0xFFFFu;
-  const float fb = __uint_as_float(h << 16);
-  const float fh = f16_bits_to_f32(uint16_t(h));
-  const float f16or = st == kScaleBF16 ? fb : fh;
-  return st == kScaleF32 ? __uint_as_float(x) : f16or;
+__device__ __forceinline__ float lds_scale(const char* p, int st) {
+  if (st == kScaleF32) return *reinterpret_cast<const float*>(p);
+  const uint16_t h = *reinterpret_cast<const uint16_t*>(p);
+  return st == kScaleBF16 ? bf16_bits_to_f32(h) : f16_bits_to_f32(h);
 }
 
-__device__ __forceinline__ void unit_to_f32(int act_t, uint4 x0, uint4 x1, float (&f)[8]) {
-  const uint32_t w[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
-  if (act_t == kActF32) {
-#pragma unroll
-    for (int j = 0; j < 8; j++) f[j] = __uint_as_float(w[j]);
-  } else if (act_t == kActBF16) {
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-      f[2 * j] = __uint_as_float(w[j] << 16);
-      f[2 * j + 1] = __uint_as_float(w[j] & 0xFFFF0000u);
-    }
-  } else {
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-      const h2_t h = as_h2(w[j]);
-      f[2 * j] = float(h[0]);
-      f[2 * j + 1] = float(h[1]);
+// consumer-only barrier: an LDS arrival counter (the loader never joins)
+__device__ __forceinline__ void cbar(uint32_t a, unsigned& epoch, unsigned* ctl, int lane, bool& failed) {
+  epoch += NC;
+  if (lane == 0) lds_add(a, 1u);
+  unsigned spins = 0;
+  while (!failed && lds_ld(a) < epoch) {
+    __builtin_amdgcn_s_sleep(1);
+    if (++spins > kSpinMax) {
+      if (lane == 0) give_up(ctl, 5);
+      failed = true;
     }
   }
 }
 
-template <int HILO>
-__device__ __forceinline__ void unit_store(char* smem, const float (&f)[8], int row, int k, int M, int Kp) {
-  h8_t hi, lo;
-#pragma unroll
-  for (int j = 0; j < 8; j++) {
-    hi[j] = _Float16(f[j]);
-    lo[j] = _Float16(f[j] - float(hi[j]));
-  }
-  *reinterpret_cast<h8_t*>(smem + (size_t(row) * Kp + k) * 2) = hi;
-  if constexpr (HILO != 0) *reinterpret_cast<h8_t*>(smem + (size_t(M + row) * Kp + k) * 2) = lo;
-}
-
-// ------------------------------------------------------------------------------------------------ the kernel
-constexpr int AR = 3;  // activation staging units (8 elements) per thread held in registers
-
-template <int HILO, bool ASYM>
-__global__ __launch_bounds__(768) void woq_chain_kernel(const GemvArgs* __restrict__ ops, int n_ops,
-                                                         unsigned* flags, unsigned* status, int npre) {
+template <int BITS, int GPT, bool ASYM, int SD>
+__global__ __launch_bounds__(kEngThreads, 1) void woq_engine_kernel(const EngOp* __restrict__ ops, int n_ops,
+                                                                    unsigned* ctl, int S, int slot_bytes, int Kp,
+                                                                    int bump) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int KT = 128, SPT = 4, BIAS = 8;  // int4, one group per >= one K tile (host-checked)
+  constexpr int KT = BITS == 4 ? 128 : 256, SPT = KT / 32, SPG = SPT / GPT, BIAS = BITS == 4 ? 8 : 2;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));
-  const int NW = __builtin_amdgcn_readfirstlane(int(blockDim.x >> 6));
-  const int G = gridDim.x, bid = blockIdx.x, bd = blockDim.x, tid = threadIdx.x;
-  const uint32_t m0 = 0x000F000Fu, m1 = 0x00F000F0u, mag = 0x64006400u;
+  const uint32_t ctl_a = lds_addr(smem);
+  float* part = reinterpret_cast<float*>(smem + kCtlBytes);          // [stripe][consumer][16]
+  char* act = smem + kCtlBytes + kPartBytes;                          // [Kp / 8] units of {hi[8], lo[8]} fp16
+  char* ring = act + size_t(Kp) * 4;
+  if (threadIdx.x < 32) reinterpret_cast<unsigned*>(smem)[threadIdx.x] = 0u;
+  __syncthreads();
+  if (wave == NC) {
+    loader<GPT, ASYM, SD>(ops, n_ops, ring, S, slot_bytes, ctl_a, ctl, lane);
+    return;
+  }
+
+  const int cw = wave, cl = wave * 64 + lane;  // consumer wave, consumer lane
+  const uint32_t full_a = ctl_a + kFull * 4, free_a = ctl_a + kFree * 4, bar_a = ctl_a + kBar * 4;
+  float* nsum = reinterpret_cast<float*>(smem) + kNsum;
+  const unsigned gen = __builtin_amdgcn_readfirstlane(__hip_atomic_load(ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  unsigned bar_epoch = 0;
+  bool failed = false;
+  const int m = lane & 15, kq = lane >> 4;
+  const uint32_t mk0 = 0x000F000Fu, mk1 = 0x00F000F0u, mag = 0x64006400u;
   const h2_t s16 = splat(1.f / 16.f);
-  bool gave_up = false;
+  const h2_t zc0 = splat(-(1024.f + BIAS)), zc1 = splat(-(64.f + BIAS));
+  // this lane's A operand: MFMA rows 0-7 read hi, rows 8-15 lo (rows 0 and 8 are the result); k unit u = k / 8 at byte
+  // 32 u (+16: lo), so step d of tile t starts at byte t * KT * 4 + d * 128 + kq * 32
+  const char* a_lane = act + (m >= 8 ? 16 : 0) + kq * 32;
+  int f = 0, slot = 0;
 
   for (int op = 0; op < n_ops; op++) {
-    const GemvArgs& a = ops[op];
-    const int M = a.M, nt = a.nt, Kp = nt * KT;
-    const int R = HILO == 0 ? M : 2 * M;
-    const int nsl = (nt + KS - 1) / KS;
-    const int NWa = a.nwa;  // waves owning K slices: as in the single-op launch, so the sums match it bit for bit
-    const int u0 = int(unsigned(bid) * unsigned(a.units) / unsigned(G));
-    const int u1 = int(unsigned(bid + 1) * unsigned(a.units) / unsigned(G));
-    const int vpu = a.dual ? 2 : 1;
-    const int v0 = u0 * vpu, nv = (u1 - u0) * vpu;
-    const bool idle = wave >= nsl || wave >= NWa;
-    float* part = reinterpret_cast<float*>(smem + a.part_off);  // [nv][NWa][M][16]
-    const int vs = a.scale_t == kScaleF32 ? (lane & 15) * 4 : (lane & 14) * 2;
+    const EngOp& o = ops[op];
+    const int K = o.K, nt = o.nt, Kpo = nt * KT, nch = (nt + FT - 1) / FT;
+    const int st = o.scale_t, ssz = st == kScaleF32 ? 4 : 2;
 
-    // 1) the first three weight stages of this op (independent of the activations): in flight during the wait
-    StageCursor lc;
-    lc.j = idle ? nv : 0;
-    lc.q = wave;
-    lc.s = 0;
-    lc.rt = rsrc(a.w[0].tiles, 0);
-    lc.rs = lc.rt;
-    lc.rz = lc.rt;
-    if (!idle && nv > 0) cursor_stripe(a, lc, v0);
-    StageRegs<ASYM> S0, S1, S2;
-    CTRACE(0);
-    if (wave != 0 && npre) {
-      load_stage<ASYM>(a, S0, lc, nv, nsl, wave, NWa, v0, lane, vs);
-      load_stage<ASYM>(a, S1, lc, nv, nsl, wave, NWa, v0, lane, vs);
-      load_stage<ASYM>(a, S2, lc, nv, nsl, wave, NWa, v0, lane, vs);
-    }
-
-    // 2) wave 0 waits until every workgroup has published ops 0..op-1, then issues its own stages
-    if (wave == 0) {
-      if (op > 0 && !gave_up) {
-        // every workgroup's flag >= op: lane l checks flags 4l..4l+3 with one sc1 16-B load (no atomics, no
-        // fan-in serialisation: measured single-counter barriers cost ~7 us at 256 workgroups)
-        const auto rf = rsrc(flags, G * 4);
-        const unsigned target = unsigned(op);
-        unsigned spins = 0;
-        while (true) {
-          const uint4 f4 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rf, lane * 16, 0, kSC1));
-          const bool ok = lane * 4 >= G || ((f4.x >= target || lane * 4 + 0 >= G) && (f4.y >= target || lane * 4 + 1 >= G) &&
-                                            (f4.z >= target || lane * 4 + 2 >= G) && (f4.w >= target || lane * 4 + 3 >= G));
-          if (__all(ok)) break;
-          __builtin_amdgcn_s_sleep(1);
-          if (++spins > (1u << 21)) {  // ~1 s: never expected; record it, stop waiting, and run on rather than hang
-            if (lane == 0) __hip_atomic_store(status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            gave_up = true;
-            break;
-          }
-        }
-      }
-      load_stage<ASYM>(a, S0, lc, nv, nsl, wave, NWa, v0, lane, vs);
-      load_stage<ASYM>(a, S1, lc, nv, nsl, wave, NWa, v0, lane, vs);
-      load_stage<ASYM>(a, S2, lc, nv, nsl, wave, NWa, v0, lane, vs);
-    }
-    __syncthreads();
-    if (wave != 0 && !npre) {
-      load_stage<ASYM>(a, S0, lc, nv, nsl, wave, NWa, v0, lane, vs);
-      load_stage<ASYM>(a, S1, lc, nv, nsl, wave, NWa, v0, lane, vs);
-      load_stage<ASYM>(a, S2, lc, nv, nsl, wave, NWa, v0, lane, vs);
-    }
-    CTRACE(1);
-
-    // 3) stage the activations (sc1 loads: they may come from another workgroup of this launch)
-    const int KU = Kp >> 3;
-    const int a_units = M * KU;
-    const int esz = a.act_t == kActF32 ? 4 : 2;
-    const auto ra = rsrc(a.A, (M - 1) * a.lda * esz + a.K * esz);
-    float f[AR][8];
-#pragma unroll
-    for (int q = 0; q < AR; q++) {
-      const int u = q * bd + tid;
-      const int row = u / KU, k = (u - row * KU) * 8;
-      const int off = (u < a_units && k < a.K) ? (row * a.lda + k) * esz : kOOB;
-      const uint4 x0 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(ra, off, 0, kSC1));
-      const uint4 x1 = a.act_t == kActF32
-                           ? __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(ra, off + 16, 0, kSC1))
-                           : make_uint4(0u, 0u, 0u, 0u);
-      unit_to_f32(a.act_t, x0, x1, f[q]);
-    }
-    if (a.norm) {  // RMSNorm of each row: per-wave row sums in LDS, combined in wave order (deterministic)
-      float* slot = reinterpret_cast<float*>(smem + a.part_off);  // [NW][8] scratch: partial slots not live yet
-      float rs[8];
-#pragma unroll
-      for (int r = 0; r < 8; r++) rs[r] = 0.f;
-#pragma unroll
-      for (int q = 0; q < AR; q++) {
-        const int u = q * bd + tid;
-        float s2 = 0.f;
-#pragma unroll
-        for (int j = 0; j < 8; j++) s2 += f[q][j] * f[q][j];
-        const int row = u < a_units ? u / KU : 8;
-#pragma unroll
-        for (int r = 0; r < 8; r++) rs[r] += row == r ? s2 : 0.f;
-      }
-      for (int r = 0; r < M; r++) {
-        float v = rs[r];
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-        if (lane == 0) slot[wave * 8 + r] = v;
-      }
-      __syncthreads();
-      float inv[8];
-#pragma unroll
-      for (int r = 0; r < 8; r++) {
-        float tot = 0.f;
-        if (r < M)
-          for (int w = 0; w < NW; w++) tot += slot[w * 8 + r];
-        inv[r] = 1.f / sqrtf(tot / float(a.K) + a.norm_eps);
-      }
-#pragma unroll
-      for (int q = 0; q < AR; q++) {
-        const int u = q * bd + tid;
-        const int row = min(u / KU, M - 1), k = (u - (u / KU) * KU) * 8;
-        float r = inv[0];
-#pragma unroll
-        for (int rr = 1; rr < 8; rr++) r = row == rr ? inv[rr] : r;
-#pragma unroll
-        for (int j = 0; j < 8; j++) {
-          const float g = (a.norm_w != nullptr && k + j < a.K) ? a.norm_w[k + j] : 1.f;
-          f[q][j] = f[q][j] * r * g;
-        }
-      }
-    }
-#pragma unroll
-    for (int q = 0; q < AR; q++) {
-      const int u = q * bd + tid;
-      if (u < a_units) unit_store<HILO>(smem, f[q], u / KU, (u - (u / KU) * KU) * 8, M, Kp);
-    }
+    // 1) the input vector -> LDS as fp32 (element i at byte 4i), then in place as MFMA-ready fp16 rows: 8-element
+    //    unit u (bytes 32u .. 32u + 31) becomes {hi[8u .. 8u + 7], lo[8u .. 8u + 7]}, so one lane converts a unit with
+    //    no hazard against other lanes
+    float s2 = 0.f;
     {
-      uint4* zr = reinterpret_cast<uint4*>(smem + size_t(R) * Kp * 2);
-      for (int i = tid; i < (Kp >> 3); i += bd) zr[i] = make_uint4(0u, 0u, 0u, 0u);
-    }
-    __syncthreads();
-    CTRACE(2);
-
-    // 4) the stripe stream (woq_gemv.hip)
-    const int m = lane & 15;
-    const int kq = lane >> 4;
-    const int arow = HILO == 1 ? (m & 7) : m;
-    const bool is_lo = HILO == 1 && m >= 8;
-    const int row_hi = arow < M ? (is_lo ? M + arow : arow) : R;
-    const char* a_hi = smem + size_t(row_hi) * Kp * 2 + kq * 16;
-    const int ssh = a.scale_t == kScaleF32 ? 0 : (lane & 1) * 16;
-    const h2_t zc0 = splat(-(1024.f + BIAS)), zc1 = splat(-(64.f + BIAS));
-
-    f4_t acc = {0.f, 0.f, 0.f, 0.f};
-    int cj = idle ? nv : 0, cq = wave;
-
-    auto compute_stage = [&](const StageRegs<ASYM>& S) {
-      if (cj >= nv) return;
-      const int t0 = cq * KS;
-      const char* ab = a_hi + t0 * KT * 2;
-      f4_t accg[KS];  // as woq_gemv.hip: KS independent chains, step-major, scaled per tile in tile order
+      float* af32 = reinterpret_cast<float*>(act);
+      const int npair = (K + 1) / 2;  // granule / element pairs: one 16-B (8-B external) load per pair
+      if (o.act_gran) {
+        const unsigned want = gen * 256u + o.act_tag;
+        const auto rg = rsrc(o.act_gran, unsigned(K) * 8u);
+        for (int q0 = 0; q0 < npair; q0 += NC * 64 * PJ) {
+          uint32_t pend = 0;
 #pragma unroll
-      for (int d = 0; d < SPT; d++) {
+          for (int j = 0; j < PJ; j++)
+            if (q0 + cl + NC * 64 * j < npair) pend |= 1u << j;
+          unsigned spins = 0;
+          while (true) {
+            uint4 g[PJ];
 #pragma unroll
-        for (int i = 0; i < KS; i++) {
-          const int ti = min(t0 + i, nt - 1) - t0;
-          h8_t bf;
-          if constexpr (ASYM) {
-            const float z = float(S.zp[i]);
-            bf = dequant4(S.b[i][d], m0, m1, mag, s16, zc0 - splat(z), zc1 - splat(z));
-          } else {
-            bf = dequant4(S.b[i][d], m0, m1, mag, s16, zc0, zc1);
+            for (int j = 0; j < PJ; j++)
+              g[j] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                   rg, (pend >> j) & 1u ? (q0 + cl + NC * 64 * j) * 16 : kOOB, 0, kSC1));
+            __builtin_amdgcn_sched_barrier(0);  // every load of the pass in flight before the first tag check
+#pragma unroll
+            for (int j = 0; j < PJ; j++) {
+              const int q = q0 + cl + NC * 64 * j;
+              // the pair's second granule is past K for odd K: its tag is never written, value 0
+              const bool ok1 = 2 * q + 1 >= K || g[j].w == want;
+              if (((pend >> j) & 1u) && g[j].y == want && ok1) {
+                const float x0 = __uint_as_float(g[j].x), x1 = 2 * q + 1 < K ? __uint_as_float(g[j].z) : 0.f;
+                *reinterpret_cast<float2*>(af32 + 2 * q) = make_float2(x0, x1);
+                s2 += x0 * x0 + x1 * x1;
+                pend &= ~(1u << j);
+              }
+            }
+            if (__all(pend == 0u) || failed) break;
+            __builtin_amdgcn_s_sleep(1);
+            if (++spins > kSpinMax) {
+              if (lane == 0) give_up(ctl, 3);
+              failed = true;
+            }
           }
-          const h8_t af = *reinterpret_cast<const h8_t*>(ab + ti * KT * 2 + d * 64);
-          accg[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, bf, d == 0 ? f4_t{0.f, 0.f, 0.f, 0.f} : accg[i], 0, 0, 0);
+        }
+      } else {  // an external vector (written before this launch): plain loads, all of a pass in flight at once
+        const auto ra = rsrc(o.act, unsigned(K) * 4u);
+        for (int q0 = 0; q0 < npair; q0 += NC * 64 * PJ) {
+          uint2 g[PJ];
+#pragma unroll
+          for (int j = 0; j < PJ; j++) {
+            const int q = q0 + cl + NC * 64 * j;
+            g[j] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(ra, q < npair ? q * 8 : kOOB, 0, 0));
+          }
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int j = 0; j < PJ; j++) {
+            const int q = q0 + cl + NC * 64 * j;
+            if (q < npair) {
+              // odd K: the last pair's second element lies past the vector (its bytes are out of range: 0)
+              const float x0 = __uint_as_float(g[j].x), x1 = 2 * q + 1 < K ? __uint_as_float(g[j].y) : 0.f;
+              *reinterpret_cast<float2*>(af32 + 2 * q) = make_float2(x0, x1);
+              s2 += x0 * x0 + x1 * x1;
+            }
+          }
         }
       }
-#pragma unroll
-      for (int i = 0; i < KS; i++) acc += accg[i] * scale_bits_to_f32(S.sc[i], a.scale_t, ssh);
-      cq += NWa;
-      if (cq >= nsl) {
-        f4_t r = acc;
-        if constexpr (HILO == 1) {
-#pragma unroll
-          for (int xx = 0; xx < 4; xx++) r[xx] += __shfl_down(r[xx], 32, 64);
-        }
-        float* ps = part + (size_t(cj) * NWa + wave) * M * 16 + m;
-#pragma unroll
-        for (int xx = 0; xx < 4; xx++) {
-          const int row = (lane >> 4) * 4 + xx;
-          if (row < M && (HILO != 1 || lane < 32)) ps[row * 16] = r[xx];
-        }
-        acc = f4_t{0.f, 0.f, 0.f, 0.f};
-        cq = wave;
-        cj++;
-      }
-    };
-
-    while (cj < nv) {
-      compute_stage(S0);
-      load_stage<ASYM>(a, S0, lc, nv, nsl, wave, NWa, v0, lane, vs);
-      compute_stage(S1);
-      load_stage<ASYM>(a, S1, lc, nv, nsl, wave, NWa, v0, lane, vs);
-      compute_stage(S2);
-      load_stage<ASYM>(a, S2, lc, nv, nsl, wave, NWa, v0, lane, vs);
+      for (int i = 2 * npair + cl; i < Kpo; i += NC * 64) af32[i] = 0.f;  // K tail of the last tile
     }
-    __syncthreads();
-    CTRACE(3);
+    if (o.norm) {
+#pragma unroll
+      for (int sh = 32; sh > 0; sh >>= 1) s2 += __shfl_xor(s2, sh, 64);
+      if (lane == 0) nsum[cw] = s2;
+    }
+    cbar(bar_a, bar_epoch, ctl, lane, failed);
+    {
+      float inv = 1.f;
+      if (o.norm) {  // RMSNorm: lane sums -> wave sums -> the same consumer-order total in every wave
+        float tot = 0.f;
+#pragma unroll
+        for (int w = 0; w < NC; w++) tot += nsum[w];
+        inv = 1.f / sqrtf(tot / float(K) + o.norm_eps);
+      }
+      for (int u = cl; u < Kpo / 8; u += NC * 64) {
+        float4* pu = reinterpret_cast<float4*>(act + u * 32);
+        const float4 a0 = pu[0], a1 = pu[1];
+        float x[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+        if (o.norm) {
+          float gw[8];
+#pragma unroll
+          for (int e = 0; e < 8; e++) gw[e] = 1.f;
+          if (o.norm_w) {  // eight independent loads, one wait
+#pragma unroll
+            for (int e = 0; e < 8; e++) gw[e] = o.norm_w[min(8 * u + e, K - 1)];
+#pragma unroll
+            for (int e = 0; e < 8; e++) gw[e] = 8 * u + e < K ? gw[e] : 1.f;
+          }
+#pragma unroll
+          for (int e = 0; e < 8; e++) x[e] = x[e] * inv * gw[e];
+        }
+        h8_t hi, lo;
+#pragma unroll
+        for (int e = 0; e < 8; e++) {
+          hi[e] = _Float16(x[e]);
+          lo[e] = _Float16(x[e] - float(hi[e]));
+        }
+        reinterpret_cast<h8_t*>(pu)[0] = hi;
+        reinterpret_cast<h8_t*>(pu)[1] = lo;
+      }
+    }
+    cbar(bar_a, bar_epoch, ctl, lane, failed);
 
-    // 5) reduce in wave order, epilogue, write-through stores; then one arrival per workgroup
-    const int nout = (u1 - u0) * M * 16;
-    const int nwl = min(NWa, nsl);
-    for (int o = tid; o < nout; o += bd) {
-      const int p = o / (M * 16), mm = (o >> 4) % M, nn = o & 15;
+    // 2) the weight stream: consumer cw takes tiles cw and cw + 8 of every fill
+    int v0, nv;
+    unit_range(o, blockIdx.x, v0, nv);
+    for (int jl = 0; jl < nv; jl++) {
+      f4_t acc = {0.f, 0.f, 0.f, 0.f};
+      for (int c = 0; c < nch; c++) {
+        unsigned spins = 0;
+        while (!failed && lds_ld(full_a + slot * 4) < unsigned(f + 1)) {
+          __builtin_amdgcn_s_sleep(1);
+          if (++spins > kSpinMax) {
+            if (lane == 0) give_up(ctl, 1);
+            failed = true;
+          }
+        }
+        const char* sb = ring + slot * slot_bytes;
+        const char* scb = sb + FT * 1024;
+        const char* zpb = scb + SD * 1024;
+        const int t0 = c * FT;
+        int g0, ngc;
+        fill_groups<GPT>(o, t0, g0, ngc);
+#pragma unroll
+        for (int h = 0; h < FT / NC; h++) {
+          const int p = cw + h * NC, t = t0 + p;
+          if (t >= nt) break;
+          const u4_t b = *reinterpret_cast<const u4_t*>(sb + p * 1024 + lane * 16);
+          const char* ab = a_lane + size_t(t) * KT * 4;
+          f4_t accg = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int d = 0; d < SPT; d++) {
+            const int gi = GPT == 1 ? (t >> o.tpg_shift) - g0 : p * GPT + d / SPG;
+            h8_t bf;
+            if constexpr (BITS == 4) {
+              if constexpr (ASYM) {
+                const float z = float(*reinterpret_cast<const int8_t*>(zpb + gi * 16 + m));
+                bf = dequant4(b[d], mk0, mk1, mag, s16, zc0 - splat(z), zc1 - splat(z));
+              } else {
+                bf = dequant4(b[d], mk0, mk1, mag, s16, zc0, zc1);
+              }
+            } else {
+              const int z = ASYM ? int(*reinterpret_cast<const int8_t*>(zpb + gi * 16 + m)) : 0;
+              bf = dequant_step<BITS>(b, d, zp_const(BIAS + z));
+            }
+            const h8_t af = *reinterpret_cast<const h8_t*>(ab + d * 128);
+            accg = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, bf, d % SPG == 0 ? f4_t{0.f, 0.f, 0.f, 0.f} : accg, 0,
+                                                          0, 0);
+            if ((d + 1) % SPG == 0) acc += accg * lds_scale(scb + (gi * 16 + m) * ssz, st);
+          }
+        }
+        if (lane == 0) lds_add(free_a + slot * 4, 1u);  // this consumer is done with the slot
+        f++;
+        slot = slot + 1 == S ? 0 : slot + 1;
+      }
+      const float r = acc[0] + __shfl_down(acc[0], 32, 64);  // row 0 (hi) + row 8 (lo)
+      if (lane < 16) part[(jl * NC + cw) * 16 + lane] = r;
+    }
+    cbar(bar_a, bar_epoch, ctl, lane, failed);
+
+    // 3) sum the consumers' partials in a fixed order, epilogue, results + granules
+    const int vpu = o.dual ? 2 : 1;
+    const int nout = nv / vpu * 16;
+    const unsigned tag = gen * 256u + o.tag;
+    for (int oi = cl; oi < nout; oi += NC * 64) {
+      const int p = oi >> 4, nn = oi & 15;
       float y[2] = {0.f, 0.f};
 #pragma unroll
       for (int h = 0; h < 2; h++) {
         if (h < vpu) {
-          const float* ps = part + (size_t(p * vpu + h) * NWa * M + mm) * 16 + nn;
-          const size_t wst = size_t(M) * 16;
-          float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-          int w = 0;
-          for (; w + 3 < nwl; w += 4) {
-            s0 += ps[size_t(w) * wst];
-            s1 += ps[size_t(w + 1) * wst];
-            s2 += ps[size_t(w + 2) * wst];
-            s3 += ps[size_t(w + 3) * wst];
-          }
-          for (; w < nwl; w++) s0 += ps[size_t(w) * wst];
-          y[h] = (s0 + s1) + (s2 + s3);
+          const float* ps = part + (p * vpu + h) * NC * 16 + nn;
+          y[h] = ((ps[0] + ps[16]) + (ps[32] + ps[48])) + ((ps[64] + ps[80]) + (ps[96] + ps[112]));
         }
       }
       int wsel, s;
-      vstripe(a, v0 + p * vpu, wsel, s);
-      if (a.dual) wsel = 0;
+      vstripe(o, v0 + p * vpu, wsel, s);
+      const EngWeight& W = o.w[wsel];
       const int n = s * 16 + nn;
-      const int nmax = sel3(wsel, a.w[0].n, a.w[1].n, a.w[2].n);
-      if (n >= nmax) continue;
-      float* out = sel3(wsel, a.w[0].out, a.w[1].out, a.w[2].out);
-      const int ldo = sel3(wsel, a.w[0].ldo, a.w[1].ldo, a.w[2].ldo);
-      float v = y[0];
-      switch (a.epi) {
-        case kEpiBias:
-          v += a.w[0].bias[size_t(mm) * a.w[0].bias_ld + n];
-          break;
-        case kEpiAddGelu:
-          v = gelu_f(v + a.w[0].bias[size_t(mm) * a.w[0].bias_ld + n]);
-          break;
-        case kEpiGelu:
-          v = gelu_f(v);
-          break;
-        case kEpiSilu:
-          v = silu_f(v);
-          break;
-        case kEpiResAdd:
-          v += ld_sc1(a.res + size_t(mm) * a.ld_res + n);
-          break;
-        case kEpiSiluMul: {
-          const float t1 = silu_f(y[0]);
-          if (a.aux) st_sc1(a.aux + size_t(mm) * a.ld_aux + n, t1);
-          v = t1 * y[1];
-          break;
+      if (n >= W.n) continue;
+      float val = y[0];
+      if (o.epi == kEpiResAdd) {
+        float r;
+        if (o.res_gran) {
+          const unsigned want = gen * 256u + o.res_tag;
+          unsigned spins = 0;
+          while (true) {
+            const unsigned long long x = __hip_atomic_load(o.res_gran + n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            r = __uint_as_float(unsigned(x));
+            if (unsigned(x >> 32) == want || failed) break;
+            __builtin_amdgcn_s_sleep(1);
+            if (++spins > kSpinMax) {
+              give_up(ctl, 4);
+              failed = true;
+            }
+          }
+        } else {
+          r = o.res[n];
         }
-        case kEpiGeluMul: {
-          const float t1 = gelu_f(y[0]);
-          if (a.aux) st_sc1(a.aux + size_t(mm) * a.ld_aux + n, t1);
-          v = t1 * y[1];
-          break;
-        }
-        default:
-          break;
+        val += r;
+      } else if (o.epi == kEpiSiluMul || o.epi == kEpiGeluMul) {
+        const float t1 = o.epi == kEpiSiluMul ? silu_f(y[0]) : gelu_f(y[0]);
+        if (o.aux) o.aux[n] = t1;
+        val = t1 * y[1];
       }
-      st_sc1(out + size_t(mm) * ldo + n, v);
+      if (W.out) W.out[n] = val;
+      if (W.gran)
+        __hip_atomic_store(W.gran + n, (static_cast<unsigned long long>(tag) << 32) | __float_as_uint(val),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) __hip_atomic_store(flags + bid, unsigned(op + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    CTRACE(4);
   }
+  // the launch generation moves on once this workgroup is done: every workgroup read it before publishing anything,
+  // and workgroup 0 got here only after gathering results of every workgroup (bump is set only when an op reads a
+  // result of this launch)
+  if (bump && blockIdx.x == 0 && cw == 0 && lane == 0)
+    __hip_atomic_fetch_add(ctl, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-}  // namespace chain
+}  // namespace eng
 
 // ------------------------------------------------------------------------------------------------ host side
-size_t chain_lds_layout(GemvArgs& a, int waves, int grid) {
-  const int R = a.act_t == kActF16 ? a.M : 2 * a.M;
-  const size_t kp = size_t(a.nt) * 128;
-  const size_t abytes = (size_t(R) + 1) * kp * 2;
-  const int upw = (a.units + grid - 1) / grid;
-  const size_t nv = size_t(upw) * (a.dual ? 2 : 1);
-  a.part_off = int((abytes + 15) & ~size_t(15));
-  const size_t part = nv * waves * a.M * 16 * 4;
-  const size_t norm_scratch = size_t(waves) * 8 * 4;  // RMSNorm per-wave row sums
-  return size_t(a.part_off) + (part > norm_scratch ? part : norm_scratch);
+bool engine_geometry(EngGeometry& g, int kp) {
+  g.kp = (kp + 15) / 16 * 16;
+  g.slot_bytes = size_t(kEngFillTiles) * 1024 + size_t(g.sd) * 1024 + (g.asym ? 1024 : 0);
+  const size_t fixed = size_t(eng::kCtlBytes) + eng::kPartBytes + size_t(g.kp) * 4;
+  const size_t budget = 160 * 1024;
+  if (fixed >= budget) return false;
+  int s = int((budget - fixed) / g.slot_bytes);
+  if (s > 8) s = 8;
+  if (s < kEngInflight + 2) return false;  // one slot to fill, D in flight, one being read
+  g.slots = s;
+  g.lds = fixed + size_t(s) * g.slot_bytes;
+  return true;
 }
 
-hipError_t launch_chain(const GemvArgs* dev_ops, int n_ops, int hilo, int asym, int waves, int grid, size_t lds,
-                        unsigned* flags, unsigned* status, int npre, hipStream_t st) {
-  auto pick = [&](auto k) -> hipError_t {
+template <int BITS, int GPT, bool ASYM, int SD>
+static hipError_t engine_launch4(const EngOp* ops, int n_ops, const EngGeometry& g, unsigned* ctl, int grid, int bump,
+                                 hipStream_t st) {
+  auto k = eng::woq_engine_kernel<BITS, GPT, ASYM, SD>;
+  static bool attr = false;
+  if (!attr) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
                                        160 * 1024);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k, dim3(grid), dim3(waves * 64), lds, st, dev_ops, n_ops, flags, status, npre);
-    return hipGetLastError();
-  };
-  if (hilo == 0) return asym ? pick(chain::woq_chain_kernel<0, true>) : pick(chain::woq_chain_kernel<0, false>);
-  return asym ? pick(chain::woq_chain_kernel<1, true>) : pick(chain::woq_chain_kernel<1, false>);
+    attr = true;
+  }
+  hipLaunchKernelGGL(k, dim3(grid), dim3(kEngThreads), g.lds, st, ops, n_ops, ctl, g.slots, int(g.slot_bytes), g.kp,
+                     bump);
+  return hipGetLastError();
+}
+
+template <int BITS, int GPT>
+static hipError_t engine_launch2(const EngOp* ops, int n_ops, const EngGeometry& g, unsigned* ctl, int grid, int bump,
+                                 hipStream_t st) {
+  if (g.sd == 1)
+    return g.asym ? engine_launch4<BITS, GPT, true, 1>(ops, n_ops, g, ctl, grid, bump, st)
+                  : engine_launch4<BITS, GPT, false, 1>(ops, n_ops, g, ctl, grid, bump, st);
+  if (g.sd == 2)
+    return g.asym ? engine_launch4<BITS, GPT, true, 2>(ops, n_ops, g, ctl, grid, bump, st)
+                  : engine_launch4<BITS, GPT, false, 2>(ops, n_ops, g, ctl, grid, bump, st);
+  return hipErrorInvalidValue;
+}
+
+hipError_t launch_engine(const EngOp* ops, int n_ops, const EngGeometry& g, unsigned* ctl, int grid, int bump,
+                         hipStream_t st) {
+  static_assert(kEngConsumers == 8, "the partial-sum order below is written for 8 consumers");
+  if (g.bits == 4) {
+    if (g.gpt == 1) return engine_launch2<4, 1>(ops, n_ops, g, ctl, grid, bump, st);
+    if (g.gpt == 2) return engine_launch2<4, 2>(ops, n_ops, g, ctl, grid, bump, st);
+  } else if (g.bits == 2) {
+    if (g.gpt == 1) return engine_launch2<2, 1>(ops, n_ops, g, ctl, grid, bump, st);
+    if (g.gpt == 2) return engine_launch2<2, 2>(ops, n_ops, g, ctl, grid, bump, st);
+    if (g.gpt == 4) return engine_launch2<2, 4>(ops, n_ops, g, ctl, grid, bump, st);
+  }
+  return hipErrorInvalidValue;
 }
 
 }  // namespace nad
-
-#ifdef NAD_CHAIN_TRACE
-extern "C" int nad_chain_trace_fetch(void* host, size_t bytes) {
-  if (hipDeviceSynchronize() != hipSuccess) return -1;
-  const size_t n = sizeof(nad::chain::nad_chain_trace) < bytes ? sizeof(nad::chain::nad_chain_trace) : bytes;
-  return hipMemcpyFromSymbol(host, HIP_SYMBOL(nad::chain::nad_chain_trace), n) == hipSuccess ? 0 : -1;
-}
-#endif

@@ -133,6 +133,15 @@ __global__ __launch_bounds__(512, 1) void woq_gemm2_kernel(GemmArgs a, const _Fl
     const float f16or = st == kScaleBF16 ? fb : fh;
     return st == kScaleF32 ? __uint_as_float(x) : f16or;
   };
+  // FOLD: this lane's two stripe scales of the current tile as fp16 pairs (fp16 scales: the stored bits, exact)
+  h2_t fsc[2] = {g2::splat(1.f), g2::splat(1.f)};
+  auto scale_h2 = [&](uint32_t x) {
+    if (st == kScaleF16) {
+      const uint32_t h = (x >> ssh) & 0xFFFFu;
+      return as_h2(h | (h << 16));
+    }
+    return g2::splat(scale_f32(x));
+  };
 
   f4_t acc[4][4], accg[4][4];
 #pragma unroll
@@ -358,7 +367,11 @@ __device__ __forceinline__ uint32_t lds_addr(const char* p) {
   return uint32_t(reinterpret_cast<uintptr_t>((const __attribute__((address_space(3))) char*)p));
 }
 
-template <bool ASYM, bool TPG1>
+// FOLD: the group scale is multiplied into the fp16 B fragment (q * s rounded once to fp16, the host checked that every
+// q * s of the weight is an fp16 normal, DeviceWeight::fold_ok) and the MFMAs accumulate straight into the result: no
+// per-group fp32 accumulator, no group-end scaling (the reference itself dequantizes to bf16 for its AMX-BF16 core,
+// bestla_prologue_b.h:732-838 getFpWeight)
+template <bool ASYM, bool TPG1, bool FOLD>
 __global__ __launch_bounds__(512, 1) void woq_gemm3_kernel(GemmArgs a, const _Float16* __restrict__ A16, int lda16) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63;
@@ -470,6 +483,15 @@ __global__ __launch_bounds__(512, 1) void woq_gemm3_kernel(GemmArgs a, const _Fl
     const float f16or = st == kScaleBF16 ? fb : fh;
     return st == kScaleF32 ? __uint_as_float(x) : f16or;
   };
+  // FOLD: this lane's two stripe scales of the current tile as fp16 pairs (fp16 scales: the stored bits, exact)
+  h2_t fsc[2] = {g2::splat(1.f), g2::splat(1.f)};
+  auto scale_h2 = [&](uint32_t x) {
+    if (st == kScaleF16) {
+      const uint32_t h = (x >> ssh) & 0xFFFFu;
+      return as_h2(h | (h << 16));
+    }
+    return g2::splat(scale_f32(x));
+  };
 
   // hand-over: batch(u - 2) (the buffers half step u + 1 reads) has landed for this wave; batches u - 1 and u
   // (8 A pieces + one B batch, whatever the order inside a batch) stay in flight across the barrier
@@ -509,10 +531,19 @@ __global__ __launch_bounds__(512, 1) void woq_gemm3_kernel(GemmArgs a, const _Fl
       zw0 = lds_b32<0>(bl + zoff);
       zw1 = lds_b32<64>(bl + zoff);
     }
+    uint32_t fw0 = 0, fw1 = 0;
+    if constexpr (FOLD && H == 0) {  // every tile carries its group's scale piece
+      fw0 = lds_b32<0>(bl + soff);
+      fw1 = lds_b32<64>(bl + soff);
+    }
     h8_t af0[8], af1[8];
     lds_frags(af0, al + roff[0], std::make_index_sequence<8>{});
     lds_frags(af1, al + roff[1], std::make_index_sequence<8>{});
-    wait_lgk<8>(bv0, bv1, zw0, zw1, af0[0], af0[1], af0[2], af0[3], af0[4], af0[5], af0[6], af0[7]);
+    wait_lgk<8>(bv0, bv1, zw0, zw1, fw0, fw1, af0[0], af0[1], af0[2], af0[3], af0[4], af0[5], af0[6], af0[7]);
+    if constexpr (FOLD && H == 0) {
+      fsc[0] = scale_h2(fw0);
+      fsc[1] = scale_h2(fw1);
+    }
     const uint32_t bw[2][2] = {{bv0.x, bv0.y}, {bv1.x, bv1.y}};
     int zp[2] = {0, 0};
     if constexpr (ASYM) {
@@ -527,7 +558,7 @@ __global__ __launch_bounds__(512, 1) void woq_gemm3_kernel(GemmArgs a, const _Fl
       if (dd == 1) {
         wait_lgk<0>(af1[0], af1[1], af1[2], af1[3], af1[4], af1[5], af1[6], af1[7]);
         if constexpr (L) {
-          if (gend) {
+          if (!FOLD && gend) {
             sw0 = lds_b32<0>(bl + soff);
             sw1 = lds_b32<64>(bl + soff);
             wait_lgk<0>(sw0, sw1);
@@ -544,20 +575,26 @@ __global__ __launch_bounds__(512, 1) void woq_gemm3_kernel(GemmArgs a, const _Fl
         } else {
           bf[j] = g2::dequant4(bw[j][dd], m0k, m1k, mag, s16, zc0, zc1);
         }
+        if constexpr (FOLD) {
+          const h8_t s8 = {fsc[j][0], fsc[j][0], fsc[j][0], fsc[j][0], fsc[j][0], fsc[j][0], fsc[j][0], fsc[j][0]};
+          bf[j] = bf[j] * s8;
+        }
       }
 #pragma unroll
       for (int i = 0; i < 8; i++) {
         const h8_t af = dd == 0 ? af0[i] : af1[i];
 #pragma unroll
         for (int j = 0; j < 2; j++) {
-          if (dd == 0 && gstart)
+          if constexpr (FOLD)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, bf[j], acc[i][j], 0, 0, 0);
+          else if (dd == 0 && gstart)
             accg[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, bf[j], zero, 0, 0, 0);
           else
             accg[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, bf[j], accg[i][j], 0, 0, 0);
         }
       }
     }
-    if (gend) {
+    if (!FOLD && gend) {
       if constexpr (!L) {
         sw0 = lds_b32<0>(bl + soff);
         sw1 = lds_b32<64>(bl + soff);
@@ -649,8 +686,8 @@ hipError_t launch_gemm3(const GemmArgs& a, const _Float16* A16, int lda16, hipSt
   const int nbm = (a.M + g3::BM - 1) / g3::BM, nbn = (a.w.ns + 7) / 8;
   const bool tpg1 = a.w.bs == g3::KT;
   auto go = [&](auto k) -> hipError_t {
-    static bool attr[2][2] = {};  // opt in to 155 KiB of dynamic LDS once per instantiation
-    bool& done = attr[a.w.zps != nullptr][a.w.bs == g3::KT];
+    static bool attr[2][2][2] = {};  // opt in to 155 KiB of dynamic LDS once per instantiation
+    bool& done = attr[a.w.zps != nullptr][a.w.bs == g3::KT][a.fold ? 1 : 0];
     if (!done) {
       hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
                                          g3::LDS_BYTES);
@@ -661,8 +698,12 @@ hipError_t launch_gemm3(const GemmArgs& a, const _Float16* A16, int lda16, hipSt
     return hipGetLastError();
   };
   const bool asym = a.w.zps != nullptr;
-  if (asym) return tpg1 ? go(g3::woq_gemm3_kernel<true, true>) : go(g3::woq_gemm3_kernel<true, false>);
-  return tpg1 ? go(g3::woq_gemm3_kernel<false, true>) : go(g3::woq_gemm3_kernel<false, false>);
+  if (a.fold) {
+    if (asym) return tpg1 ? go(g3::woq_gemm3_kernel<true, true, true>) : go(g3::woq_gemm3_kernel<true, false, true>);
+    return tpg1 ? go(g3::woq_gemm3_kernel<false, true, true>) : go(g3::woq_gemm3_kernel<false, false, true>);
+  }
+  if (asym) return tpg1 ? go(g3::woq_gemm3_kernel<true, true, false>) : go(g3::woq_gemm3_kernel<true, false, false>);
+  return tpg1 ? go(g3::woq_gemm3_kernel<false, true, false>) : go(g3::woq_gemm3_kernel<false, false, false>);
 }
 
 hipError_t launch_cvt_act(const void* A, int act_t, int lda, int M, int K, int Kp, const int32_t* shuffle,

@@ -57,6 +57,8 @@ struct DeviceWeight {
                       // 3 F8_E4M3, 4 F8_E5M2 (raw codes in the int8 layout); -1 = integer
   int32_t compute;    // per-weight arithmetic (nad_device_set_compute): 0 follow the thread / process mode, 1 fp,
                       // 2 int8 (integer-core blobs and Q4_0 only)
+  int32_t fold_ok;    // every (q - zp) * scale of the weight is 0 or an fp16 normal: the prefill GEMMs may fold the
+                      // group scale into the fp16 B fragment (checked at load)
 };
 
 // Tile (s, t) and scale row (s, g) positions.  K-major interleaves the stripes at every K position, so the waves of a
@@ -97,6 +99,7 @@ inline uint64_t layout_geometry(DeviceWeight& w, int bits, int n, int k, int blo
   w.blob_bs = blocksize;
   w.f4kind = -1;
   w.compute = 0;
+  w.fold_ok = 0;
   uint64_t rbytes = uint64_t(w.ng) * w.red_ld * 2;
   return align256(tiles) + align256(sbytes) + align256(zbytes) + align256(shf) + align256(rbytes);
 }

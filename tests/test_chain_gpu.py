@@ -1,9 +1,14 @@
-"""The persistent decode chain (woq_chain.hip, nad_chain_*): a sequence of decode GEMV ops in one launch.
+"""The decode weight-stream engine (woq_chain.hip, nad_chain_*): M = 1 WOQ matmuls of a decode segment in one
+persistent launch, weights streamed by an LDS-DMA loader wave, results handed between ops as tagged granules.
 
-Parity bar: every op of the chain runs the same tiles, dequant, MFMA and reduction order as the single-op stripe
-stream (woq_gemv.hip), so chain outputs must be BIT-identical to the same ops launched one by one; the single-op path
-itself is pinned against the oracle by test_gpu_parity.py.  The RMSNorm staging option is checked against a torch
-fp32 reference of the same formula (x / sqrt(mean(x^2) + eps) * g) within 1e-5 relative.
+Parity bars:
+  * every op of a launch computes exactly what a ONE-op launch of the same op computes (same tiles per consumer, same
+    reduction order, same RMSNorm order): chain outputs are BIT-identical to the ops launched one by one, whether the
+    launch is a whole token or cut at the attention nodes (the form the reference graph can dispatch);
+  * against the oracle (fp64 GEMM on the reference's dequantized weights): 2e-5 of max|ref| per op (fp32 activations
+    split into fp16 hi + lo, fp32 accumulation) -- the same bar as the single-op decode kernels;
+  * against the per-op decode kernel (woq_gemv.hip): 1e-6 (only the order of the fp32 partial sums differs);
+  * RMSNorm staging against a torch fp32 reference of x / sqrt(mean(x^2) + eps) * g: 1e-5.
 """
 import numpy as np
 import pytest
@@ -12,132 +17,207 @@ torch = pytest.importorskip("torch")
 
 pytestmark = pytest.mark.gpu
 
-
-@pytest.fixture(autouse=True)
-def _four_tile_slices(monkeypatch):
-    # the chain streams 4-tile K-slices; the per-op M = 1 launch takes 2-tile slices at K <= 16 tiles (a different
-    # summation order), so the bit-identity reference runs the per-op launches with 4-tile slices
-    monkeypatch.setenv("NAD_GEMV_KS", "4")
-
 from neural_amd import bestla  # noqa: E402
 from neural_amd.bestla import CHAIN_GATE_UP, CHAIN_LINEAR, CHAIN_QKV, EPI_RES_ADD  # noqa: E402
+from tests.oracle_lib import F16, S4  # noqa: E402
+from tests.test_gpu_parity import _rel_err  # noqa: E402
 
 
-def _w(n, k, seed, asym=False, stype="fp16", bs=128):
-    return bestla.DeviceWeight.synthetic(4, n, k, bs, stype, asym, seed=seed)
+def _w(n, k, seed, asym=False, stype="fp16", bs=128, bits=4):
+    return bestla.DeviceWeight.synthetic(bits, n, k, bs, stype, asym, seed=seed)
 
 
-def _layer_weights(hid, ffn, seed, asym=False):
-    return dict(wq=_w(hid, hid, seed + 1, asym), wk=_w(hid, hid, seed + 2, asym), wv=_w(hid, hid, seed + 3, asym),
-                wo=_w(hid, hid, seed + 4, asym), w1=_w(ffn, hid, seed + 5, asym), w3=_w(ffn, hid, seed + 6, asym),
-                w2=_w(hid, ffn, seed + 7, asym))
+def _layer_weights(hid, ffn, seed, asym=False, bits=4, bs=128):
+    mk = lambda n, k, s: _w(n, k, seed + s, asym, bs=bs, bits=bits)  # noqa: E731
+    return dict(wq=mk(hid, hid, 1), wk=mk(hid, hid, 2), wv=mk(hid, hid, 3), wo=mk(hid, hid, 4), w1=mk(ffn, hid, 5),
+                w3=mk(ffn, hid, 6), w2=mk(hid, ffn, 7))
 
 
-def _build(layers, hid, ffn, m, vocab_w, norm, scale=1.0):
-    dev = "cuda"
-    f = dict(dtype=torch.float32, device=dev)
-    xs = [torch.empty((m, hid), **f) for _ in range(2)]
-    g = torch.Generator(device="cpu").manual_seed(5)
-    xs[0].copy_((torch.rand((m, hid), generator=g) - 0.5) * scale)
-    q, k, v = (torch.empty((m, hid), **f) for _ in range(3))
-    h = torch.empty((m, hid), **f)
-    t = torch.empty((m, ffn), **f)
-    logits = torch.empty((m, vocab_w.n), **f)
-    ops = []
-    for li, L in enumerate(layers):
-        x, xn = xs[li % 2], xs[(li + 1) % 2]
-        ops.append(dict(kind=CHAIN_QKV, w=[L["wq"], L["wk"], L["wv"]], act=x, out=[q, k, v], norm=norm))
-        ops.append(dict(kind=CHAIN_LINEAR, w=[L["wo"]], act=v, out=[h], epi=EPI_RES_ADD, res=x))
-        ops.append(dict(kind=CHAIN_GATE_UP, w=[L["w1"], L["w3"]], act=h, out=[t], norm=norm))
-        ops.append(dict(kind=CHAIN_LINEAR, w=[L["w2"]], act=t, out=[xn], epi=EPI_RES_ADD, res=h))
-    ops.append(dict(kind=CHAIN_LINEAR, w=[vocab_w], act=xs[len(layers) % 2], out=[logits], norm=norm))
-    return ops, xs, (q, k, v, h, t, logits)
+class Stack:
+    """Buffers + the op list of L decoder layers and the lm_head tail (llama.cpp op order):
+    x -> RMSNorm -> QKV -> (attention: here V, exact for a single-token context) -> O + x -> RMSNorm -> gate/up
+    SiLU*mul -> down + h -> next layer ... -> RMSNorm -> lm_head."""
+
+    def __init__(self, layers, hid, ffn, lm, scale=1.0, norm_w=False):
+        f = dict(dtype=torch.float32, device="cuda")
+        g = torch.Generator(device="cpu").manual_seed(5)
+        self.x0 = ((torch.rand((1, hid), generator=g) - 0.5) * scale).cuda()
+        L = len(layers)
+        self.xs = [torch.empty((1, hid), **f) for _ in range(L + 1)]
+        self.q, self.k, self.v = ([torch.empty((1, hid), **f) for _ in range(L)] for _ in range(3))
+        self.h = [torch.empty((1, hid), **f) for _ in range(L)]
+        self.t = [torch.empty((1, ffn), **f) for _ in range(L)]
+        self.logits = torch.empty((1, lm.n), **f)
+        self.gw = [(torch.rand(hid, generator=g) + 0.5).cuda() if norm_w else None for _ in range(2 * L + 1)]
+        self.layers, self.lm = layers, lm
+
+    def ops(self):
+        """(ops, boundaries): the whole token, and the indices where the reference graph cuts it (attention)."""
+        ops, cuts = [], [1]
+        for li, Lw in enumerate(self.layers):
+            x = self.xs[li]
+            ops.append(dict(kind=CHAIN_QKV, w=[Lw["wq"], Lw["wk"], Lw["wv"]], act=x,
+                            out=[self.q[li], self.k[li], self.v[li]], norm=True, norm_w=self.gw[2 * li]))
+            ops.append(dict(kind=CHAIN_LINEAR, w=[Lw["wo"]], act=self.v[li], out=[self.h[li]], epi=EPI_RES_ADD, res=x))
+            ops.append(dict(kind=CHAIN_GATE_UP, w=[Lw["w1"], Lw["w3"]], act=self.h[li], out=[self.t[li]], norm=True,
+                            norm_w=self.gw[2 * li + 1]))
+            ops.append(dict(kind=CHAIN_LINEAR, w=[Lw["w2"]], act=self.t[li], out=[self.xs[li + 1]], epi=EPI_RES_ADD,
+                            res=self.h[li]))
+            cuts.append(len(ops) + 1)   # next cut: after the next layer's QKV
+        ops.append(dict(kind=CHAIN_LINEAR, w=[self.lm], act=self.xs[-1], out=[self.logits], norm=True,
+                        norm_w=self.gw[-1]))
+        cuts[-1] = len(ops)
+        return ops, cuts
+
+    def results(self):
+        return [t.clone() for t in self.xs + self.q + self.k + self.v + self.h + self.t + [self.logits]]
+
+    def reset(self):
+        for t in self.xs + self.q + self.k + self.v + self.h + self.t + [self.logits]:
+            t.fill_(float("nan"))
+        self.xs[0].copy_(self.x0)
 
 
-def _per_op(ops):
-    """The same ops, one launch each (the single-op stripe stream)."""
-    for o in ops:
-        if o["kind"] == CHAIN_QKV:
-            q, k, v = bestla.qkv_forward(o["act"], *o["w"])
-            for dst, src in zip(o["out"], (q, k, v)):
-                dst.copy_(src)
-        elif o["kind"] == CHAIN_GATE_UP:
-            w1, w3 = o["w"]
-            tmp1 = torch.empty_like(o["out"][0])
-            rc = bestla.lib().nad_device_ffn_gate_up(o["act"].data_ptr(), 0, w1.desc, w3.desc, tmp1.data_ptr(),
-                                                      o["out"][0].data_ptr(), o["act"].shape[0], w1.k, w1.n,
-                                                      o["act"].stride(0), bestla.EPI_SILU_MUL,
-                                                      torch.cuda.current_stream().cuda_stream)
-            assert rc == 0, bestla.last_error()
-        else:
-            o["w"][0].forward(o["act"], out=o["out"][0], epilogue=o.get("epi", 0), residual=o.get("res"))
+def _run_chains(chains):
+    for c in chains:
+        c.run()
+    torch.cuda.synchronize()
+    for c in chains:
+        assert c.status() == 0
 
 
-@pytest.mark.parametrize("m", [1, 2])
+def _same(a, b):
+    assert len(a) == len(b)
+    for i, (x, y) in enumerate(zip(a, b)):
+        assert torch.isfinite(y).all(), i
+        assert torch.equal(x, y), (i, (x - y).abs().max().item())
+
+
 @pytest.mark.parametrize("asym", [False, True])
-def test_chain_bit_identical_to_per_op(m, asym):
-    hid, ffn = 1024, 2816  # ffn: 22 K tiles -> 6 slices over 6 waves, as Llama's 86 -> 22 over 11
-    layers = [_layer_weights(hid, ffn, 100 * i, asym) for i in range(2)]
-    lm = _w(1000, hid, 999, asym)
-    # small input: without norms the random stack grows ~6x per matmul and must stay inside fp16 staging range
-    ops, xs, bufs = _build(layers, hid, ffn, m, lm, norm=False, scale=0.01)
-    x0 = xs[0].clone()
-    chain = bestla.Chain(ops, m)
-    chain.run()
-    torch.cuda.synchronize()
-    assert chain.status() == 0
-    got = [b.clone() for b in bufs] + [x.clone() for x in xs]
-    xs[0].copy_(x0)
-    _per_op(ops)
-    torch.cuda.synchronize()
-    ref = list(bufs) + list(xs)
-    for a, b in zip(got, ref):
-        assert torch.isfinite(b).all()
-        assert torch.equal(a, b), (a - b).abs().max().item()
+def test_chain_bit_identical_to_one_op_launches_and_cut_segments(asym):
+    hid, ffn = 1024, 2816   # ffn: 22 K tiles -> two fills per stripe, the second ragged
+    st = Stack([_layer_weights(hid, ffn, 100 * i, asym) for i in range(2)], hid, ffn, _w(1000, hid, 999, asym),
+               norm_w=True)
+    ops, cuts = st.ops()
+    st.reset()
+    _run_chains([bestla.Chain(ops, 1)])                         # the whole token: one launch
+    whole = st.results()
+    st.reset()
+    _run_chains([bestla.Chain([o], 1) for o in ops])            # one launch per op
+    _same(whole, st.results())
+    st.reset()
+    bounds = [0] + cuts
+    _run_chains([bestla.Chain(ops[a:b], 1) for a, b in zip(bounds, bounds[1:])])   # cut at attention
+    _same(whole, st.results())
 
 
-def test_chain_llama_shapes_and_replay():
-    """One Llama-2-7B layer + lm_head: bit-identical to per-op launches, repeatable, graph-capturable."""
+def _per_op_kernels(st):
+    """the same math through the per-op decode kernels (woq_gemv.hip) + torch for RMSNorm (fp32)"""
+    def norm(x, g):
+        y = x / torch.sqrt((x * x).mean(dim=1, keepdim=True) + 1e-5)
+        return y * g if g is not None else y
+    outs = {}
+    for li, Lw in enumerate(st.layers):
+        x = st.xs[li]
+        q, k, v = bestla.qkv_forward(norm(x, st.gw[2 * li]), Lw["wq"], Lw["wk"], Lw["wv"])
+        h = Lw["wo"].forward(st.v[li], epilogue=EPI_RES_ADD, residual=x)
+        t = bestla.ffn_gate_up(norm(st.h[li], st.gw[2 * li + 1]), Lw["w1"], Lw["w3"])
+        xn = Lw["w2"].forward(st.t[li], epilogue=EPI_RES_ADD, residual=st.h[li])
+        outs[li] = (q, k, v, h, t, xn)
+    logits = st.lm.forward(norm(st.xs[-1], st.gw[-1]))
+    return outs, logits
+
+
+def test_chain_matches_per_op_kernels():
+    hid, ffn = 2048, 5632
+    st = Stack([_layer_weights(hid, ffn, 7)], hid, ffn, _w(4000, hid, 77), norm_w=True)
+    ops, _ = st.ops()
+    st.reset()
+    _run_chains([bestla.Chain(ops, 1)])
+    outs, logits = _per_op_kernels(st)   # each op fed the chain's own inputs
+    q, k, v, h, t, xn = outs[0]
+    for got, ref in ((st.q[0], q), (st.k[0], k), (st.v[0], v), (st.h[0], h), (st.t[0], t), (st.xs[1], xn),
+                     (st.logits, logits)):
+        err = ((got - ref).abs().max() / ref.abs().max()).item()
+        assert err <= 1e-6, err
+
+
+def test_chain_matches_oracle(oracle):
+    """Weights packed by the oracle (the reference's blob format), each op of a launch against the oracle's fp64
+    forward on that op's actual input: 2e-5."""
+    hid, ffn = 1024, 2816
+    rng = np.random.default_rng(3)
+
+    def blob(n, k):
+        q = rng.integers(-8, 8, size=(k, n), dtype=np.int8)
+        s = rng.uniform(0.001, 0.005, size=(k // 128, n)).astype(np.float32)
+        return oracle.pack_q(q, s, None, n, k, 128, S4, F16, False, oracle.lib.orc_select_core(4, S4, 128, 0, 0))
+    names = [("wq", hid, hid), ("wk", hid, hid), ("wv", hid, hid), ("wo", hid, hid), ("w1", ffn, hid),
+             ("w3", ffn, hid), ("w2", hid, ffn)]
+    blobs = {nm: (blob(n, k), n, k) for nm, n, k in names}
+    layer = {nm: bestla.DeviceWeight(b[0]) for nm, b in blobs.items()}
+    lmb = blob(512, hid)
+    st = Stack([layer], hid, ffn, bestla.DeviceWeight(lmb))
+    ops, _ = st.ops()
+    st.reset()
+    _run_chains([bestla.Chain(ops, 1)])
+
+    def rms(x):
+        x = x.astype(np.float64)
+        return (x / np.sqrt((x * x).mean() + 1e-5)).astype(np.float32)
+    f = lambda nm, a: oracle.forward(a, blobs[nm][0], blobs[nm][1], blobs[nm][2])  # noqa: E731
+    x0 = st.xs[0].cpu().numpy()
+    xn = rms(x0)
+    for got, nm in ((st.q[0], "wq"), (st.k[0], "wk"), (st.v[0], "wv")):
+        assert _rel_err(got.cpu().numpy(), f(nm, xn)) <= 2e-5, nm
+    h_ref = f("wo", st.v[0].cpu().numpy()) + x0
+    assert _rel_err(st.h[0].cpu().numpy(), h_ref) <= 2e-5
+    hn = rms(st.h[0].cpu().numpy())
+    g, u = f("w1", hn).astype(np.float64), f("w3", hn).astype(np.float64)
+    assert _rel_err(st.t[0].cpu().numpy(), g / (1 + np.exp(-g)) * u) <= 1e-4
+    x1_ref = f("w2", st.t[0].cpu().numpy()) + st.h[0].cpu().numpy()
+    assert _rel_err(st.xs[1].cpu().numpy(), x1_ref) <= 2e-5
+    lg = oracle.forward(rms(st.xs[1].cpu().numpy()), lmb, 512, hid)
+    assert _rel_err(st.logits.cpu().numpy(), lg) <= 2e-5
+
+
+def test_chain_llama_shapes_graph_replay():
+    """One Llama-2-7B layer + lm_head as the bench's cut launches ([QKV] [O, gate/up, down, lm_head]): bit-identical to
+    the whole-token launch, and every graph replay reproduces it exactly (the launch generation moves on, stale
+    granules of the previous replay never match)."""
     hid, ffn = 4096, 11008
-    layers = [_layer_weights(hid, ffn, 7)]
-    lm = _w(32000, hid, 77)
-    ops, xs, bufs = _build(layers, hid, ffn, 1, lm, norm=False)
-    x0 = xs[0].clone()
-    chain = bestla.Chain(ops, 1)
-    chain.run()
-    torch.cuda.synchronize()
-    got = [b.clone() for b in bufs]
-    xs[0].copy_(x0)
-    _per_op(ops)
-    torch.cuda.synchronize()
-    for a, b in zip(got, bufs):
-        assert torch.equal(a, b)
-    # graph replay of the single launch reproduces the first run exactly
+    st = Stack([_layer_weights(hid, ffn, 7)], hid, ffn, _w(32000, hid, 77))
+    ops, cuts = st.ops()
+    st.reset()
+    _run_chains([bestla.Chain(ops, 1)])
+    whole = st.results()
+    bounds = [0] + cuts
+    chains = [bestla.Chain(ops[a:b], 1) for a, b in zip(bounds, bounds[1:])]
     s = torch.cuda.Stream()
     s.wait_stream(torch.cuda.current_stream())
     g = torch.cuda.CUDAGraph()
     with torch.cuda.stream(s):
-        xs[0].copy_(x0)
+        st.reset()
         with torch.cuda.graph(g, stream=s):
-            chain.run(stream=s)
+            for c in chains:
+                c.run(stream=s)
     torch.cuda.current_stream().wait_stream(s)
     for _ in range(3):
-        xs[0].copy_(x0)
+        st.reset()
         g.replay()
         torch.cuda.synchronize()
-        for a, b in zip(got, bufs):
-            assert torch.equal(a, b)
-    assert chain.status() == 0
+        _same(whole, st.results())
+    for c in chains:
+        assert c.status() == 0
 
 
 def test_chain_rmsnorm_staging():
-    hid, ffn = 2048, 1024
+    hid = 2048
     w = _w(512, hid, 3)
-    m = 2
-    x = (torch.rand((m, hid), device="cuda") - 0.5) * 3
+    x = (torch.rand((1, hid), device="cuda") - 0.5) * 3
     gw = torch.rand(hid, device="cuda") + 0.5
-    out = torch.empty((m, 512), device="cuda")
-    chain = bestla.Chain([dict(kind=CHAIN_LINEAR, w=[w], act=x, out=[out], norm=True, norm_eps=1e-5, norm_w=gw)], m)
+    out = torch.empty((1, 512), device="cuda")
+    chain = bestla.Chain([dict(kind=CHAIN_LINEAR, w=[w], act=x, out=[out], norm=True, norm_eps=1e-5, norm_w=gw)], 1)
     chain.run()
     xn = x / torch.sqrt((x.double() ** 2).mean(dim=1, keepdim=True) + 1e-5).float() * gw
     ref = w.forward(xn)
@@ -146,9 +226,29 @@ def test_chain_rmsnorm_staging():
     assert err <= 1e-5, err
 
 
+def test_chain_int2_stack():
+    """int2 weights (KT = 256, two groups of 64 per... one group of 128 per tile here) through the same engine."""
+    hid, ffn = 1024, 2048
+    st = Stack([_layer_weights(hid, ffn, 11, bits=2, bs=128)], hid, ffn, _w(1024, hid, 12, bits=2), norm_w=True)
+    ops, _ = st.ops()
+    st.reset()
+    _run_chains([bestla.Chain(ops, 1)])
+    whole = st.results()
+    st.reset()
+    _run_chains([bestla.Chain([o], 1) for o in ops])
+    _same(whole, st.results())
+    outs, logits = _per_op_kernels(st)
+    err = ((st.logits - logits).abs().max() / logits.abs().max()).item()
+    assert err <= 1e-6, err
+
+
 def test_chain_rejects_ineligible():
     w8 = bestla.DeviceWeight.synthetic(8, 128, 256, 64, "fp16", False, seed=1)
     x = torch.zeros((1, 256), device="cuda")
     out = torch.empty((1, 128), device="cuda")
     with pytest.raises(RuntimeError, match="nad_chain_create"):
         bestla.Chain([dict(kind=CHAIN_LINEAR, w=[w8], act=x, out=[out])], 1)
+    w4 = _w(128, 256, 2)
+    with pytest.raises(RuntimeError, match="m = 1"):
+        bestla.Chain([dict(kind=CHAIN_LINEAR, w=[w4], act=torch.zeros((2, 256), device="cuda"),
+                           out=[torch.empty((2, 128), device="cuda")])], 2)
