@@ -422,6 +422,7 @@ class Chain:
             self._keep.extend(t for t in [x, *o["out"], o.get("res"), o.get("aux"), o.get("bias"), o.get("norm_w")]
                               if t is not None)
         self._ops = arr
+        self.n_ops = len(ops)
         h = lib().nad_chain_create(C.cast(arr, C.c_void_p), len(ops), m)
         if not h:
             raise RuntimeError(f"nad_chain_create failed: {last_error()}")

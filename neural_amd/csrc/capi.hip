@@ -967,7 +967,8 @@ static int run_gemm(const void* act, int act_t, int lda, int m, int k, const Dev
   a.ld_aux = ld_aux;
   a.prio = env_int("NAD_GEMM3_PRIO", 0);
   a.stagger = env_int("NAD_GEMM3_STAGGER", 1);  // measured +3-7 % (profiles/r02_gemm3_stagger.txt)
-  a.fold = w.fold_ok && env_int("NAD_GEMM_FOLD", 1) ? 1 : 0;
+  // scale folding measured 1-5 % SLOWER on gemm3 (profiles/r03_gemm3_fold.txt) and it rounds q * s to fp16: opt-in
+  a.fold = w.fold_ok && env_int("NAD_GEMM_FOLD", 0) ? 1 : 0;
   a.w = view(w, out, ldo, bias, bias_ld);
   const int pg = pipelined_gemm(w, m);
   if (h16) {
@@ -1375,9 +1376,11 @@ extern "C" void* nad_chain_create(const nad_chain_op* ops, int n_ops, int m) {
     kp = std::max(kp, w0.nt * KT);
     // scale (+ zero point) bytes of one fill of 16 tiles
     const int ssz = w0.scale_t == kScaleF32 ? 4 : 2;
-    const size_t groups = gpt == 1 ? size_t((16 + std::max(tpg, 1) - 1) / std::max(tpg, 1) + 1) : size_t(16) * gpt;
+    const size_t groups = gpt == 1 ? size_t((kEngFillTiles + std::max(tpg, 1) - 1) / std::max(tpg, 1) + 1)
+                                   : size_t(kEngFillTiles) * gpt;
     sd_bytes = std::max(sd_bytes, std::min(groups, size_t(w0.ng)) * 16 * ssz);
   }
+  g.thin = env_int("NAD_ENGINE_THIN", 0);  // measured slower on every edge (trace_chain.py): off
   g.sd = int((sd_bytes + 1023) / 1024);
   if (g.sd < 1) g.sd = 1;
   if (g.sd > 2 || !engine_geometry(g, kp)) {

@@ -42,11 +42,12 @@ struct EngOp {
   unsigned tag;                 // this op's index in the launch + 1
 };
 
-// Engine geometry: 8 consumer waves + 1 loader wave, fills of 16 tiles, 3 fills in flight
+// Engine geometry: 8 consumer waves + 1 loader wave, fills of 16 tiles (two per consumer), as many fills in flight as
+// the 6-bit vmcnt can count (63 DMA instructions: 3 fills of 16 tiles + their scale pieces).  Measured (trace_chain.py,
+// DESIGN.md section 4): 8-tile fills with 7 in flight stream SLOWER (the loader's per-fill LDS round trips dominate).
 constexpr int kEngConsumers = 8;
 constexpr int kEngThreads = (kEngConsumers + 1) * 64;
 constexpr int kEngFillTiles = 16;
-constexpr int kEngInflight = 3;
 constexpr int kEngMaxStripes = 16;   // virtual stripes of one op per workgroup (partial-sum slots)
 constexpr int kEngMaxK = 16384;      // input length (gather registers)
 
@@ -56,6 +57,7 @@ struct EngGeometry {
   int kp;                       // activation row length (max over ops of nt * KT)
   size_t lds;                   // dynamic LDS bytes
   size_t slot_bytes;
+  int thin;                     // thin the loader to one fill in flight while the consumers gather (NAD_ENGINE_THIN)
 };
 
 // fills g.kp/slots/lds from g.bits/gpt/asym/sd and the ops' largest padded K; false if the ring does not fit

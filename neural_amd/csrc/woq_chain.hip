@@ -49,16 +49,31 @@
 namespace nad {
 namespace eng {
 
+// Development instrumentation (make chaintrace): per-(op, workgroup) wall-clock stamps of the engine's phases.
+#ifdef NAD_CHAIN_TRACE
+constexpr int kTrOps = 160, kTrWg = 256, kTrSlots = 14;
+__device__ unsigned long long nad_chain_trace[kTrSlots][kTrOps][kTrWg];
+#define ETRACE(slot, opi, val)                                                                     \
+  do {                                                                                             \
+    if (lane == 0 && (opi) < kTrOps && blockIdx.x < kTrWg) nad_chain_trace[slot][opi][blockIdx.x] = (val); \
+  } while (0)
+#else
+#define ETRACE(slot, opi, val) \
+  do {                         \
+  } while (0)
+#endif
+
 constexpr int NC = kEngConsumers;
 constexpr int FT = kEngFillTiles;
-constexpr int D = kEngInflight;
+constexpr int TPC = FT / NC;  // tiles per consumer per fill
+static_assert(FT % NC == 0, "every consumer takes the same number of tiles of a fill");
 constexpr int PJ = 8;                       // granule pairs per consumer lane per gather pass
 constexpr int kOOB = 0x7FFF0000;            // buffer offset past every resource: no memory access, returns 0
 constexpr int kSC1 = 16;                    // buffer-load aux: sc1 (bypass this CU's L1)
 constexpr int kNT = 2;                      // buffer-load aux: non-temporal (weights, read once per token)
 constexpr unsigned kSpinMax = 1u << 24;     // ~1 s of s_sleep(1) polls
-// LDS control words (u32 index): FULL[8], FREE[8], consumer barrier, RMS partial sums[8]
-constexpr int kFull = 0, kFree = 8, kBar = 16, kNsum = 20, kCtlBytes = 128;
+// LDS control words (u32 index): FULL[16], FREE[16], consumer barrier, RMS partial sums[8], gather phase
+constexpr int kFull = 0, kFree = 16, kBar = 32, kNsum = 36, kPhase = 44, kCtlBytes = 192;
 constexpr int kPartBytes = kEngMaxStripes * NC * 16 * 4;
 
 typedef __attribute__((address_space(3))) void lds_void_t;
@@ -88,6 +103,13 @@ __device__ __forceinline__ void wait_vm() {
 }
 __device__ __forceinline__ void give_up(unsigned* ctl, unsigned code) {
   __hip_atomic_store(ctl + 1, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// per-lane selection among an op's (at most 3) weights from uniform (scalar) loads of all of them -- indexing o.w[]
+// with a lane-varying index would turn every field access into a vector load with full memory latency
+template <class T>
+__device__ __forceinline__ T sel3(int w, T x0, T x1, T x2) {
+  return w == 0 ? x0 : (w == 1 ? x1 : x2);
 }
 
 // virtual stripe -> (weight, stripe within it)
@@ -123,8 +145,9 @@ __device__ __forceinline__ void fill_groups(const EngOp& o, int t0, int& g0, int
 // ------------------------------------------------------------------------------------------------ loader
 template <int GPT, bool ASYM, int SD>
 __device__ void loader(const EngOp* ops, int n_ops, char* ring, int S, int slot_bytes, uint32_t ctl_a, unsigned* ctl,
-                       int lane) {
+                       int lane, int thin) {
   constexpr int IPF = FT + SD + (ASYM ? 1 : 0);  // DMA instructions per fill: constant, so vmcnt counts are exact
+  constexpr int D = 63 / IPF;                     // fills in flight: as many as vmcnt (6 bits) can count
   const uint32_t full_a = ctl_a + kFull * 4, free_a = ctl_a + kFree * 4;
   int f = 0, fpub = 0, slot = 0, pslot = 0;
   unsigned round = 0;
@@ -140,6 +163,9 @@ __device__ void loader(const EngOp* ops, int n_ops, char* ring, int S, int slot_
     const int ssz = o.scale_t == kScaleF32 ? 4 : 2;
     int v0, nv;
     unit_range(o, blockIdx.x, v0, nv);
+#ifdef NAD_CHAIN_TRACE
+    unsigned long long tr_wait = 0;
+#endif
     for (int jl = 0; jl < nv; jl++) {
       int wsel, s;
       vstripe(o, v0 + jl, wsel, s);
@@ -156,6 +182,9 @@ __device__ void loader(const EngOp* ops, int n_ops, char* ring, int S, int slot_
         if (round > 0) {  // this slot's previous fill must have been released by every consumer
           const unsigned need = NC * round;
           if (lds_ld(free_a + slot * 4) < need) {
+#ifdef NAD_CHAIN_TRACE
+            const unsigned long long tw0 = wall_clock64();
+#endif
             wait_vm<0>();  // about to wait anyway: publish everything in flight first
             while (fpub < f) publish_one();
             unsigned spins = 0;
@@ -166,7 +195,19 @@ __device__ void loader(const EngOp* ops, int n_ops, char* ring, int S, int slot_
                 failed = true;
               }
             }
+#ifdef NAD_CHAIN_TRACE
+            tr_wait += wall_clock64() - tw0;
+#endif
           }
+        }
+#ifdef NAD_CHAIN_TRACE
+        if (jl == 0 && c == 0) ETRACE(6, op, wall_clock64());
+#endif
+        // while the consumers gather an input, keep one fill in flight: their loads queue behind this wave's DMAs
+        // (MI355X_MICROARCH.md gather-pass: 0.3-0.65 us with the own DMA quiet vs 1.0-1.7 behind a refill burst)
+        if (thin && lds_ld(ctl_a + kPhase * 4) != 0u) {
+          wait_vm<0>();
+          while (fpub < f) publish_one();
         }
         char* sb = ring + slot * slot_bytes;
         const int t0 = c * FT;
@@ -195,6 +236,10 @@ __device__ void loader(const EngOp* ops, int n_ops, char* ring, int S, int slot_
         }
       }
     }
+    ETRACE(7, op, wall_clock64());
+#ifdef NAD_CHAIN_TRACE
+    ETRACE(8, op, tr_wait);
+#endif
   }
   wait_vm<0>();
   while (fpub < f) publish_one();
@@ -254,7 +299,7 @@ __device__ __forceinline__ void cbar(uint32_t a, unsigned& epoch, unsigned* ctl,
 template <int BITS, int GPT, bool ASYM, int SD>
 __global__ __launch_bounds__(kEngThreads, 1) void woq_engine_kernel(const EngOp* __restrict__ ops, int n_ops,
                                                                     unsigned* ctl, int S, int slot_bytes, int Kp,
-                                                                    int bump) {
+                                                                    int bump, int thin) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int KT = BITS == 4 ? 128 : 256, SPT = KT / 32, SPG = SPT / GPT, BIAS = BITS == 4 ? 8 : 2;
   const int lane = threadIdx.x & 63;
@@ -263,10 +308,10 @@ __global__ __launch_bounds__(kEngThreads, 1) void woq_engine_kernel(const EngOp*
   float* part = reinterpret_cast<float*>(smem + kCtlBytes);          // [stripe][consumer][16]
   char* act = smem + kCtlBytes + kPartBytes;                          // [Kp / 8] units of {hi[8], lo[8]} fp16
   char* ring = act + size_t(Kp) * 4;
-  if (threadIdx.x < 32) reinterpret_cast<unsigned*>(smem)[threadIdx.x] = 0u;
+  if (threadIdx.x < kCtlBytes / 4) reinterpret_cast<unsigned*>(smem)[threadIdx.x] = 0u;
   __syncthreads();
   if (wave == NC) {
-    loader<GPT, ASYM, SD>(ops, n_ops, ring, S, slot_bytes, ctl_a, ctl, lane);
+    loader<GPT, ASYM, SD>(ops, n_ops, ring, S, slot_bytes, ctl_a, ctl, lane, thin);
     return;
   }
 
@@ -282,29 +327,75 @@ __global__ __launch_bounds__(kEngThreads, 1) void woq_engine_kernel(const EngOp*
   const h2_t zc0 = splat(-(1024.f + BIAS)), zc1 = splat(-(64.f + BIAS));
   // this lane's A operand: MFMA rows 0-7 read hi, rows 8-15 lo (rows 0 and 8 are the result); k unit u = k / 8 at byte
   // 32 u (+16: lo), so step d of tile t starts at byte t * KT * 4 + d * 128 + kq * 32
-  const char* a_lane = act + (m >= 8 ? 16 : 0) + kq * 32;
+  const uint32_t a_lane = lds_addr(act) + (m >= 8 ? 16 : 0) + kq * 32;
+  const uint32_t ring_a = lds_addr(ring);
   int f = 0, slot = 0;
 
   for (int op = 0; op < n_ops; op++) {
     const EngOp& o = ops[op];
     const int K = o.K, nt = o.nt, Kpo = nt * KT, nch = (nt + FT - 1) / FT;
+    if (cw == 0) ETRACE(0, op, wall_clock64());
     const int st = o.scale_t, ssz = st == kScaleF32 ? 4 : 2;
+    int v0, nv;
+    unit_range(o, blockIdx.x, v0, nv);
+    const int vpu = o.dual ? 2 : 1;
+    const int nout = nv / vpu * 16;
 
-    // 1) the input vector -> LDS as fp32 (element i at byte 4i), then in place as MFMA-ready fp16 rows: 8-element
-    //    unit u (bytes 32u .. 32u + 31) becomes {hi[8u .. 8u + 7], lo[8u .. 8u + 7]}, so one lane converts a unit with
-    //    no hazard against other lanes
+    if (thin && cw == 0 && lane == 0) lds_st(ctl_a + kPhase * 4, 1u);  // gathering: loader thinned
+    // 0) this lane's residual (one output per lane at most: nout <= 256), issued now, used in the epilogue
+    float res_v = 0.f;
+    unsigned long long res_g = 0;
+    int my_n = -1;
+    {
+      const int oi = cl;
+      if (oi < nout && o.epi == kEpiResAdd) {
+        int wsel, sx;
+        vstripe(o, v0 + (oi >> 4) * vpu, wsel, sx);
+        const int n = sx * 16 + (oi & 15);
+        if (n < sel3(wsel, o.w[0].n, o.w[1].n, o.w[2].n)) {
+          my_n = n;
+          if (o.res_gran)
+            res_g = __hip_atomic_load(o.res_gran + n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          else
+            res_v = o.res[n];
+        }
+      }
+    }
+
+    // 1) the input vector straight into the MFMA-ready fp16 rows: element pair (2q, 2q + 1) of 8-element unit
+    //    u = q / 4 -> hi at byte 32 u + 4 (q & 3), lo 16 bytes further.  An RMSNorm of the input is applied as
+    //    x * g here and the scalar 1 / rms(x) on the results (y = W (x * g) / rms: the same products, no second pass)
     float s2 = 0.f;
     {
-      float* af32 = reinterpret_cast<float*>(act);
       const int npair = (K + 1) / 2;  // granule / element pairs: one 16-B (8-B external) load per pair
+      const bool gw = o.norm && o.norm_w;
+      float sq[PJ];  // per-slot squares, summed in slot order once the pass is complete (arrival order varies)
+      auto put = [&](int j, int q, float x0, float x1) {
+        // explicit fma: put() is inlined at two call sites, and hipcc's fp contraction may differ between them
+        sq[j] = __builtin_fmaf(x1, x1, x0 * x0);
+        if (gw) {
+          x0 *= o.norm_w[2 * q];
+          x1 *= 2 * q + 1 < K ? o.norm_w[2 * q + 1] : 0.f;
+        }
+        h2_t hi, lo;
+        hi[0] = _Float16(x0);
+        hi[1] = _Float16(x1);
+        lo[0] = _Float16(x0 - float(hi[0]));
+        lo[1] = _Float16(x1 - float(hi[1]));
+        char* pu = act + (q >> 2) * 32 + (q & 3) * 4;
+        *reinterpret_cast<h2_t*>(pu) = hi;
+        *reinterpret_cast<h2_t*>(pu + 16) = lo;
+      };
       if (o.act_gran) {
         const unsigned want = gen * 256u + o.act_tag;
         const auto rg = rsrc(o.act_gran, unsigned(K) * 8u);
         for (int q0 = 0; q0 < npair; q0 += NC * 64 * PJ) {
           uint32_t pend = 0;
 #pragma unroll
-          for (int j = 0; j < PJ; j++)
+          for (int j = 0; j < PJ; j++) {
+            sq[j] = 0.f;
             if (q0 + cl + NC * 64 * j < npair) pend |= 1u << j;
+          }
           unsigned spins = 0;
           while (true) {
             uint4 g[PJ];
@@ -319,12 +410,11 @@ __global__ __launch_bounds__(kEngThreads, 1) void woq_engine_kernel(const EngOp*
               // the pair's second granule is past K for odd K: its tag is never written, value 0
               const bool ok1 = 2 * q + 1 >= K || g[j].w == want;
               if (((pend >> j) & 1u) && g[j].y == want && ok1) {
-                const float x0 = __uint_as_float(g[j].x), x1 = 2 * q + 1 < K ? __uint_as_float(g[j].z) : 0.f;
-                *reinterpret_cast<float2*>(af32 + 2 * q) = make_float2(x0, x1);
-                s2 += x0 * x0 + x1 * x1;
+                put(j, q, __uint_as_float(g[j].x), 2 * q + 1 < K ? __uint_as_float(g[j].z) : 0.f);
                 pend &= ~(1u << j);
               }
             }
+            if (cw == 0 && spins == 0 && q0 == 0) ETRACE(11, op, wall_clock64());  // first pass returned
             if (__all(pend == 0u) || failed) break;
             __builtin_amdgcn_s_sleep(1);
             if (++spins > kSpinMax) {
@@ -332,6 +422,8 @@ __global__ __launch_bounds__(kEngThreads, 1) void woq_engine_kernel(const EngOp*
               failed = true;
             }
           }
+#pragma unroll
+          for (int j = 0; j < PJ; j++) s2 += sq[j];
         }
       } else {  // an external vector (written before this launch): plain loads, all of a pass in flight at once
         const auto ra = rsrc(o.act, unsigned(K) * 4u);
@@ -343,123 +435,171 @@ __global__ __launch_bounds__(kEngThreads, 1) void woq_engine_kernel(const EngOp*
             g[j] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(ra, q < npair ? q * 8 : kOOB, 0, 0));
           }
           __builtin_amdgcn_sched_barrier(0);
+          if (cw == 0 && q0 == 0) ETRACE(11, op, wall_clock64());
 #pragma unroll
           for (int j = 0; j < PJ; j++) {
             const int q = q0 + cl + NC * 64 * j;
-            if (q < npair) {
-              // odd K: the last pair's second element lies past the vector (its bytes are out of range: 0)
-              const float x0 = __uint_as_float(g[j].x), x1 = 2 * q + 1 < K ? __uint_as_float(g[j].y) : 0.f;
-              *reinterpret_cast<float2*>(af32 + 2 * q) = make_float2(x0, x1);
-              s2 += x0 * x0 + x1 * x1;
-            }
+            sq[j] = 0.f;
+            // odd K: the last pair's second element lies past the vector (its bytes are out of range: 0)
+            if (q < npair) put(j, q, __uint_as_float(g[j].x), 2 * q + 1 < K ? __uint_as_float(g[j].y) : 0.f);
           }
+#pragma unroll
+          for (int j = 0; j < PJ; j++) s2 += sq[j];
         }
       }
-      for (int i = 2 * npair + cl; i < Kpo; i += NC * 64) af32[i] = 0.f;  // K tail of the last tile
+      for (int q = npair + cl; q < Kpo / 2; q += NC * 64) {  // K tail of the last tile: zero rows
+        char* pu = act + (q >> 2) * 32 + (q & 3) * 4;
+        *reinterpret_cast<uint32_t*>(pu) = 0u;
+        *reinterpret_cast<uint32_t*>(pu + 16) = 0u;
+      }
     }
+    if (cw == 0) ETRACE(1, op, wall_clock64());
     if (o.norm) {
 #pragma unroll
       for (int sh = 32; sh > 0; sh >>= 1) s2 += __shfl_xor(s2, sh, 64);
       if (lane == 0) nsum[cw] = s2;
     }
     cbar(bar_a, bar_epoch, ctl, lane, failed);
-    {
-      float inv = 1.f;
-      if (o.norm) {  // RMSNorm: lane sums -> wave sums -> the same consumer-order total in every wave
-        float tot = 0.f;
+    if (thin && cw == 0 && lane == 0) lds_st(ctl_a + kPhase * 4, 0u);
+    if (cw == 0) ETRACE(2, op, wall_clock64());
+    // 1 / rms of the input, read right after the barrier: the next op's partial sums overwrite nsum as soon as a
+    // consumer has passed this op's post-loop barrier
+    float inv = 1.f;
+    if (o.norm) {
+      float tot = 0.f;
 #pragma unroll
-        for (int w = 0; w < NC; w++) tot += nsum[w];
-        inv = 1.f / sqrtf(tot / float(K) + o.norm_eps);
-      }
-      for (int u = cl; u < Kpo / 8; u += NC * 64) {
-        float4* pu = reinterpret_cast<float4*>(act + u * 32);
-        const float4 a0 = pu[0], a1 = pu[1];
-        float x[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-        if (o.norm) {
-          float gw[8];
-#pragma unroll
-          for (int e = 0; e < 8; e++) gw[e] = 1.f;
-          if (o.norm_w) {  // eight independent loads, one wait
-#pragma unroll
-            for (int e = 0; e < 8; e++) gw[e] = o.norm_w[min(8 * u + e, K - 1)];
-#pragma unroll
-            for (int e = 0; e < 8; e++) gw[e] = 8 * u + e < K ? gw[e] : 1.f;
-          }
-#pragma unroll
-          for (int e = 0; e < 8; e++) x[e] = x[e] * inv * gw[e];
-        }
-        h8_t hi, lo;
-#pragma unroll
-        for (int e = 0; e < 8; e++) {
-          hi[e] = _Float16(x[e]);
-          lo[e] = _Float16(x[e] - float(hi[e]));
-        }
-        reinterpret_cast<h8_t*>(pu)[0] = hi;
-        reinterpret_cast<h8_t*>(pu)[1] = lo;
-      }
+      for (int w = 0; w < NC; w++) tot += nsum[w];
+      inv = 1.f / sqrtf(tot / float(K) + o.norm_eps);
     }
-    cbar(bar_a, bar_epoch, ctl, lane, failed);
 
-    // 2) the weight stream: consumer cw takes tiles cw and cw + 8 of every fill
-    int v0, nv;
-    unit_range(o, blockIdx.x, v0, nv);
+    // 2) the weight stream: consumer cw takes tiles cw and cw + 8 of every fill.  One LDS round trip per fill: the FULL
+    //    word and every operand of both tiles are read together (a wave's LDS reads complete in order, and the loader
+    //    publishes FULL only after the fill landed, so operands read behind a FULL that says "landed" are that fill's);
+    //    the slot is released as soon as they are in registers, then two interleaved MFMA chains run.
+#ifdef NAD_CHAIN_TRACE
+    unsigned long long tr_fw = 0;
+#endif
+    const int gsh = st == kScaleF32 ? 0 : (m & 1) * 16;  // this lane's scale bits within the dword read
     for (int jl = 0; jl < nv; jl++) {
       f4_t acc = {0.f, 0.f, 0.f, 0.f};
       for (int c = 0; c < nch; c++) {
-        unsigned spins = 0;
-        while (!failed && lds_ld(full_a + slot * 4) < unsigned(f + 1)) {
+        const int t0 = c * FT;
+        int g0, ngc;
+        fill_groups<GPT>(o, t0, g0, ngc);
+        const uint32_t sb = ring_a + slot * slot_bytes;
+        int tt[TPC];
+        uint32_t ab[TPC], sca[TPC][GPT], zpa[TPC][GPT];
+        bool valid[TPC];
+#pragma unroll
+        for (int h = 0; h < TPC; h++) {
+          const int p = cw + h * NC, t = t0 + p;
+          valid[h] = t < nt;
+          tt[h] = min(t, nt - 1);
+          ab[h] = a_lane + uint32_t(tt[h]) * KT * 4;
+#pragma unroll
+          for (int g = 0; g < GPT; g++) {
+            const int gi = GPT == 1 ? (tt[h] >> o.tpg_shift) - g0 : p * GPT + g;
+            sca[h][g] = sb + FT * 1024 + ((gi * 16 + m) * ssz & ~3);
+            zpa[h][g] = sb + FT * 1024 + SD * 1024 + ((gi * 16 + m) & ~3);
+          }
+        }
+        u4_t bq[TPC];
+        h8_t af[TPC][SPT];
+        uint32_t scw[TPC][GPT], zpw[TPC][GPT];
+        unsigned full;
+#ifdef NAD_CHAIN_TRACE
+        const unsigned long long tf0 = wall_clock64();
+#endif
+        for (unsigned spins = 0;; spins++) {
+          asm volatile("ds_read_b32 %0, %1" : "=v"(full) : "v"(full_a + slot * 4) : "memory");
+#pragma unroll
+          for (int h = 0; h < TPC; h++) {
+            const uint32_t tb = sb + (cw + h * NC) * 1024 + lane * 16;
+            asm volatile("ds_read_b128 %0, %1" : "=v"(bq[h]) : "v"(tb) : "memory");
+#pragma unroll
+            for (int d = 0; d < SPT; d++) asm volatile("ds_read_b128 %0, %1" : "=v"(af[h][d]) : "v"(ab[h] + d * 128) : "memory");
+#pragma unroll
+            for (int g = 0; g < GPT; g++) {
+              asm volatile("ds_read_b32 %0, %1" : "=v"(scw[h][g]) : "v"(sca[h][g]) : "memory");
+              if constexpr (ASYM) asm volatile("ds_read_b32 %0, %1" : "=v"(zpw[h][g]) : "v"(zpa[h][g]) : "memory");
+            }
+          }
+          asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(full) : : "memory");  // full is defined here, not at its load
+          if (__builtin_amdgcn_readfirstlane(full) >= unsigned(f + 1) || failed) break;
           __builtin_amdgcn_s_sleep(1);
-          if (++spins > kSpinMax) {
+          if (spins > kSpinMax) {
             if (lane == 0) give_up(ctl, 1);
             failed = true;
           }
         }
-        const char* sb = ring + slot * slot_bytes;
-        const char* scb = sb + FT * 1024;
-        const char* zpb = scb + SD * 1024;
-        const int t0 = c * FT;
-        int g0, ngc;
-        fill_groups<GPT>(o, t0, g0, ngc);
 #pragma unroll
-        for (int h = 0; h < FT / NC; h++) {
-          const int p = cw + h * NC, t = t0 + p;
-          if (t >= nt) break;
-          const u4_t b = *reinterpret_cast<const u4_t*>(sb + p * 1024 + lane * 16);
-          const char* ab = a_lane + size_t(t) * KT * 4;
-          f4_t accg = {0.f, 0.f, 0.f, 0.f};
+        for (int h = 0; h < TPC; h++) {  // registers are defined by the wait above: pin every use below it
+          asm volatile("" : "+v"(bq[h]));
 #pragma unroll
-          for (int d = 0; d < SPT; d++) {
-            const int gi = GPT == 1 ? (t >> o.tpg_shift) - g0 : p * GPT + d / SPG;
+          for (int d = 0; d < SPT; d++) asm volatile("" : "+v"(af[h][d]));
+#pragma unroll
+          for (int g = 0; g < GPT; g++) {
+            asm volatile("" : "+v"(scw[h][g]));
+            if constexpr (ASYM) asm volatile("" : "+v"(zpw[h][g]));
+          }
+        }
+        if (lane == 0) lds_add(free_a + slot * 4, 1u);  // operands in registers: the slot may be refilled
+#ifdef NAD_CHAIN_TRACE
+        tr_fw += wall_clock64() - tf0;
+        if (cw == 0 && jl == 0 && c == 0) ETRACE(3, op, wall_clock64());
+#endif
+        float scf[TPC][GPT];
+        int zpv[TPC][GPT];
+#pragma unroll
+        for (int h = 0; h < TPC; h++)
+#pragma unroll
+          for (int g = 0; g < GPT; g++) {
+            const uint32_t x = scw[h][g];
+            const uint32_t hb = (x >> gsh) & 0xFFFFu;
+            const float fb = __uint_as_float(hb << 16), fh = f16_bits_to_f32(uint16_t(hb));
+            const float sv = st == kScaleF32 ? __uint_as_float(x) : (st == kScaleBF16 ? fb : fh);
+            scf[h][g] = valid[h] ? sv : 0.f;  // a ragged last fill: the missing tile contributes nothing
+            zpv[h][g] = ASYM ? int(int8_t((zpw[h][g] >> ((m & 3) * 8)) & 0xFFu)) : 0;
+          }
+        f4_t accg[TPC];
+#pragma unroll
+        for (int d = 0; d < SPT; d++) {
+          const int g = GPT == 1 ? 0 : d / SPG;
+#pragma unroll
+          for (int h = 0; h < TPC; h++) {
             h8_t bf;
             if constexpr (BITS == 4) {
               if constexpr (ASYM) {
-                const float z = float(*reinterpret_cast<const int8_t*>(zpb + gi * 16 + m));
-                bf = dequant4(b[d], mk0, mk1, mag, s16, zc0 - splat(z), zc1 - splat(z));
+                const float z = float(zpv[h][g]);
+                bf = dequant4(bq[h][d], mk0, mk1, mag, s16, zc0 - splat(z), zc1 - splat(z));
               } else {
-                bf = dequant4(b[d], mk0, mk1, mag, s16, zc0, zc1);
+                bf = dequant4(bq[h][d], mk0, mk1, mag, s16, zc0, zc1);
               }
             } else {
-              const int z = ASYM ? int(*reinterpret_cast<const int8_t*>(zpb + gi * 16 + m)) : 0;
-              bf = dequant_step<BITS>(b, d, zp_const(BIAS + z));
+              bf = dequant_step<BITS>(bq[h], d, zp_const(BIAS + zpv[h][g]));
             }
-            const h8_t af = *reinterpret_cast<const h8_t*>(ab + d * 128);
-            accg = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, bf, d % SPG == 0 ? f4_t{0.f, 0.f, 0.f, 0.f} : accg, 0,
-                                                          0, 0);
-            if ((d + 1) % SPG == 0) acc += accg * lds_scale(scb + (gi * 16 + m) * ssz, st);
+            accg[h] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[h][d], bf, d % SPG == 0 ? f4_t{0.f, 0.f, 0.f, 0.f}
+                                                                                       : accg[h], 0, 0, 0);
+          }
+          if ((d + 1) % SPG == 0) {
+#pragma unroll
+            for (int h = 0; h < TPC; h++) acc += accg[h] * scf[h][g];
           }
         }
-        if (lane == 0) lds_add(free_a + slot * 4, 1u);  // this consumer is done with the slot
         f++;
         slot = slot + 1 == S ? 0 : slot + 1;
       }
       const float r = acc[0] + __shfl_down(acc[0], 32, 64);  // row 0 (hi) + row 8 (lo)
       if (lane < 16) part[(jl * NC + cw) * 16 + lane] = r;
     }
+    if (cw == 0) ETRACE(4, op, wall_clock64());
+#ifdef NAD_CHAIN_TRACE
+    if (cw == 0) ETRACE(9, op, tr_fw);
+#endif
     cbar(bar_a, bar_epoch, ctl, lane, failed);
+    if (cw == 0) ETRACE(10, op, wall_clock64());
 
-    // 3) sum the consumers' partials in a fixed order, epilogue, results + granules
-    const int vpu = o.dual ? 2 : 1;
-    const int nout = nv / vpu * 16;
+    // 3) sum the consumers' partials in a fixed order, RMS scale, epilogue, results + granules
     const unsigned tag = gen * 256u + o.tag;
     for (int oi = cl; oi < nout; oi += NC * 64) {
       const int p = oi >> 4, nn = oi & 15;
@@ -468,44 +608,44 @@ __global__ __launch_bounds__(kEngThreads, 1) void woq_engine_kernel(const EngOp*
       for (int h = 0; h < 2; h++) {
         if (h < vpu) {
           const float* ps = part + (p * vpu + h) * NC * 16 + nn;
-          y[h] = ((ps[0] + ps[16]) + (ps[32] + ps[48])) + ((ps[64] + ps[80]) + (ps[96] + ps[112]));
+          y[h] = (((ps[0] + ps[16]) + (ps[32] + ps[48])) + ((ps[64] + ps[80]) + (ps[96] + ps[112]))) * inv;
         }
       }
-      int wsel, s;
-      vstripe(o, v0 + p * vpu, wsel, s);
-      const EngWeight& W = o.w[wsel];
-      const int n = s * 16 + nn;
-      if (n >= W.n) continue;
+      int wsel, sx;
+      vstripe(o, v0 + p * vpu, wsel, sx);
+      const int n = sx * 16 + nn;
+      if (n >= sel3(wsel, o.w[0].n, o.w[1].n, o.w[2].n)) continue;
+      float* const w_out = sel3(wsel, o.w[0].out, o.w[1].out, o.w[2].out);
+      unsigned long long* const w_gran = sel3(wsel, o.w[0].gran, o.w[1].gran, o.w[2].gran);
       float val = y[0];
       if (o.epi == kEpiResAdd) {
-        float r;
         if (o.res_gran) {
           const unsigned want = gen * 256u + o.res_tag;
           unsigned spins = 0;
-          while (true) {
-            const unsigned long long x = __hip_atomic_load(o.res_gran + n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            r = __uint_as_float(unsigned(x));
-            if (unsigned(x >> 32) == want || failed) break;
+          unsigned long long x = res_g;
+          while (unsigned(x >> 32) != want && !failed) {  // the early load normally already holds it
             __builtin_amdgcn_s_sleep(1);
+            x = __hip_atomic_load(o.res_gran + n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (++spins > kSpinMax) {
               give_up(ctl, 4);
               failed = true;
             }
           }
-        } else {
-          r = o.res[n];
+          res_v = __uint_as_float(unsigned(x));
         }
-        val += r;
+        val += res_v;
       } else if (o.epi == kEpiSiluMul || o.epi == kEpiGeluMul) {
         const float t1 = o.epi == kEpiSiluMul ? silu_f(y[0]) : gelu_f(y[0]);
         if (o.aux) o.aux[n] = t1;
         val = t1 * y[1];
       }
-      if (W.out) W.out[n] = val;
-      if (W.gran)
-        __hip_atomic_store(W.gran + n, (static_cast<unsigned long long>(tag) << 32) | __float_as_uint(val),
+      if (w_out) w_out[n] = val;
+      if (w_gran)
+        __hip_atomic_store(w_gran + n, (static_cast<unsigned long long>(tag) << 32) | __float_as_uint(val),
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    (void)my_n;
+    if (cw == 0) ETRACE(5, op, wall_clock64());
   }
   // the launch generation moves on once this workgroup is done: every workgroup read it before publishing anything,
   // and workgroup 0 got here only after gathering results of every workgroup (bump is set only when an op reads a
@@ -524,8 +664,9 @@ bool engine_geometry(EngGeometry& g, int kp) {
   const size_t budget = 160 * 1024;
   if (fixed >= budget) return false;
   int s = int((budget - fixed) / g.slot_bytes);
-  if (s > 8) s = 8;
-  if (s < kEngInflight + 2) return false;  // one slot to fill, D in flight, one being read
+  if (s > 16) s = 16;
+  const int ipf = kEngFillTiles + g.sd + (g.asym ? 1 : 0);
+  if (s < 63 / ipf + 2) return false;  // D fills in flight + at least two published ones for the consumers
   g.slots = s;
   g.lds = fixed + size_t(s) * g.slot_bytes;
   return true;
@@ -543,7 +684,7 @@ static hipError_t engine_launch4(const EngOp* ops, int n_ops, const EngGeometry&
     attr = true;
   }
   hipLaunchKernelGGL(k, dim3(grid), dim3(kEngThreads), g.lds, st, ops, n_ops, ctl, g.slots, int(g.slot_bytes), g.kp,
-                     bump);
+                     bump, g.thin);
   return hipGetLastError();
 }
 
@@ -574,3 +715,11 @@ hipError_t launch_engine(const EngOp* ops, int n_ops, const EngGeometry& g, unsi
 }
 
 }  // namespace nad
+
+#ifdef NAD_CHAIN_TRACE
+extern "C" int nad_chain_trace_fetch(void* host, size_t bytes) {
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  const size_t n = sizeof(nad::eng::nad_chain_trace) < bytes ? sizeof(nad::eng::nad_chain_trace) : bytes;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(nad::eng::nad_chain_trace), n) == hipSuccess ? 0 : -1;
+}
+#endif

@@ -88,9 +88,10 @@ def _run_chains(chains):
 
 def _same(a, b):
     assert len(a) == len(b)
-    for i, (x, y) in enumerate(zip(a, b)):
+    bad = [(i, (x - y).abs().max().item()) for i, (x, y) in enumerate(zip(a, b)) if not torch.equal(x, y)]
+    for i, y in enumerate(b):
         assert torch.isfinite(y).all(), i
-        assert torch.equal(x, y), (i, (x - y).abs().max().item())
+    assert not bad, bad
 
 
 @pytest.mark.parametrize("asym", [False, True])

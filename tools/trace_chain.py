@@ -1,5 +1,10 @@
-"""Phase trace of the decode chain (development tool): per op, median / max over workgroups of
-prefetch->barrier-passed, staging, stream, publish; and the gaps between ops.  Needs `make -C neural_amd chaintrace`."""
+"""Phase trace of the decode weight-stream engine (development tool; needs `make -C neural_amd chaintrace`).
+
+Runs the bench's Llama-2-7B stack as the cut launches (default) or the whole token as one launch (arg "whole"), then
+prints per op kind the medians over workgroups of: gather (op start -> input read), stage (-> hi/lo rows staged),
+first fill (-> first weight fill ready), loop (stream), publish (reduce + granules), the consumer's FULL-wait and the
+loader's FREE-wait inside the op, and the op's span (first start -> last publish over workgroups).
+Usage: python tools/trace_chain.py [cut|whole] [layers]"""
 import ctypes as C
 import os
 import sys
@@ -13,35 +18,63 @@ import torch  # noqa: E402
 import bench  # noqa: E402
 from neural_amd import _lib  # noqa: E402
 
-layers = int(sys.argv[1]) if len(sys.argv) > 1 else 32
-bench.LAYERS = layers
-stack = bench.Stack(0, 1)
-cr = bench.ChainRunner(stack, 1, "cuda")
-for _ in range(3):
-    cr.step()
-torch.cuda.synchronize()
+mode = sys.argv[1] if len(sys.argv) > 1 else "cut"
+layers = int(sys.argv[2]) if len(sys.argv) > 2 else 32
+cfg = dict(bench.LLAMA, layers=layers)
+stack = bench.Stack(cfg, 0, 1)
+cr = bench.ChainRunner(stack, "cuda", cut=(mode == "cut"))
 L = _lib.lib()
 L.nad_chain_trace_fetch.argtypes = [C.c_void_p, C.c_size_t]
-buf = np.zeros((6, 160, 256), np.uint64)
-cr.step()
-assert L.nad_chain_trace_fetch(buf.ctypes.data, buf.nbytes) == 0
-khz = 100000.0  # wall_clock64 runs at 100 MHz on MI300-class parts
-tick = 1e3 / khz
-n = cr.n_ops
-t0 = buf[0, 0].astype(np.int64).min()
+tick = 1e-2  # wall_clock64: 100 MHz -> us
 names = ["qkv", "o", "gate_up", "down"]
-tot = (buf[4, n - 1].astype(np.int64).max() - t0) * tick
-print(f"chain span {tot:.1f} us over {n} ops")
-rows = {}
-for op in range(n):
-    b = buf[:, op].astype(np.int64)
-    nm = names[op % 4] if op < n - 1 else "lm_head"
-    d = dict(wait=np.median(b[1] - b[0]) * tick, stage=np.median(b[2] - b[1]) * tick,
-             stream=np.median(b[3] - b[2]) * tick, stream_max=(b[3] - b[2]).max() * tick,
-             publish=np.median(b[4] - b[3]) * tick,
-             span=(b[4].max() - b[0].min()) * tick,
-             start_skew=(b[0].max() - b[0].min()) * tick)
-    rows.setdefault(nm, []).append(d)
-for nm, ds in rows.items():
-    keys = ds[0].keys()
-    print(nm.ljust(8), " ".join(f"{k} {np.median([d[k] for d in ds]):6.2f}" for k in keys))
+if mode == "cut":
+    # one launch at a time (the trace buffer holds one launch): trace each segment kind once, warm
+    rows = {}
+    for ci, ch in enumerate(cr.chains[:3] + cr.chains[-1:]):
+        for _ in range(3):
+            ch.run()
+        torch.cuda.synchronize()
+        buf = np.zeros((14, 160, 256), np.uint64)
+        ch.run()
+        assert L.nad_chain_trace_fetch(buf.ctypes.data, buf.nbytes) == 0
+        nops = ch.n_ops if hasattr(ch, "n_ops") else len(ch._ops)
+        b = buf.astype(np.int64)
+        t0 = b[0, 0].min()
+        span = (b[5, nops - 1].max() - t0) * tick
+        kinds = ["qkv"] if nops == 1 else ["o", "gate_up", "down", "qkv" if ci < 3 else "lm_head"]
+        print(f"launch {ci}: {nops} ops, span {span:.2f} us (first op start -> last publish)")
+        for op in range(nops):
+            x = b[:, op]
+            g1 = x[11] - x[0]
+            d = dict(gather=np.median(x[1] - x[0]) * tick,
+                     pass1=(np.median(g1[x[11] > 0]) * tick if (x[11] > 0).any() else 0.0),
+                     stage=np.median(x[2] - x[1]) * tick,
+                     first=np.median(x[3] - x[2]) * tick, loop=np.median(x[4] - x[3]) * tick,
+                     publish=np.median(x[5] - x[4]) * tick, pbar=np.median(x[10] - x[4]) * tick,
+                     fullwait=np.median(x[9]) * tick,
+                     freewait=np.median(x[8]) * tick, start=(x[0].min() - t0) * tick,
+                     end=(x[5].max() - t0) * tick, endskew=(x[5].max() - x[5].min()) * tick)
+            print("  " + kinds[op].ljust(8) + " ".join(f"{k} {v:6.2f}" for k, v in d.items()), flush=True)
+else:
+    ch = cr.chains[0]
+    for _ in range(3):
+        ch.run()
+    torch.cuda.synchronize()
+    buf = np.zeros((14, 160, 256), np.uint64)
+    ch.run()
+    assert L.nad_chain_trace_fetch(buf.ctypes.data, buf.nbytes) == 0
+    b = buf.astype(np.int64)
+    n = cr.n_ops
+    t0 = b[0, 0].min()
+    print(f"whole token: {n} ops, span {(b[5, n - 1].max() - t0) * tick:.1f} us")
+    rows = {}
+    for op in range(n):
+        x = b[:, op]
+        nm = "lm_head" if op == n - 1 else names[op % 4]
+        rows.setdefault(nm, []).append(dict(
+            gather=np.median(x[1] - x[0]) * tick, stage=np.median(x[2] - x[1]) * tick,
+            first=np.median(x[3] - x[2]) * tick, loop=np.median(x[4] - x[3]) * tick,
+            publish=np.median(x[5] - x[4]) * tick, fullwait=np.median(x[9]) * tick, freewait=np.median(x[8]) * tick,
+            span=(x[5].max() - x[0].min()) * tick, endskew=(x[5].max() - x[5].min()) * tick))
+    for nm, ds in rows.items():
+        print(nm.ljust(8), " ".join(f"{k} {np.median([d[k] for d in ds]):6.2f}" for k in ds[0]), flush=True)
