@@ -576,7 +576,7 @@ __global__ __launch_bounds__(kEngThreads, 1) void woq_engine_kernel(const EngOp*
                 bf = dequant4(bq[h][d], mk0, mk1, mag, s16, zc0, zc1);
               }
             } else {
-              bf = dequant_step<BITS>(bq[h], d, zp_const(BIAS + zpv[h][g]));
+              bf = dequant2_step(bq[h], d, BIAS + zpv[h][g]);
             }
             accg[h] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[h][d], bf, d % SPG == 0 ? f4_t{0.f, 0.f, 0.f, 0.f}
                                                                                        : accg[h], 0, 0, 0);

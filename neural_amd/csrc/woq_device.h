@@ -70,6 +70,51 @@ __device__ __forceinline__ h8_t dequant_step(const u4_t& b, int d, h2_t c2) {
   return r;
 }
 
+// int2 through scaled magic numbers: crumb i of each 16-bit half (bits 2i .. 2i + 1 of x) or'ed into 0x6400 is the fp16
+// 1024 + 4^i q (exact: 4^i q <= 192), and fma(that, 4^-i, -(1024 * 4^-i + bias + zp)) is q - bias - zp exactly (fused,
+// and every intermediate is representable).  4 v_and_or + 4 packed fp16 ops per 8 weights, plus one shift for the odd
+// step of a dword -- dequant_step<2> spends a shift per crumb pair.  Same element order as dequant_step<2>.
+__device__ __forceinline__ h2_t zp_const(int bias_plus_zp);
+struct Dq2c {
+  h2_t c0, c1, c2, c3;
+};
+__device__ __forceinline__ h2_t h2_splat(float v) {
+  h2_t r;
+  r[0] = _Float16(v);
+  r[1] = _Float16(v);
+  return r;
+}
+__device__ __forceinline__ Dq2c dq2_consts(int bias_plus_zp) {
+  const float b = float(bias_plus_zp);
+  return Dq2c{h2_splat(-(1024.f + b)), h2_splat(-(256.f + b)), h2_splat(-(64.f + b)), h2_splat(-(16.f + b))};
+}
+// x: the dword already shifted right by 8 for the odd step (b[d >> 1] >> ((d & 1) * 8))
+__device__ __forceinline__ h8_t dequant2s(uint32_t x, const Dq2c& c) {
+  const uint32_t mag = 0x64006400u;
+  const h2_t p0 = as_h2((x & 0x00030003u) | mag) + c.c0;
+  const h2_t p1 = __builtin_elementwise_fma(as_h2((x & 0x000C000Cu) | mag), h2_splat(0.25f), c.c1);
+  const h2_t p2 = __builtin_elementwise_fma(as_h2((x & 0x00300030u) | mag), h2_splat(0.0625f), c.c2);
+  const h2_t p3 = __builtin_elementwise_fma(as_h2((x & 0x00C000C0u) | mag), h2_splat(0.015625f), c.c3);
+  h8_t r;
+  r[0] = p0[0];
+  r[1] = p0[1];
+  r[2] = p1[0];
+  r[3] = p1[1];
+  r[4] = p2[0];
+  r[5] = p2[1];
+  r[6] = p3[0];
+  r[7] = p3[1];
+  return r;
+}
+// one 32-deep step of an int2 tile (the dwords of a lane's 16 B): the faster form unless NAD_INT2_DQ_OLD (A/B builds)
+__device__ __forceinline__ h8_t dequant2_step(const u4_t& b, int d, int bias_plus_zp) {
+#ifdef NAD_INT2_DQ_OLD
+  return dequant_step<2>(b, d, zp_const(bias_plus_zp));
+#else
+  return dequant2s(b[d >> 1] >> ((d & 1) * 8), dq2_consts(bias_plus_zp));
+#endif
+}
+
 // NFloat 4-bit weights (F4_BNB, F4_E2M1, F4_NF4): code -> value LUTs of bestla_utils.h:749-790, rounded to fp16 for
 // the MFMA B operand (the fp32 group scale is applied after the MFMA, as for the integer formats)
 static __constant__ _Float16 kF4LutH[3][16] = {

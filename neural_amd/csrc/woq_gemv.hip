@@ -434,7 +434,8 @@ __global__ __launch_bounds__(gemv_max_threads<GPT>()) void woq_gemv_kernel(GemvA
             bf = dequant4(S.b[i][d], dq, zc0, zc1);
           }
         } else {
-          bf = dequant_step<BITS>(S.b[i], d, zp_const(BIAS + S.zp[i][g]));
+          bf = BITS == 2 ? dequant2_step(S.b[i], d, BIAS + S.zp[i][g])
+                         : dequant_step<BITS>(S.b[i], d, zp_const(BIAS + S.zp[i][g]));
         }
         const h8_t af = *reinterpret_cast<const h8_t*>(ab + ti * KT * 2 + d * 64);
         const bool first = d % SPG == 0;
@@ -687,7 +688,8 @@ __global__ __launch_bounds__((m1_max_threads<GPT, KSN>())) void woq_gemv_m1_kern
             bf = dequant4(S.b[i][d], dq, zc0, zc1);
           }
         } else {
-          bf = dequant_step<BITS>(S.b[i], d, zp_const(BIAS + S.zp[i][g]));
+          bf = BITS == 2 ? dequant2_step(S.b[i], d, BIAS + S.zp[i][g])
+                         : dequant_step<BITS>(S.b[i], d, zp_const(BIAS + S.zp[i][g]));
         }
         const h8_t af = *reinterpret_cast<const h8_t*>(ab + i * KT * 2 + d * 64);
         accg[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, bf, d % SPG == 0 ? f4_t{0.f, 0.f, 0.f, 0.f} : accg[i], 0,
