@@ -1381,6 +1381,8 @@ extern "C" void* nad_chain_create(const nad_chain_op* ops, int n_ops, int m) {
     sd_bytes = std::max(sd_bytes, std::min(groups, size_t(w0.ng)) * 16 * ssz);
   }
   g.thin = env_int("NAD_ENGINE_THIN", 0);  // measured slower on every edge (trace_chain.py): off
+  g.loaders = env_int("NAD_ENGINE_LOADERS", 2);  // loader waves (tools/dma_probe.hip: 2 x 2 fills in flight best)
+  g.depth = env_int("NAD_ENGINE_DEPTH", 1);      // fills in flight per loader wave (1 measured faster than 2)
   g.sd = int((sd_bytes + 1023) / 1024);
   if (g.sd < 1) g.sd = 1;
   if (g.sd > 2 || !engine_geometry(g, kp)) {

@@ -42,11 +42,12 @@ struct EngOp {
   unsigned tag;                 // this op's index in the launch + 1
 };
 
-// Engine geometry: 8 consumer waves + 1 loader wave, fills of 16 tiles (two per consumer), as many fills in flight as
-// the 6-bit vmcnt can count (63 DMA instructions: 3 fills of 16 tiles + their scale pieces).  Measured (trace_chain.py,
-// DESIGN.md section 4): 8-tile fills with 7 in flight stream SLOWER (the loader's per-fill LDS round trips dominate).
+// Engine geometry: 8 consumer waves + `loaders` loader waves (each keeping `depth` fills in flight), fills of 16 tiles
+// (two per consumer).  Measured (trace_chain.py): 8-tile fills stream SLOWER (the loader's per-fill
+// LDS round trips dominate); one loader wave tops out near 20 GB/s per CU whatever its depth (tools/dma_probe.hip).
 constexpr int kEngConsumers = 8;
-constexpr int kEngThreads = (kEngConsumers + 1) * 64;
+constexpr int kEngMaxLoaders = 4;
+constexpr int kEngMaxThreads = (kEngConsumers + kEngMaxLoaders) * 64;
 constexpr int kEngFillTiles = 16;
 constexpr int kEngMaxStripes = 16;   // virtual stripes of one op per workgroup (partial-sum slots)
 constexpr int kEngMaxK = 16384;      // input length (gather registers)
@@ -58,6 +59,7 @@ struct EngGeometry {
   size_t lds;                   // dynamic LDS bytes
   size_t slot_bytes;
   int thin;                     // thin the loader to one fill in flight while the consumers gather (NAD_ENGINE_THIN)
+  int loaders, depth;           // loader waves, fills in flight per loader wave
 };
 
 // fills g.kp/slots/lds from g.bits/gpt/asym/sd and the ops' largest padded K; false if the ring does not fit

@@ -51,7 +51,7 @@ namespace eng {
 
 // Development instrumentation (make chaintrace): per-(op, workgroup) wall-clock stamps of the engine's phases.
 #ifdef NAD_CHAIN_TRACE
-constexpr int kTrOps = 160, kTrWg = 256, kTrSlots = 14;
+constexpr int kTrOps = 160, kTrWg = 256, kTrSlots = 20;
 __device__ unsigned long long nad_chain_trace[kTrSlots][kTrOps][kTrWg];
 #define ETRACE(slot, opi, val)                                                                     \
   do {                                                                                             \
@@ -112,17 +112,27 @@ __device__ __forceinline__ T sel3(int w, T x0, T x1, T x2) {
   return w == 0 ? x0 : (w == 1 ? x1 : x2);
 }
 
+// The op fields a role reads, loaded as scalars once at the op's start: the inline-asm "memory" clobbers of the LDS
+// protocol would otherwise make hipcc re-load a field from the op table (a dependent scalar-cache round trip) at every
+// use -- the consumer's per-op code held ~30 such load -> wait pairs.
+struct OpGeom {
+  int nt, ng, tpg_shift, scale_t, u_q, u_r, dual, sb1, sb2;
+};
+__device__ __forceinline__ OpGeom op_geom(const EngOp& o) {
+  return OpGeom{o.nt, o.ng, o.tpg_shift, o.scale_t, o.u_q, o.u_r, o.dual, o.stripe_base[1], o.stripe_base[2]};
+}
+
 // virtual stripe -> (weight, stripe within it)
-__device__ __forceinline__ void vstripe(const EngOp& o, int v, int& w, int& s) {
+__device__ __forceinline__ void vstripe(const OpGeom& o, int v, int& w, int& s) {
   if (o.dual) {
     w = v & 1;
     s = v >> 1;
   } else {
-    w = (v >= o.stripe_base[1] ? 1 : 0) + (v >= o.stripe_base[2] ? 1 : 0);
-    s = v - o.stripe_base[w];
+    w = (v >= o.sb1 ? 1 : 0) + (v >= o.sb2 ? 1 : 0);
+    s = v - (w == 0 ? 0 : (w == 1 ? o.sb1 : o.sb2));
   }
 }
-__device__ __forceinline__ void unit_range(const EngOp& o, int bid, int& v0, int& nv) {
+__device__ __forceinline__ void unit_range(const OpGeom& o, int bid, int& v0, int& nv) {
   const int u0 = bid * o.u_q + min(bid, o.u_r);
   const int nu = o.u_q + (bid < o.u_r ? 1 : 0);
   const int vpu = o.dual ? 2 : 1;
@@ -131,7 +141,7 @@ __device__ __forceinline__ void unit_range(const EngOp& o, int bid, int& v0, int
 }
 // groups of one fill (chunk c of a stripe): first group and count
 template <int GPT>
-__device__ __forceinline__ void fill_groups(const EngOp& o, int t0, int& g0, int& ngc) {
+__device__ __forceinline__ void fill_groups(const OpGeom& o, int t0, int& g0, int& ngc) {
   const int t1 = min(t0 + FT, o.nt);
   if constexpr (GPT == 1) {
     g0 = t0 >> o.tpg_shift;
@@ -142,107 +152,128 @@ __device__ __forceinline__ void fill_groups(const EngOp& o, int t0, int& g0, int
   }
 }
 
-// ------------------------------------------------------------------------------------------------ loader
-template <int GPT, bool ASYM, int SD>
+// ------------------------------------------------------------------------------------------------ loaders
+// NL loader waves share the launch's fill sequence: loader lw issues the fills f = lw, lw + NL, ... (every loader walks
+// the whole sequence, skipping the others' fills), keeps D of its own in flight (counted vmcnt) and publishes them in
+// its order.  One wave cannot keep more than ~2 fills usefully in flight (tools/dma_probe.hip on MI355X: 1 wave x 2-3
+// fills 19-20 GB/s per CU, 2 waves x 2 fills 27 GB/s = 6.9 TB/s chip-wide, 3 waves x 1 fill 26.6).  Slot of fill f:
+// f mod S; it is re-filled only when all consumers released fill f - S (FREE counter >= NC * (f / S)), so fills into one
+// slot stay ordered whichever loader issues them.
+template <int GPT, bool ASYM, int SD, int D>
 __device__ void loader(const EngOp* ops, int n_ops, char* ring, int S, int slot_bytes, uint32_t ctl_a, unsigned* ctl,
-                       int lane, int thin) {
+                       int lane, int thin, int lw, int NL) {
   constexpr int IPF = FT + SD + (ASYM ? 1 : 0);  // DMA instructions per fill: constant, so vmcnt counts are exact
-  constexpr int D = 63 / IPF;                     // fills in flight: as many as vmcnt (6 bits) can count
+  static_assert(D * IPF <= 63, "in-flight DMAs beyond what vmcnt counts");
   const uint32_t full_a = ctl_a + kFull * 4, free_a = ctl_a + kFree * 4;
-  int f = 0, fpub = 0, slot = 0, pslot = 0;
-  unsigned round = 0;
+  int slot = 0, rr = 0;   // slot of fill f, f mod NL
+  unsigned round = 0;     // f / S
+  int mine = 0, mpub = 0;         // own fills issued / published
+  int pub_f = lw, pub_slot = lw;  // the next own fill to publish and its slot
+  while (pub_slot >= S) pub_slot -= S;
   bool failed = false;
   auto publish_one = [&]() {
-    lds_st(full_a + pslot * 4, unsigned(fpub + 1));
-    fpub++;
-    pslot = pslot + 1 == S ? 0 : pslot + 1;
+    lds_st(full_a + pub_slot * 4, unsigned(pub_f + 1));
+    mpub++;
+    pub_f += NL;
+    pub_slot += NL;
+    while (pub_slot >= S) pub_slot -= S;
   };
   for (int op = 0; op < n_ops; op++) {
-    const EngOp& o = ops[op];
+    const EngOp& od = ops[op];
+    const OpGeom o = op_geom(od);
+    const void *tl0 = od.w[0].tiles, *tl1 = od.w[1].tiles, *tl2 = od.w[2].tiles;
+    const void *sc0 = od.w[0].scales, *sc1 = od.w[1].scales, *sc2 = od.w[2].scales;
+    const void *zp0 = od.w[0].zps, *zp1 = od.w[1].zps, *zp2 = od.w[2].zps;
+    const int ns0 = od.w[0].ns, ns1 = od.w[1].ns, ns2 = od.w[2].ns;
     const int nt = o.nt, ng = o.ng, nch = (nt + FT - 1) / FT;
     const int ssz = o.scale_t == kScaleF32 ? 4 : 2;
     int v0, nv;
     unit_range(o, blockIdx.x, v0, nv);
 #ifdef NAD_CHAIN_TRACE
     unsigned long long tr_wait = 0;
+    bool tr_first = true;
 #endif
     for (int jl = 0; jl < nv; jl++) {
       int wsel, s;
       vstripe(o, v0 + jl, wsel, s);
-      const EngWeight& W = o.w[wsel];
-      const auto rt = rsrc(W.tiles, unsigned(W.ns) * nt * 1024u);
-      const auto rs = rsrc(W.scales, unsigned(W.ns) * ng * 16u * ssz);
-      const auto rz = rsrc(ASYM ? static_cast<const void*>(W.zps) : W.tiles, ASYM ? unsigned(W.ns) * ng * 16u : 0u);
+      const unsigned wns = unsigned(sel3(wsel, ns0, ns1, ns2));
+      const auto rt = rsrc(sel3(wsel, tl0, tl1, tl2), wns * nt * 1024u);
+      const auto rs = rsrc(sel3(wsel, sc0, sc1, sc2), wns * ng * 16u * ssz);
+      const auto rz = rsrc(ASYM ? sel3(wsel, zp0, zp1, zp2) : sel3(wsel, tl0, tl1, tl2), ASYM ? wns * ng * 16u : 0u);
       const int tbase = s * nt * 1024 + lane * 16;
       for (int c = 0; c < nch; c++) {
-        if (f - fpub == D) {  // keep at most D fills in flight: the oldest has landed -> publish it
-          wait_vm<(D - 1) * IPF>();
-          publish_one();
-        }
-        if (round > 0) {  // this slot's previous fill must have been released by every consumer
-          const unsigned need = NC * round;
-          if (lds_ld(free_a + slot * 4) < need) {
-#ifdef NAD_CHAIN_TRACE
-            const unsigned long long tw0 = wall_clock64();
-#endif
-            wait_vm<0>();  // about to wait anyway: publish everything in flight first
-            while (fpub < f) publish_one();
-            unsigned spins = 0;
-            while (!failed && lds_ld(free_a + slot * 4) < need) {
-              __builtin_amdgcn_s_sleep(1);
-              if (++spins > kSpinMax) {
-                give_up(ctl, 2);
-                failed = true;
-              }
-            }
-#ifdef NAD_CHAIN_TRACE
-            tr_wait += wall_clock64() - tw0;
-#endif
+        if (rr == lw) {
+          if (mine - mpub == D) {  // keep at most D own fills in flight: the oldest has landed -> publish it
+            wait_vm<(D - 1) * IPF>();
+            publish_one();
           }
-        }
+          if (round > 0) {  // this slot's previous fill must have been released by every consumer
+            const unsigned need = NC * round;
+            if (lds_ld(free_a + slot * 4) < need) {
 #ifdef NAD_CHAIN_TRACE
-        if (jl == 0 && c == 0) ETRACE(6, op, wall_clock64());
+              const unsigned long long tw0 = wall_clock64();
 #endif
-        // while the consumers gather an input, keep one fill in flight: their loads queue behind this wave's DMAs
-        // (MI355X_MICROARCH.md gather-pass: 0.3-0.65 us with the own DMA quiet vs 1.0-1.7 behind a refill burst)
-        if (thin && lds_ld(ctl_a + kPhase * 4) != 0u) {
-          wait_vm<0>();
-          while (fpub < f) publish_one();
-        }
-        char* sb = ring + slot * slot_bytes;
-        const int t0 = c * FT;
+              wait_vm<0>();  // about to wait anyway: publish everything in flight first
+              while (mpub < mine) publish_one();
+              unsigned spins = 0;
+              while (!failed && lds_ld(free_a + slot * 4) < need) {
+                __builtin_amdgcn_s_sleep(1);
+                if (++spins > kSpinMax) {
+                  give_up(ctl, 2);
+                  failed = true;
+                }
+              }
+#ifdef NAD_CHAIN_TRACE
+              tr_wait += wall_clock64() - tw0;
+#endif
+            }
+          }
+#ifdef NAD_CHAIN_TRACE
+          if (tr_first && lw == 0) ETRACE(6, op, wall_clock64());
+          tr_first = false;
+#endif
+          // while the consumers gather an input, keep no fill in flight: their loads queue behind this wave's DMAs
+          // (MI355X_MICROARCH.md gather-pass: 0.3-0.65 us with the own DMA quiet vs 1.0-1.7 behind a refill burst)
+          if (thin && lds_ld(ctl_a + kPhase * 4) != 0u) {
+            wait_vm<0>();
+            while (mpub < mine) publish_one();
+          }
+          char* sb = ring + slot * slot_bytes;
+          const int t0 = c * FT;
 #pragma unroll
-        for (int i = 0; i < FT; i++)
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(rt, (lds_void_t*)(sb + i * 1024), 16,
-                                                   t0 + i < nt ? tbase + (t0 + i) * 1024 : kOOB, 0, 0, kNT);
-        int g0, ngc;
-        fill_groups<GPT>(o, t0, g0, ngc);
-        const int sbytes = ngc * 16 * ssz, soff = (s * ng + g0) * 16 * ssz;
+          for (int i = 0; i < FT; i++)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rt, (lds_void_t*)(sb + i * 1024), 16,
+                                                     t0 + i < nt ? tbase + (t0 + i) * 1024 : kOOB, 0, 0, kNT);
+          int g0, ngc;
+          fill_groups<GPT>(o, t0, g0, ngc);
+          const int sbytes = ngc * 16 * ssz, soff = (s * ng + g0) * 16 * ssz;
 #pragma unroll
-        for (int j = 0; j < SD; j++) {
-          const int b = j * 1024 + lane * 16;
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)(sb + FT * 1024 + j * 1024), 16,
-                                                   b < sbytes ? soff + b : kOOB, 0, 0, 0);
+          for (int j = 0; j < SD; j++) {
+            const int b = j * 1024 + lane * 16;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)(sb + FT * 1024 + j * 1024), 16,
+                                                     b < sbytes ? soff + b : kOOB, 0, 0, 0);
+          }
+          if constexpr (ASYM) {
+            const int b = lane * 16;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rz, (lds_void_t*)(sb + FT * 1024 + SD * 1024), 16,
+                                                     b < ngc * 16 ? (s * ng + g0) * 16 + b : kOOB, 0, 0, 0);
+          }
+          mine++;
         }
-        if constexpr (ASYM) {
-          const int b = lane * 16;
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(rz, (lds_void_t*)(sb + FT * 1024 + SD * 1024), 16,
-                                                   b < ngc * 16 ? (s * ng + g0) * 16 + b : kOOB, 0, 0, 0);
-        }
-        f++;
+        if (++rr == NL) rr = 0;
         if (++slot == S) {
           slot = 0;
           round++;
         }
       }
     }
-    ETRACE(7, op, wall_clock64());
+    if (lw == 0) ETRACE(7, op, wall_clock64());
 #ifdef NAD_CHAIN_TRACE
-    ETRACE(8, op, tr_wait);
+    if (lw == 0) ETRACE(8, op, tr_wait);
 #endif
   }
   wait_vm<0>();
-  while (fpub < f) publish_one();
+  while (mpub < mine) publish_one();
 }
 
 // ------------------------------------------------------------------------------------------------ consumers
@@ -297,9 +328,9 @@ __device__ __forceinline__ void cbar(uint32_t a, unsigned& epoch, unsigned* ctl,
 }
 
 template <int BITS, int GPT, bool ASYM, int SD>
-__global__ __launch_bounds__(kEngThreads, 1) void woq_engine_kernel(const EngOp* __restrict__ ops, int n_ops,
-                                                                    unsigned* ctl, int S, int slot_bytes, int Kp,
-                                                                    int bump, int thin) {
+__global__ __launch_bounds__(kEngMaxThreads, 1) void woq_engine_kernel(const EngOp* __restrict__ ops, int n_ops,
+                                                                       unsigned* ctl, int S, int slot_bytes, int Kp,
+                                                                       int bump, int thin, int nl, int depth) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int KT = BITS == 4 ? 128 : 256, SPT = KT / 32, SPG = SPT / GPT, BIAS = BITS == 4 ? 8 : 2;
   const int lane = threadIdx.x & 63;
@@ -310,12 +341,19 @@ __global__ __launch_bounds__(kEngThreads, 1) void woq_engine_kernel(const EngOp*
   char* ring = act + size_t(Kp) * 4;
   if (threadIdx.x < kCtlBytes / 4) reinterpret_cast<unsigned*>(smem)[threadIdx.x] = 0u;
   __syncthreads();
-  if (wave == NC) {
-    loader<GPT, ASYM, SD>(ops, n_ops, ring, S, slot_bytes, ctl_a, ctl, lane, thin);
+  if (wave >= NC) {
+    const int lw = wave - NC;
+    if (depth == 1)
+      loader<GPT, ASYM, SD, 1>(ops, n_ops, ring, S, slot_bytes, ctl_a, ctl, lane, thin, lw, nl);
+    else
+      loader<GPT, ASYM, SD, 2>(ops, n_ops, ring, S, slot_bytes, ctl_a, ctl, lane, thin, lw, nl);
     return;
   }
 
   const int cw = wave, cl = wave * 64 + lane;  // consumer wave, consumer lane
+#ifdef NAD_EXP_PRIO  // experiment: the younger half of the consumers at a higher issue priority
+  if (cw >= NC / 2) __builtin_amdgcn_s_setprio(NAD_EXP_PRIO);
+#endif
   const uint32_t full_a = ctl_a + kFull * 4, free_a = ctl_a + kFree * 4, bar_a = ctl_a + kBar * 4;
   float* nsum = reinterpret_cast<float*>(smem) + kNsum;
   const unsigned gen = __builtin_amdgcn_readfirstlane(__hip_atomic_load(ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
@@ -332,8 +370,22 @@ __global__ __launch_bounds__(kEngThreads, 1) void woq_engine_kernel(const EngOp*
   int f = 0, slot = 0;
 
   for (int op = 0; op < n_ops; op++) {
-    const EngOp& o = ops[op];
-    const int K = o.K, nt = o.nt, Kpo = nt * KT, nch = (nt + FT - 1) / FT;
+    const EngOp& od = ops[op];
+    const OpGeom o = op_geom(od);
+    const int K = od.K;
+    const float* const o_act = od.act;
+    const unsigned long long* const o_act_gran = od.act_gran;
+    const unsigned o_act_tag = od.act_tag, o_res_tag = od.res_tag, o_tag = od.tag;
+    const int o_norm = od.norm, o_epi = od.epi;
+    const float o_norm_eps = od.norm_eps;
+    const float* const o_norm_w = od.norm_w;
+    const float* const o_res = od.res;
+    const unsigned long long* const o_res_gran = od.res_gran;
+    float* const o_aux = od.aux;
+    const int wn0 = od.w[0].n, wn1 = od.w[1].n, wn2 = od.w[2].n;
+    float *const wo0 = od.w[0].out, *const wo1 = od.w[1].out, *const wo2 = od.w[2].out;
+    unsigned long long *const wg0 = od.w[0].gran, *const wg1 = od.w[1].gran, *const wg2 = od.w[2].gran;
+    const int nt = o.nt, Kpo = nt * KT, nch = (nt + FT - 1) / FT;
     if (cw == 0) ETRACE(0, op, wall_clock64());
     const int st = o.scale_t, ssz = st == kScaleF32 ? 4 : 2;
     int v0, nv;
@@ -348,16 +400,16 @@ __global__ __launch_bounds__(kEngThreads, 1) void woq_engine_kernel(const EngOp*
     int my_n = -1;
     {
       const int oi = cl;
-      if (oi < nout && o.epi == kEpiResAdd) {
+      if (oi < nout && o_epi == kEpiResAdd) {
         int wsel, sx;
         vstripe(o, v0 + (oi >> 4) * vpu, wsel, sx);
         const int n = sx * 16 + (oi & 15);
-        if (n < sel3(wsel, o.w[0].n, o.w[1].n, o.w[2].n)) {
+        if (n < sel3(wsel, wn0, wn1, wn2)) {
           my_n = n;
-          if (o.res_gran)
-            res_g = __hip_atomic_load(o.res_gran + n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (o_res_gran)
+            res_g = __hip_atomic_load(o_res_gran + n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           else
-            res_v = o.res[n];
+            res_v = o_res[n];
         }
       }
     }
@@ -368,14 +420,14 @@ __global__ __launch_bounds__(kEngThreads, 1) void woq_engine_kernel(const EngOp*
     float s2 = 0.f;
     {
       const int npair = (K + 1) / 2;  // granule / element pairs: one 16-B (8-B external) load per pair
-      const bool gw = o.norm && o.norm_w;
+      const bool gw = o_norm && o_norm_w;
       float sq[PJ];  // per-slot squares, summed in slot order once the pass is complete (arrival order varies)
       auto put = [&](int j, int q, float x0, float x1) {
         // explicit fma: put() is inlined at two call sites, and hipcc's fp contraction may differ between them
         sq[j] = __builtin_fmaf(x1, x1, x0 * x0);
         if (gw) {
-          x0 *= o.norm_w[2 * q];
-          x1 *= 2 * q + 1 < K ? o.norm_w[2 * q + 1] : 0.f;
+          x0 *= o_norm_w[2 * q];
+          x1 *= 2 * q + 1 < K ? o_norm_w[2 * q + 1] : 0.f;
         }
         h2_t hi, lo;
         hi[0] = _Float16(x0);
@@ -386,9 +438,9 @@ __global__ __launch_bounds__(kEngThreads, 1) void woq_engine_kernel(const EngOp*
         *reinterpret_cast<h2_t*>(pu) = hi;
         *reinterpret_cast<h2_t*>(pu + 16) = lo;
       };
-      if (o.act_gran) {
-        const unsigned want = gen * 256u + o.act_tag;
-        const auto rg = rsrc(o.act_gran, unsigned(K) * 8u);
+      if (o_act_gran) {
+        const unsigned want = gen * 256u + o_act_tag;
+        const auto rg = rsrc(o_act_gran, unsigned(K) * 8u);
         for (int q0 = 0; q0 < npair; q0 += NC * 64 * PJ) {
           uint32_t pend = 0;
 #pragma unroll
@@ -426,7 +478,7 @@ __global__ __launch_bounds__(kEngThreads, 1) void woq_engine_kernel(const EngOp*
           for (int j = 0; j < PJ; j++) s2 += sq[j];
         }
       } else {  // an external vector (written before this launch): plain loads, all of a pass in flight at once
-        const auto ra = rsrc(o.act, unsigned(K) * 4u);
+        const auto ra = rsrc(o_act, unsigned(K) * 4u);
         for (int q0 = 0; q0 < npair; q0 += NC * 64 * PJ) {
           uint2 g[PJ];
 #pragma unroll
@@ -454,7 +506,7 @@ __global__ __launch_bounds__(kEngThreads, 1) void woq_engine_kernel(const EngOp*
       }
     }
     if (cw == 0) ETRACE(1, op, wall_clock64());
-    if (o.norm) {
+    if (o_norm) {
 #pragma unroll
       for (int sh = 32; sh > 0; sh >>= 1) s2 += __shfl_xor(s2, sh, 64);
       if (lane == 0) nsum[cw] = s2;
@@ -465,11 +517,11 @@ __global__ __launch_bounds__(kEngThreads, 1) void woq_engine_kernel(const EngOp*
     // 1 / rms of the input, read right after the barrier: the next op's partial sums overwrite nsum as soon as a
     // consumer has passed this op's post-loop barrier
     float inv = 1.f;
-    if (o.norm) {
+    if (o_norm) {
       float tot = 0.f;
 #pragma unroll
       for (int w = 0; w < NC; w++) tot += nsum[w];
-      inv = 1.f / sqrtf(tot / float(K) + o.norm_eps);
+      inv = 1.f / sqrtf(tot / float(K) + o_norm_eps);
     }
 
     // 2) the weight stream: consumer cw takes tiles cw and cw + 8 of every fill.  One LDS round trip per fill: the FULL
@@ -503,34 +555,54 @@ __global__ __launch_bounds__(kEngThreads, 1) void woq_engine_kernel(const EngOp*
             zpa[h][g] = sb + FT * 1024 + SD * 1024 + ((gi * 16 + m) & ~3);
           }
         }
+#if defined(NAD_EXP_NOOPS) || defined(NAD_EXP_NOACT)
+        u4_t bq[TPC] = {};
+        h8_t af[TPC][SPT] = {};
+#else
         u4_t bq[TPC];
         h8_t af[TPC][SPT];
+#endif
         uint32_t scw[TPC][GPT], zpw[TPC][GPT];
         unsigned full;
 #ifdef NAD_CHAIN_TRACE
         const unsigned long long tf0 = wall_clock64();
 #endif
-        for (unsigned spins = 0;; spins++) {
-          asm volatile("ds_read_b32 %0, %1" : "=v"(full) : "v"(full_a + slot * 4) : "memory");
+        // every operand of both tiles in one round trip with the FULL word: one LDS round trip per fill when it has
+        // landed.  If it has not, poll the FULL word alone (an operand re-read per poll by 8 waves saturates the LDS
+        // and starves the loader's DMA writes), then read the operands once more.
+        auto rd_ops = [&]() {
 #pragma unroll
           for (int h = 0; h < TPC; h++) {
             const uint32_t tb = sb + (cw + h * NC) * 1024 + lane * 16;
+#ifdef NAD_EXP_NOOPS  // timing experiment: no operand reads at all (wrong results)
+            continue;
+#endif
             asm volatile("ds_read_b128 %0, %1" : "=v"(bq[h]) : "v"(tb) : "memory");
+#ifndef NAD_EXP_NOACT  // timing experiment: no activation reads (wrong results)
 #pragma unroll
             for (int d = 0; d < SPT; d++) asm volatile("ds_read_b128 %0, %1" : "=v"(af[h][d]) : "v"(ab[h] + d * 128) : "memory");
+#endif
 #pragma unroll
             for (int g = 0; g < GPT; g++) {
               asm volatile("ds_read_b32 %0, %1" : "=v"(scw[h][g]) : "v"(sca[h][g]) : "memory");
               if constexpr (ASYM) asm volatile("ds_read_b32 %0, %1" : "=v"(zpw[h][g]) : "v"(zpa[h][g]) : "memory");
             }
           }
-          asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(full) : : "memory");  // full is defined here, not at its load
-          if (__builtin_amdgcn_readfirstlane(full) >= unsigned(f + 1) || failed) break;
-          __builtin_amdgcn_s_sleep(1);
-          if (spins > kSpinMax) {
-            if (lane == 0) give_up(ctl, 1);
-            failed = true;
+        };
+        asm volatile("ds_read_b32 %0, %1" : "=v"(full) : "v"(full_a + slot * 4) : "memory");
+        rd_ops();
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(full) : : "memory");  // full is defined here, not at its load
+        if (__builtin_amdgcn_readfirstlane(full) < unsigned(f + 1) && !failed) {
+          for (unsigned spins = 0;; spins++) {
+            __builtin_amdgcn_s_sleep(1);
+            if (lds_ld(full_a + slot * 4) >= unsigned(f + 1) || failed) break;
+            if (spins > kSpinMax) {
+              if (lane == 0) give_up(ctl, 1);
+              failed = true;
+            }
           }
+          rd_ops();
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         }
 #pragma unroll
         for (int h = 0; h < TPC; h++) {  // registers are defined by the wait above: pin every use below it
@@ -593,6 +665,7 @@ __global__ __launch_bounds__(kEngThreads, 1) void woq_engine_kernel(const EngOp*
       if (lane < 16) part[(jl * NC + cw) * 16 + lane] = r;
     }
     if (cw == 0) ETRACE(4, op, wall_clock64());
+    ETRACE(12 + cw, op, wall_clock64());  // every consumer's loop end (slots 12..19)
 #ifdef NAD_CHAIN_TRACE
     if (cw == 0) ETRACE(9, op, tr_fw);
 #endif
@@ -600,7 +673,7 @@ __global__ __launch_bounds__(kEngThreads, 1) void woq_engine_kernel(const EngOp*
     if (cw == 0) ETRACE(10, op, wall_clock64());
 
     // 3) sum the consumers' partials in a fixed order, RMS scale, epilogue, results + granules
-    const unsigned tag = gen * 256u + o.tag;
+    const unsigned tag = gen * 256u + o_tag;
     for (int oi = cl; oi < nout; oi += NC * 64) {
       const int p = oi >> 4, nn = oi & 15;
       float y[2] = {0.f, 0.f};
@@ -614,18 +687,18 @@ __global__ __launch_bounds__(kEngThreads, 1) void woq_engine_kernel(const EngOp*
       int wsel, sx;
       vstripe(o, v0 + p * vpu, wsel, sx);
       const int n = sx * 16 + nn;
-      if (n >= sel3(wsel, o.w[0].n, o.w[1].n, o.w[2].n)) continue;
-      float* const w_out = sel3(wsel, o.w[0].out, o.w[1].out, o.w[2].out);
-      unsigned long long* const w_gran = sel3(wsel, o.w[0].gran, o.w[1].gran, o.w[2].gran);
+      if (n >= sel3(wsel, wn0, wn1, wn2)) continue;
+      float* const w_out = sel3(wsel, wo0, wo1, wo2);
+      unsigned long long* const w_gran = sel3(wsel, wg0, wg1, wg2);
       float val = y[0];
-      if (o.epi == kEpiResAdd) {
-        if (o.res_gran) {
-          const unsigned want = gen * 256u + o.res_tag;
+      if (o_epi == kEpiResAdd) {
+        if (o_res_gran) {
+          const unsigned want = gen * 256u + o_res_tag;
           unsigned spins = 0;
           unsigned long long x = res_g;
           while (unsigned(x >> 32) != want && !failed) {  // the early load normally already holds it
             __builtin_amdgcn_s_sleep(1);
-            x = __hip_atomic_load(o.res_gran + n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            x = __hip_atomic_load(o_res_gran + n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (++spins > kSpinMax) {
               give_up(ctl, 4);
               failed = true;
@@ -634,9 +707,9 @@ __global__ __launch_bounds__(kEngThreads, 1) void woq_engine_kernel(const EngOp*
           res_v = __uint_as_float(unsigned(x));
         }
         val += res_v;
-      } else if (o.epi == kEpiSiluMul || o.epi == kEpiGeluMul) {
-        const float t1 = o.epi == kEpiSiluMul ? silu_f(y[0]) : gelu_f(y[0]);
-        if (o.aux) o.aux[n] = t1;
+      } else if (o_epi == kEpiSiluMul || o_epi == kEpiGeluMul) {
+        const float t1 = o_epi == kEpiSiluMul ? silu_f(y[0]) : gelu_f(y[0]);
+        if (o_aux) o_aux[n] = t1;
         val = t1 * y[1];
       }
       if (w_out) w_out[n] = val;
@@ -665,8 +738,8 @@ bool engine_geometry(EngGeometry& g, int kp) {
   if (fixed >= budget) return false;
   int s = int((budget - fixed) / g.slot_bytes);
   if (s > 16) s = 16;
-  const int ipf = kEngFillTiles + g.sd + (g.asym ? 1 : 0);
-  if (s < 63 / ipf + 2) return false;  // D fills in flight + at least two published ones for the consumers
+  if (g.loaders < 1 || g.loaders > kEngMaxLoaders || g.depth < 1 || g.depth > 2) return false;
+  if (s < g.loaders * g.depth + 2) return false;  // fills in flight + at least two published ones for the consumers
   g.slots = s;
   g.lds = fixed + size_t(s) * g.slot_bytes;
   return true;
@@ -683,8 +756,8 @@ static hipError_t engine_launch4(const EngOp* ops, int n_ops, const EngGeometry&
     if (e != hipSuccess) return e;
     attr = true;
   }
-  hipLaunchKernelGGL(k, dim3(grid), dim3(kEngThreads), g.lds, st, ops, n_ops, ctl, g.slots, int(g.slot_bytes), g.kp,
-                     bump, g.thin);
+  hipLaunchKernelGGL(k, dim3(grid), dim3((kEngConsumers + g.loaders) * 64), g.lds, st, ops, n_ops, ctl, g.slots,
+                     int(g.slot_bytes), g.kp, bump, g.thin, g.loaders, g.depth);
   return hipGetLastError();
 }
 

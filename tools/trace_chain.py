@@ -10,7 +10,7 @@ import os
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-os.environ["NAD_LIB_PATH"] = os.path.join(REPO, "neural_amd", "libneural_amd_chaintrace.so")
+os.environ["NAD_LIB_PATH"] = os.environ.get("NAD_LIB_PATH") or os.path.join(REPO, "neural_amd", "libneural_amd_chaintrace.so")
 sys.path.insert(0, REPO)
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
@@ -34,7 +34,7 @@ if mode == "cut":
         for _ in range(3):
             ch.run()
         torch.cuda.synchronize()
-        buf = np.zeros((14, 160, 256), np.uint64)
+        buf = np.zeros((20, 160, 256), np.uint64)
         ch.run()
         assert L.nad_chain_trace_fetch(buf.ctypes.data, buf.nbytes) == 0
         nops = ch.n_ops if hasattr(ch, "n_ops") else len(ch._ops)
@@ -54,13 +54,15 @@ if mode == "cut":
                      fullwait=np.median(x[9]) * tick,
                      freewait=np.median(x[8]) * tick, start=(x[0].min() - t0) * tick,
                      end=(x[5].max() - t0) * tick, endskew=(x[5].max() - x[5].min()) * tick)
+            lag = [np.median(x[12 + c] - x[12]) * tick for c in range(8)]
             print("  " + kinds[op].ljust(8) + " ".join(f"{k} {v:6.2f}" for k, v in d.items()), flush=True)
+            print("           loop end vs consumer 0: " + " ".join(f"{v:5.2f}" for v in lag), flush=True)
 else:
     ch = cr.chains[0]
     for _ in range(3):
         ch.run()
     torch.cuda.synchronize()
-    buf = np.zeros((14, 160, 256), np.uint64)
+    buf = np.zeros((20, 160, 256), np.uint64)
     ch.run()
     assert L.nad_chain_trace_fetch(buf.ctypes.data, buf.nbytes) == 0
     b = buf.astype(np.int64)
