@@ -51,7 +51,7 @@ namespace eng {
 
 // Development instrumentation (make chaintrace): per-(op, workgroup) wall-clock stamps of the engine's phases.
 #ifdef NAD_CHAIN_TRACE
-constexpr int kTrOps = 160, kTrWg = 256, kTrSlots = 20;
+constexpr int kTrOps = 160, kTrWg = 256, kTrSlots = 22;
 __device__ unsigned long long nad_chain_trace[kTrSlots][kTrOps][kTrWg];
 #define ETRACE(slot, opi, val)                                                                     \
   do {                                                                                             \
@@ -719,6 +719,12 @@ __global__ __launch_bounds__(kEngMaxThreads, 1) void woq_engine_kernel(const Eng
     }
     (void)my_n;
     if (cw == 0) ETRACE(5, op, wall_clock64());
+#ifdef NAD_CHAIN_TRACE
+    if (cw == 0) {  // development: how long the published stores take to complete (delays wave 0 only)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      ETRACE(20, op, wall_clock64());
+    }
+#endif
   }
   // the launch generation moves on once this workgroup is done: every workgroup read it before publishing anything,
   // and workgroup 0 got here only after gathering results of every workgroup (bump is set only when an op reads a

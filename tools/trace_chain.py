@@ -34,7 +34,7 @@ if mode == "cut":
         for _ in range(3):
             ch.run()
         torch.cuda.synchronize()
-        buf = np.zeros((20, 160, 256), np.uint64)
+        buf = np.zeros((22, 160, 256), np.uint64)
         ch.run()
         assert L.nad_chain_trace_fetch(buf.ctypes.data, buf.nbytes) == 0
         nops = ch.n_ops if hasattr(ch, "n_ops") else len(ch._ops)
@@ -56,13 +56,14 @@ if mode == "cut":
                      end=(x[5].max() - t0) * tick, endskew=(x[5].max() - x[5].min()) * tick)
             lag = [np.median(x[12 + c] - x[12]) * tick for c in range(8)]
             print("  " + kinds[op].ljust(8) + " ".join(f"{k} {v:6.2f}" for k, v in d.items()), flush=True)
-            print("           loop end vs consumer 0: " + " ".join(f"{v:5.2f}" for v in lag), flush=True)
+            print("           loop end vs consumer 0: " + " ".join(f"{v:5.2f}" for v in lag) +
+                  f"   stores done after publish: {np.median(x[20] - x[5]) * tick:5.2f}", flush=True)
 else:
     ch = cr.chains[0]
     for _ in range(3):
         ch.run()
     torch.cuda.synchronize()
-    buf = np.zeros((20, 160, 256), np.uint64)
+    buf = np.zeros((22, 160, 256), np.uint64)
     ch.run()
     assert L.nad_chain_trace_fetch(buf.ctypes.data, buf.nbytes) == 0
     b = buf.astype(np.int64)
