@@ -1383,6 +1383,10 @@ extern "C" void* nad_chain_create(const nad_chain_op* ops, int n_ops, int m) {
   g.thin = env_int("NAD_ENGINE_THIN", 0);  // measured slower on every edge (trace_chain.py): off
   g.loaders = env_int("NAD_ENGINE_LOADERS", 2);  // loader waves (tools/dma_probe.hip: 2 x 2 fills in flight best)
   g.depth = env_int("NAD_ENGINE_DEPTH", 1);      // fills in flight per loader wave (1 measured faster than 2)
+  // consumer arithmetic: fp16 hi + lo (default) or the int8-limb form (woq_chain.hip X8, NAD_ENGINE_X8=1): X8 streams
+  // the weights 22-25 % faster per tile but stages each input 0.6-1.1 us slower, which is on every hand-off's critical
+  // path -- measured 3-10 % slower per token
+  g.x8 = env_int("NAD_ENGINE_X8", 0) ? 1 : 0;
   g.sd = int((sd_bytes + 1023) / 1024);
   if (g.sd < 1) g.sd = 1;
   if (g.sd > 2 || !engine_geometry(g, kp)) {
