@@ -51,6 +51,7 @@ constexpr int kEngMaxThreads = (kEngConsumers + kEngMaxLoaders) * 64;
 constexpr int kEngFillTiles = 16;
 constexpr int kEngMaxStripes = 16;   // virtual stripes of one op per workgroup (partial-sum slots)
 constexpr int kEngMaxK = 16384;      // input length (gather registers)
+constexpr int kEngZeroBytes = 1024;  // LDS zero rows for a ragged fill's missing tile (one int2 tile's fp16 hi/lo rows)
 
 struct EngGeometry {
   int bits, gpt, asym, sd;      // kernel instantiation: bits 4 / 2, groups per tile 1 / 2 / 4, scale DMAs per fill

@@ -72,8 +72,8 @@ constexpr int kOOB = 0x7FFF0000;            // buffer offset past every resource
 constexpr int kSC1 = 16;                    // buffer-load aux: sc1 (bypass this CU's L1)
 constexpr int kNT = 2;                      // buffer-load aux: non-temporal (weights, read once per token)
 constexpr unsigned kSpinMax = 1u << 24;     // ~1 s of s_sleep(1) polls
-// LDS control words (u32 index): FULL[16], FREE[16], consumer barrier, RMS partial sums[8], gather phase
-constexpr int kFull = 0, kFree = 16, kBar = 32, kNsum = 36, kPhase = 44, kCtlBytes = 192;
+// LDS control words (u32 index): FULL[16], FREE[16], consumer barrier, RMS partial sums[2][8], gather phase
+constexpr int kFull = 0, kFree = 16, kBar = 32, kNsum = 36, kPhase = 52, kCtlBytes = 256;
 constexpr int kPartBytes = kEngMaxStripes * NC * 16 * 4;
 
 typedef __attribute__((address_space(3))) void lds_void_t;
@@ -402,8 +402,10 @@ __global__ __launch_bounds__(kEngMaxThreads, 1) void woq_engine_kernel(const Eng
   float* part = reinterpret_cast<float*>(smem + kCtlBytes);          // [stripe][consumer][16]
   // fp16: [Kp / 8] units of {hi[8], lo[8]}; X8: the limb image (3 Kp bytes) + the block scales S_b 2^-14 (Kp / 128)
   char* act = smem + kCtlBytes + kPartBytes;
-  char* ring = act + (X8 ? size_t(x8_act_bytes(Kp)) : size_t(Kp) * 4);
+  char* zrows = act + (X8 ? size_t(x8_act_bytes(Kp)) : size_t(Kp) * 4);  // kEngZeroBytes of zeros (never written)
+  char* ring = zrows + kEngZeroBytes;
   if (threadIdx.x < kCtlBytes / 4) reinterpret_cast<unsigned*>(smem)[threadIdx.x] = 0u;
+  if (threadIdx.x < kEngZeroBytes / 4) reinterpret_cast<unsigned*>(zrows)[threadIdx.x] = 0u;
   __syncthreads();
   if (wave >= NC) {
     const int lw = wave - NC;
@@ -430,6 +432,7 @@ __global__ __launch_bounds__(kEngMaxThreads, 1) void woq_engine_kernel(const Eng
   // this lane's A operand: MFMA rows 0-7 read hi, rows 8-15 lo (rows 0 and 8 are the result); k unit u = k / 8 at byte
   // 32 u (+16: lo), so step d of tile t starts at byte t * KT * 4 + d * 128 + kq * 32
   const uint32_t a_lane = lds_addr(act) + (m >= 8 ? 16 : 0) + kq * 32;
+  const uint32_t zrow_lane = lds_addr(zrows) + (m >= 8 ? 16 : 0) + kq * 32;
   const uint32_t ring_a = lds_addr(ring);
   int f = 0, slot = 0;
 
@@ -483,28 +486,31 @@ __global__ __launch_bounds__(kEngMaxThreads, 1) void woq_engine_kernel(const Eng
     //    x * g here and the scalar 1 / rms(x) on the results (y = W (x * g) / rms: the same products, no second pass)
     float s2 = 0.f;
     if constexpr (X8) {
-      // 1') the input vector as int8 limbs (see x8_quad): each lane takes quads of four elements (two pairs = two
-      //     granule loads), one 32-lane half-wave exactly one 128-k block, so the block's amax is a half-wave reduction
-      constexpr int QJ = 4;
-      const int npair = (K + 1) / 2, nquad = Kpo / 4;
+      // 1') this consumer's tiles of the input as int8 limbs (see x8_quad): each lane takes quads of four elements (two
+      //     pairs = two granule loads), one 32-lane half-wave exactly one 128-k block, so the block's amax is a
+      //     half-wave reduction; like the fp16 form, a consumer stages exactly the tiles it reads (no barrier)
+      constexpr int QJ = 4, QPT = KT / 4;  // quads per lane per pass, quads per tile
+      constexpr float kMagic = 12582912.f;  // 1.5 * 2^23: RN(v + kMagic) holds rint(v) in its low mantissa bits
+      const int npair = (K + 1) / 2;
+      const int nqc = (nt > cw ? (nt - cw + NC - 1) / NC : 0) * QPT;  // this consumer's quads
       const bool gw = o_norm && o_norm_w;
       float* sblk = reinterpret_cast<float*>(act + 3 * Kp);
-      for (int q0 = 0; q0 < nquad; q0 += NC * 64 * QJ) {
-        int qa[QJ], qb[QJ];
+      for (int i0 = 0; i0 < nqc; i0 += 64 * QJ) {
+        int qa[QJ], qb[QJ], qi[QJ];
         uint32_t off[QJ];
         float xv[QJ][4];  // byte order: x[2 qa], x[2 qb], x[2 qa + 1], x[2 qb + 1]
+        float nw[QJ][4];  // RMSNorm weights, loaded before the input arrives (not a round trip after it)
 #pragma unroll
         for (int j = 0; j < QJ; j++) {
-          x8_quad<BITS>(q0 + cl + NC * 64 * j, qa[j], qb[j], off[j]);
-#pragma unroll
-          for (int e = 0; e < 4; e++) xv[j][e] = 0.f;
-        }
-        float nw[QJ][4];  // RMSNorm weights of the quads, loaded before the input arrives (not a round trip after it)
-#pragma unroll
-        for (int j = 0; j < QJ; j++) {
+          const int i = i0 + lane + 64 * j;
+          qi[j] = i < nqc ? (cw + NC * (i / QPT)) * QPT + (i % QPT) : -1;
+          x8_quad<BITS>(max(qi[j], 0), qa[j], qb[j], off[j]);
           const int ks[4] = {2 * qa[j], 2 * qb[j], 2 * qa[j] + 1, 2 * qb[j] + 1};
 #pragma unroll
-          for (int e = 0; e < 4; e++) nw[j][e] = gw && ks[e] < K ? o_norm_w[ks[e]] : 0.f;
+          for (int e = 0; e < 4; e++) {
+            xv[j][e] = 0.f;
+            nw[j][e] = gw && qi[j] >= 0 && ks[e] < K ? o_norm_w[ks[e]] : 0.f;
+          }
         }
         auto take = [&](int j, int side, float x0, float x1) {  // side 0: pair qa, 1: pair qb
           xv[j][side] = x0;
@@ -516,7 +522,7 @@ __global__ __launch_bounds__(kEngMaxThreads, 1) void woq_engine_kernel(const Eng
           uint32_t pend = 0;
 #pragma unroll
           for (int j = 0; j < QJ; j++) {
-            if (q0 + cl + NC * 64 * j < nquad) {
+            if (qi[j] >= 0) {
               if (qa[j] < npair) pend |= 1u << (2 * j);
               if (qb[j] < npair) pend |= 2u << (2 * j);
             }
@@ -540,7 +546,7 @@ __global__ __launch_bounds__(kEngMaxThreads, 1) void woq_engine_kernel(const Eng
                 pend &= ~(1u << j);
               }
             }
-            if (cw == 0 && spins == 0 && q0 == 0) ETRACE(11, op, wall_clock64());  // first pass returned
+            if (cw == 0 && spins == 0 && i0 == 0) ETRACE(11, op, wall_clock64());  // first pass returned
             if (__all(pend == 0u) || failed) break;
             __builtin_amdgcn_s_sleep(1);
             if (++spins > kSpinMax) {
@@ -554,11 +560,11 @@ __global__ __launch_bounds__(kEngMaxThreads, 1) void woq_engine_kernel(const Eng
 #pragma unroll
           for (int j = 0; j < 2 * QJ; j++) {
             const int q = (j & 1) ? qb[j >> 1] : qa[j >> 1];
-            const bool in = q0 + cl + NC * 64 * (j >> 1) < nquad && q < npair;
+            const bool in = qi[j >> 1] >= 0 && q < npair;
             g[j] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(ra, in ? q * 8 : kOOB, 0, 0));
           }
           __builtin_amdgcn_sched_barrier(0);
-          if (cw == 0 && q0 == 0) ETRACE(11, op, wall_clock64());
+          if (cw == 0 && i0 == 0) ETRACE(11, op, wall_clock64());
 #pragma unroll
           for (int j = 0; j < 2 * QJ; j++) {
             const int q = (j & 1) ? qb[j >> 1] : qa[j >> 1];
@@ -569,7 +575,8 @@ __global__ __launch_bounds__(kEngMaxThreads, 1) void woq_engine_kernel(const Eng
         // the pass is complete: squares in slot order, then the limbs of every quad
 #pragma unroll
         for (int j = 0; j < QJ; j++) {
-          if (q0 + cl + NC * 64 * j >= nquad) continue;  // whole half-waves (nquad is a multiple of 32)
+          if (i0 + 64 * j >= nqc) break;  // whole half-waves (nqc is a multiple of 32)
+          if (qi[j] < 0) continue;
           float* x = xv[j];
           s2 += __builtin_fmaf(x[3], x[3], __builtin_fmaf(x[2], x[2], __builtin_fmaf(x[1], x[1], x[0] * x[0])));
           if (gw) {
@@ -577,22 +584,26 @@ __global__ __launch_bounds__(kEngMaxThreads, 1) void woq_engine_kernel(const Eng
             for (int e = 0; e < 4; e++) x[e] *= nw[j][e];
           }
           const float amax = max32(fmaxf(fmaxf(fabsf(x[0]), fabsf(x[1])), fmaxf(fabsf(x[2]), fabsf(x[3]))));
-          const float inv = amax > 0.f ? 127.f / amax : 0.f;
-          int a[kX8Rows][4];
+          const float inv = amax > 0.f ? 127.f * __builtin_amdgcn_rcpf(amax) : 0.f;
+          // limbs by magic-number rounding: t = RN(v + kMagic) carries rint(v) in its low byte (two's complement),
+          // t - kMagic is that integer exactly, and one fma gives the next residual
+          uint32_t t[kX8Rows][4];
 #pragma unroll
           for (int e = 0; e < 4; e++) {
-            const float r = x[e] * inv;
-            const float l0 = rintf(r), d1 = (r - l0) * 128.f;
-            const float l1 = rintf(d1), d2 = (d1 - l1) * 128.f;
-            a[0][e] = int(l0);
-            a[1][e] = int(l1);
-            a[2][e] = int(rintf(d2));
+            const float t0 = __builtin_fmaf(x[e], inv, kMagic);
+            const float r1 = __builtin_fmaf(x[e], inv, -(t0 - kMagic));
+            const float t1 = __builtin_fmaf(r1, 128.f, kMagic);
+            const float r2 = __builtin_fmaf(r1, 128.f, -(t1 - kMagic));
+            t[0][e] = __float_as_uint(t0);
+            t[1][e] = __float_as_uint(t1);
+            t[2][e] = __float_as_uint(__builtin_fmaf(r2, 128.f, kMagic));
           }
           char* base = act + off[j];
 #pragma unroll
           for (int row = 0; row < kX8Rows; row++)
-            *reinterpret_cast<uint32_t*>(base + row * 64) = pack4(a[row][0], a[row][1], a[row][2], a[row][3]);
-          if ((lane & 31) == 0) sblk[(q0 + cl + NC * 64 * j) >> 5] = amax * (1.f / 127.f) * (1.f / 16384.f);
+            *reinterpret_cast<uint32_t*>(base + row * 64) = __builtin_amdgcn_perm(t[row][1], t[row][0], 0x0c0c0400u) |
+                                                             __builtin_amdgcn_perm(t[row][3], t[row][2], 0x04000c0cu);
+          if ((lane & 31) == 0) sblk[qi[j] >> 5] = amax * (1.f / 127.f) * (1.f / 16384.f);
         }
       }
     } else {
@@ -683,23 +694,19 @@ __global__ __launch_bounds__(kEngMaxThreads, 1) void woq_engine_kernel(const Eng
       }
     }
     if (cw == 0) ETRACE(1, op, wall_clock64());
+    // per-consumer sums of squares, double-buffered by op parity: they are read after this op's post-stream barrier,
+    // and no consumer can write this parity again before every consumer has passed the next op's one
+    float* const nsum_op = nsum + (op & 1) * NC;
     if (o_norm) {
 #pragma unroll
       for (int sh = 32; sh > 0; sh >>= 1) s2 += __shfl_xor(s2, sh, 64);
-      if (lane == 0) nsum[cw] = s2;
+      if (lane == 0) nsum_op[cw] = s2;
     }
-    cbar(bar_a, bar_epoch, ctl, lane, failed);
+    // fp16: every consumer staged a share of the whole vector, so all meet before the stream.  (Staging only the
+    // consumer's own tiles with no barrier measured 2-3 % slower per whole-token launch; X8 does that.)
+    if constexpr (!X8) cbar(bar_a, bar_epoch, ctl, lane, failed);
     if (thin && cw == 0 && lane == 0) lds_st(ctl_a + kPhase * 4, 0u);
     if (cw == 0) ETRACE(2, op, wall_clock64());
-    // 1 / rms of the input, read right after the barrier: the next op's partial sums overwrite nsum as soon as a
-    // consumer has passed this op's post-loop barrier
-    float inv = 1.f;
-    if (o_norm) {
-      float tot = 0.f;
-#pragma unroll
-      for (int w = 0; w < NC; w++) tot += nsum[w];
-      inv = 1.f / sqrtf(tot / float(K) + o_norm_eps);
-    }
 
     // 2) the weight stream: consumer cw takes tiles cw and cw + 8 of every fill.  One LDS round trip per fill: the FULL
     //    word and every operand of both tiles are read together (a wave's LDS reads complete in order, and the loader
@@ -715,6 +722,7 @@ __global__ __launch_bounds__(kEngMaxThreads, 1) void woq_engine_kernel(const Eng
       constexpr int NBLK = KT / 128;
       static_assert(GPT == 1 || GPT == NSEG, "segments are the groups of a tile when a tile holds several");
       const uint32_t a8_lane = lds_addr(act) + uint32_t(min(m & 3, kX8Rows - 1) * 64 + kq * 16);
+      const uint32_t z8_lane = lds_addr(zrows) + uint32_t(min(m & 3, kX8Rows - 1) * 64 + kq * 16);
       const uint32_t sblk_a = lds_addr(act) + uint32_t(3 * Kp);
       const uint32_t bsym = BITS == 4 ? 0xF8F8F8F8u : 0xFEFEFEFEu;  // splat(-bias)
       for (int jl = 0; jl < nv; jl++) {
@@ -751,7 +759,8 @@ __global__ __launch_bounds__(kEngMaxThreads, 1) void woq_engine_kernel(const Eng
             for (int h = 0; h < TPC; h++) {
               const uint32_t tb = sb + (cw + h * NC) * 1024 + lane * 16;
               if (h > 0 || !skip_first_tile) asm volatile("ds_read_b128 %0, %1" : "=v"(bq[h]) : "v"(tb) : "memory");
-              const uint32_t ab = a8_lane + uint32_t(tt[h] * 3 * KT);
+              // a ragged last fill's missing tile reads zero rows (tile nt - 1 belongs to another consumer)
+              const uint32_t ab = valid[h] ? a8_lane + uint32_t(tt[h] * 3 * KT) : z8_lane;
 #pragma unroll
               for (int u = 0; u < NU; u++) asm volatile("ds_read_b128 %0, %1" : "=v"(ax[h][u]) : "v"(ab + u * 192) : "memory");
 #pragma unroll
@@ -838,7 +847,9 @@ __global__ __launch_bounds__(kEngMaxThreads, 1) void woq_engine_kernel(const Eng
             for (int h = 0; h < TPC; h++) {
               // rows 0..2 of column m (lanes 0..15): the limb dot products, exact; they meet once per segment
               const float fsum = __builtin_fmaf(float(ai[h][0]), 16384.f, __builtin_fmaf(float(ai[h][1]), 128.f, float(ai[h][2])));
-              accf = __builtin_fmaf(fsum, scf[h][g] * __uint_as_float(sbw[h][(sg * UPS) / 2]), accf);
+              // (a missing tile's block scale belongs to another consumer's stale rows: select, do not multiply)
+              const float sc = valid[h] ? scf[h][g] * __uint_as_float(sbw[h][(sg * UPS) / 2]) : 0.f;
+              accf = __builtin_fmaf(fsum, sc, accf);
             }
           }
           f++;
@@ -862,7 +873,9 @@ __global__ __launch_bounds__(kEngMaxThreads, 1) void woq_engine_kernel(const Eng
           const int p = cw + h * NC, t = t0 + p;
           valid[h] = t < nt;
           tt[h] = min(t, nt - 1);
-          ab[h] = a_lane + uint32_t(tt[h]) * KT * 4;
+          // a ragged last fill's missing tile reads the zero rows (tile nt - 1's rows belong to another consumer, staged
+          // with no barrier in between: stale bits there could be a NaN, which a zero scale does not cancel)
+          ab[h] = (valid[h] ? a_lane + uint32_t(tt[h]) * KT * 4 : zrow_lane);
 #pragma unroll
           for (int g = 0; g < GPT; g++) {
             const int gi = GPT == 1 ? (tt[h] >> o.tpg_shift) - g0 : p * GPT + g;
@@ -923,7 +936,9 @@ __global__ __launch_bounds__(kEngMaxThreads, 1) void woq_engine_kernel(const Eng
         for (int h = 0; h < TPC; h++) {  // registers are defined by the wait above: pin every use below it
           asm volatile("" : "+v"(bq[h]));
 #pragma unroll
-          for (int d = 0; d < SPT; d++) asm volatile("" : "+v"(af[h][d]));
+          for (int d = 0; d < SPT; d++) {
+            asm volatile("" : "+v"(af[h][d]));
+          }
 #pragma unroll
           for (int g = 0; g < GPT; g++) {
             asm volatile("" : "+v"(scw[h][g]));
@@ -986,6 +1001,13 @@ __global__ __launch_bounds__(kEngMaxThreads, 1) void woq_engine_kernel(const Eng
 #endif
     cbar(bar_a, bar_epoch, ctl, lane, failed);
     if (cw == 0) ETRACE(10, op, wall_clock64());
+    float inv = 1.f;  // 1 / rms of the input
+    if (o_norm) {
+      float tot = 0.f;
+#pragma unroll
+      for (int w = 0; w < NC; w++) tot += nsum_op[w];
+      inv = 1.f / sqrtf(tot / float(K) + o_norm_eps);
+    }
 
     // 3) sum the consumers' partials in a fixed order, RMS scale, epilogue, results + granules
     const unsigned tag = gen * 256u + o_tag;
@@ -1055,7 +1077,7 @@ bool engine_geometry(EngGeometry& g, int kp) {
   g.kp = (kp + 15) / 16 * 16;
   g.slot_bytes = size_t(kEngFillTiles) * 1024 + size_t(g.sd) * 1024 + (g.asym ? 1024 : 0);
   const size_t act = g.x8 ? size_t(eng::x8_act_bytes(g.kp)) : size_t(g.kp) * 4;
-  const size_t fixed = size_t(eng::kCtlBytes) + eng::kPartBytes + act;
+  const size_t fixed = size_t(eng::kCtlBytes) + eng::kPartBytes + act + kEngZeroBytes;
   const size_t budget = 160 * 1024;
   if (fixed >= budget) return false;
   int s = int((budget - fixed) / g.slot_bytes);

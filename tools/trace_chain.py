@@ -54,6 +54,9 @@ if mode == "cut":
                      fullwait=np.median(x[9]) * tick,
                      freewait=np.median(x[8]) * tick, start=(x[0].min() - t0) * tick,
                      end=(x[5].max() - t0) * tick, endskew=(x[5].max() - x[5].min()) * tick)
+            if op > 0:  # hand-off: the previous op's LAST publish (any CU) -> this CU's input gathered
+                ho = (x[1] - b[5, op - 1].max()) * tick
+                d["handoff_med"], d["handoff_max"] = np.median(ho), ho.max()
             lag = [np.median(x[12 + c] - x[12]) * tick for c in range(8)]
             print("  " + kinds[op].ljust(8) + " ".join(f"{k} {v:6.2f}" for k, v in d.items()), flush=True)
             print("           loop end vs consumer 0: " + " ".join(f"{v:5.2f}" for v in lag) +
