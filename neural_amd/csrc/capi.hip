@@ -423,6 +423,7 @@ static int prepare_gemv(GemvArgs& a, int& waves, int& grid, int& gpt_out, const 
   a.u_q = a.units / grid;
   a.u_r = a.units % grid;
   a.lean = env_int("NAD_GEMV_LEAN", 1);
+  a.valu = env_int("NAD_GEMV_VALU", 0);  // A/B: the M = 1 kernel's VALU dot-product body
   // M = 1 single-op launches may stream 2-tile K-slices, one per wave (up to 16 waves); the chain keeps 4-tile ones
   if (single_op)
     gemv_lean_slices(a, w0.bits, &waves, env_int("NAD_GEMV_WAVES", 0) > 0 ? 4 : env_int("NAD_GEMV_KS", 2));

@@ -122,6 +122,7 @@ struct GemvArgs {
   int lean;             // M = 1 int4 single-group-per-tile launches may take woq_gemv_m1_kernel (NAD_GEMV_LEAN)
   int lean_ks;          // woq_gemv_m1_kernel: K tiles per K-slice (4, or 1 / 2 where that gives each of up to 16 waves one)
   int lean_spw;         // woq_gemv_m1_kernel: K-slices per wave at most (2, or 4 for long K)
+  int valu;             // woq_gemv_m1_kernel, fp32 activations: v_dot2_f32_f16 + lane reductions instead of MFMA (A/B)
   SkinnyWeight w[3];
 };
 

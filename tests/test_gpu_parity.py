@@ -339,6 +339,34 @@ def test_gemv_m1_two_tile_slices(oracle, monkeypatch, cfg, grid):
     assert _rel_err(y2, y4) <= 1e-6
 
 
+M1_VALU = [
+    # n, k, bs, qtype, stype, ks: the M = 1 kernel's VALU body (v_dot2_f32_f16 + lane reductions; fp32 activations, sym)
+    (4096, 4096, 128, S4, F16, "2"),
+    (520, 3968, 128, S4, F16, "2"),   # K tail
+    (320, 2048, 64, S4, F32, "4"),    # 2 groups per tile, 4-tile slices
+    (1024, 4096, 64, S2, F16, "2"),   # int2 g64 (Mistral): 4 groups per tile
+    (256, 14336, 64, S4, BF16, "2"),  # long K: 4 slices per wave
+]
+
+
+@pytest.mark.parametrize("cfg", M1_VALU)
+def test_gemv_m1_valu_body(oracle, monkeypatch, cfg):
+    """NAD_GEMV_VALU=1 (the decode A/B of DESIGN.md section 4): the VALU dot-product body against the oracle (2e-5) and
+    within 1e-6 of the MFMA body (only the fp32 summation order differs)."""
+    n, k, bs, qt, st, ks = cfg
+    monkeypatch.setenv("NAD_GEMV_KS", ks)
+    blob = _blob(oracle, n, k, bs, qt, st, False, 4, seed=n + k + 1)
+    w = bestla.DeviceWeight(blob)
+    A = np.random.default_rng(k + 1).uniform(-0.5, 0.5, size=(1, k)).astype(np.float32)
+    xa = torch.from_numpy(A).cuda()
+    ref = oracle.forward(A, blob, n, k)
+    ym = w.forward(xa).cpu().numpy()
+    monkeypatch.setenv("NAD_GEMV_VALU", "1")
+    yv = w.forward(xa).cpu().numpy()
+    assert _rel_err(yv, ref) <= TOL_DECODE
+    assert _rel_err(yv, ym) <= 1e-6
+
+
 @pytest.mark.parametrize("geom", [(None, None), ("2", "3"), ("5", "16")])
 def test_gemv_stream_fused(oracle, monkeypatch, geom):
     """QKV (three weights in one stream) and the dual gate/up stream with SiLU*mul under forced geometries."""
