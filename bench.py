@@ -192,21 +192,32 @@ class ChainRunner:
         self.h = [torch.empty((1, H), **f) for _ in range(L)]
         self.t = [torch.empty((1, stack.nf), **f) for _ in range(L)]
         self.logits = torch.empty((1, stack.nv), **f)
-        ops, cuts = [], [1]
+        # O's input: V itself when it is the whole attention output (kv == hidden: softmax over one key returns V);
+        # with grouped KV heads (Mistral) the attention output is hidden-wide -- an external vector here, exactly as the
+        # per-op Runner's (the attention node between launches writes it; its work is outside the WOQ path)
+        self.o_in = self.v if stack.nkv == stack.nq else [((torch.rand((1, stack.nq), generator=g) - 0.5)).to(device)
+                                                          for _ in range(L)]
+        bits = stack.cfg["bits"]
+        ops, bounds = [], [0]
         for li, Lw in enumerate(stack.layers):
             x = self.xs[li]
-            ops.append(dict(kind=bestla.CHAIN_QKV, w=[Lw["wq"], Lw["wk"], Lw["wv"]], act=x,
-                            out=[self.q[li], self.k[li], self.v[li]], norm=True))
-            ops.append(dict(kind=bestla.CHAIN_LINEAR, w=[Lw["wo"]], act=self.v[li], out=[self.h[li]],
+            if bits["v"] == bits["q"]:
+                ops.append(dict(kind=bestla.CHAIN_QKV, w=[Lw["wq"], Lw["wk"], Lw["wv"]], act=x,
+                                out=[self.q[li], self.k[li], self.v[li]], norm=True))
+            else:  # Mistral's policy: {Q, K} int2 in one op, V int4 in its own (one format per op)
+                ops.append(dict(kind=bestla.CHAIN_QKV, w=[Lw["wq"], Lw["wk"]], act=x, out=[self.q[li], self.k[li]],
+                                norm=True))
+                ops.append(dict(kind=bestla.CHAIN_LINEAR, w=[Lw["wv"]], act=x, out=[self.v[li]], norm=True))
+            bounds.append(len(ops))   # a cut after each layer's QKV: attention follows
+            ops.append(dict(kind=bestla.CHAIN_LINEAR, w=[Lw["wo"]], act=self.o_in[li], out=[self.h[li]],
                             epi=bestla.EPI_RES_ADD, res=x))
             ops.append(dict(kind=bestla.CHAIN_GATE_UP, w=[Lw["w1"], Lw["w3"]], act=self.h[li], out=[self.t[li]],
                             norm=True))
             ops.append(dict(kind=bestla.CHAIN_LINEAR, w=[Lw["w2"]], act=self.t[li], out=[self.xs[li + 1]],
                             epi=bestla.EPI_RES_ADD, res=self.h[li]))
-            cuts.append(len(ops) + 1)
         ops.append(dict(kind=bestla.CHAIN_LINEAR, w=[stack.lm_head], act=self.xs[L], out=[self.logits], norm=True))
-        cuts[-1] = len(ops)
-        bounds = [0] + cuts if cut else [0, len(ops)]
+        # [QKV_0], then per layer [O, gate/up, down, next QKV] and [O, gate/up, down, lm_head] last
+        bounds = bounds + [len(ops)] if cut else [0, len(ops)]
         self.chains = [bestla.Chain(ops[a:b], 1) for a, b in zip(bounds, bounds[1:])]
         self.n_ops = len(ops)
         self.n_launches = len(self.chains)
@@ -280,10 +291,24 @@ def decode_workload(cfg, torch, reps=20, prefill=True, prefill_steps=2):
     t = graph_time(lambda s: run.step(), reps, torch)
     L1 = st.launches(1)
     byts = sum(b * c for _, b, _, c in L1)
-    out = {"tokens_per_s": round(1.0 / t, 2), "ms_per_token": round(t * 1e3, 4), "bytes_per_token": int(byts),
-           "roofline": {"bound": "hbm", "achieved": round(byts / t / 1e9, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                        "frac": round(byts / t / 1e9 / HBM_PEAK_GBPS, 4)},
-           "launches_per_token": sum(c for *_, c in L1)}
+    del run
+    # the same token on the weight-stream engine: cut at the attention nodes (the headline form) and as one launch
+    eng = {}
+    for cut in (True, False):
+        cr = ChainRunner(st, "cuda", cut=cut)
+        te = graph_time(lambda s: cr.step(stream=s), reps, torch)
+        assert cr.status() == 0, "decode engine hand-off timed out"
+        eng["cut" if cut else "whole"] = (te, cr.n_launches)
+        del cr
+    te, nl = eng["cut"]
+    best = min(t, te)
+    path = "per-op launches" if t <= te else f"weight-stream engine ({nl} launches per token)"
+    out = {"tokens_per_s": round(1.0 / best, 2), "ms_per_token": round(best * 1e3, 4), "bytes_per_token": int(byts),
+           "roofline": {"bound": "hbm", "achieved": round(byts / best / 1e9, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                        "frac": round(byts / best / 1e9 / HBM_PEAK_GBPS, 4)},
+           "decode_path": path, "per_op_tokens_per_s": round(1.0 / t, 2),
+           "engine_cut_tokens_per_s": round(1.0 / te, 2), "engine_whole_token_tokens_per_s": round(1.0 / eng["whole"][0], 2),
+           "launches_per_token": nl if t > te else sum(c for *_, c in L1)}
     if prefill:
         pre = Runner(st, 2048, None, "cuda")
         pre.step()
@@ -297,7 +322,7 @@ def decode_workload(cfg, torch, reps=20, prefill=True, prefill_steps=2):
         out["prefill_tflops"] = round(fl / pdt / 1e12, 2)
         out["prefill_ms_per_2048_tokens"] = round(pdt * 1e3, 3)
         del pre
-    del run, st
+    del st
     torch.cuda.empty_cache()
     return out
 

@@ -1269,7 +1269,8 @@ extern "C" void* nad_chain_create(const nad_chain_op* ops, int n_ops, int m) {
   for (int i = 0; i < n_ops; i++) {
     const nad_chain_op& o = ops[i];
     EngOp& e = host[size_t(i)];
-    const int nw = o.kind == NAD_CHAIN_QKV ? 3 : (o.kind == NAD_CHAIN_GATE_UP ? 2 : 1);
+    // QKV: three weights, or two ({Q, K} of a GQA model whose V has another format, w[2] = NULL)
+    const int nw = o.kind == NAD_CHAIN_QKV ? (o.w[2] ? 3 : 2) : (o.kind == NAD_CHAIN_GATE_UP ? 2 : 1);
     const DeviceWeight* ws[3] = {nullptr, nullptr, nullptr};
     for (int j = 0; j < nw; j++)
       if (!(ws[j] = as_weight(o.w[j]))) return nullptr;
@@ -1290,15 +1291,29 @@ extern "C" void* nad_chain_create(const nad_chain_op* ops, int n_ops, int m) {
       set_err("nad_chain_create: op %d's group size %d does not tile the K tiles", i, w0.blocksize);
       return nullptr;
     }
+    // at most two weight formats per launch (EngOp::fmt), one symmetry
+    int fmt = 0;
     if (g.bits == 0) {
-      g.bits = w0.bits;
-      g.gpt = gpt;
+      g.bits = g.bits1 = w0.bits;
+      g.gpt = g.gpt1 = gpt;
       g.asym = w0.asym;
-    } else if (g.bits != w0.bits || g.gpt != gpt || g.asym != w0.asym) {
-      set_err("nad_chain_create: op %d's format (bits %d, %d groups per tile, asym %d) differs from op 0's", i,
-              w0.bits, gpt, w0.asym);
+    } else if (g.asym != w0.asym) {
+      set_err("nad_chain_create: op %d's symmetry (asym %d) differs from op 0's", i, w0.asym);
       return nullptr;
+    } else if (g.bits != w0.bits || g.gpt != gpt) {
+      if (g.bits1 == g.bits && g.gpt1 == g.gpt) {
+        g.bits1 = w0.bits;
+        g.gpt1 = gpt;
+      }
+      if (g.bits1 != w0.bits || g.gpt1 != gpt || !engine_format_pair_ok(g.bits, g.gpt, g.bits1, g.gpt1)) {
+        set_err("nad_chain_create: op %d's format (bits %d, %d groups per tile) cannot join the launch's (bits %d / %d, "
+                "%d / %d groups per tile)", i, w0.bits, gpt, g.bits, g.bits1, g.gpt, g.gpt1);
+        return nullptr;
+      }
+      fmt = 1;
     }
+    e.fmt = fmt;
+    e.gpt = gpt;
     if (o.act_dtype != kActF32 || !o.act) {
       set_err("nad_chain_create: op %d: the engine takes fp32 activations", i);
       return nullptr;

@@ -40,6 +40,8 @@ struct EngOp {
   unsigned res_tag;
   float* aux;                   // dual: act(x.w0) (optional)
   unsigned tag;                 // this op's index in the launch + 1
+  int fmt;                      // weight format of the op: 0 = the launch's first (bits, gpt), 1 = its second
+  int gpt;                      // groups per K tile (the loader's scale pieces per fill)
 };
 
 // Engine geometry: 8 consumer waves + `loaders` loader waves (each keeping `depth` fills in flight), fills of 16 tiles
@@ -55,6 +57,7 @@ constexpr int kEngZeroBytes = 1024;  // LDS zero rows for a ragged fill's missin
 
 struct EngGeometry {
   int bits, gpt, asym, sd;      // kernel instantiation: bits 4 / 2, groups per tile 1 / 2 / 4, scale DMAs per fill
+  int bits1, gpt1;              // the second weight format of a mixed launch (= bits, gpt when there is one)
   int slots;                    // ring slots
   int kp;                       // activation row length (max over ops of nt * KT)
   size_t lds;                   // dynamic LDS bytes
@@ -68,6 +71,9 @@ struct EngGeometry {
 bool engine_geometry(EngGeometry& g, int kp);
 // ops: device array; ctl: [0] launch generation (tags), [1] status (0 ok, else the first give-up code); bump: some op
 // reads a result of this launch (the generation then moves on after the launch)
+// the (bits, groups per tile) formats one launch may hold: one of int4 g >= 128 / g64, int2 g >= 256 / g128 / g64, or the
+// mixed pairs (int2 g64, int4 g64) and (int2 g128, int4 g128)
+bool engine_format_pair_ok(int bits0, int gpt0, int bits1, int gpt1);
 hipError_t launch_engine(const EngOp* ops, int n_ops, const EngGeometry& g, unsigned* ctl, int grid, int bump,
                          hipStream_t st);
 

@@ -41,6 +41,7 @@
 
 #include <climits>
 #include <cstdint>
+#include <type_traits>
 
 #include "woq_chain.h"
 #include "woq_device.h"
@@ -152,6 +153,17 @@ __device__ __forceinline__ void fill_groups(const OpGeom& o, int t0, int& g0, in
   }
 }
 
+__device__ __forceinline__ void fill_groups_rt(const OpGeom& o, int gpt, int t0, int& g0, int& ngc) {
+  const int t1 = min(t0 + FT, o.nt);
+  if (gpt == 1) {
+    g0 = t0 >> o.tpg_shift;
+    ngc = ((t1 - 1) >> o.tpg_shift) - g0 + 1;
+  } else {
+    g0 = t0 * gpt;
+    ngc = (t1 - t0) * gpt;
+  }
+}
+
 // ------------------------------------------------------------------------------------------------ loaders
 // NL loader waves share the launch's fill sequence: loader lw issues the fills f = lw, lw + NL, ... (every loader walks
 // the whole sequence, skipping the others' fills), keeps D of its own in flight (counted vmcnt) and publishes them in
@@ -159,7 +171,7 @@ __device__ __forceinline__ void fill_groups(const OpGeom& o, int t0, int& g0, in
 // fills 19-20 GB/s per CU, 2 waves x 2 fills 27 GB/s = 6.9 TB/s chip-wide, 3 waves x 1 fill 26.6).  Slot of fill f:
 // f mod S; it is re-filled only when all consumers released fill f - S (FREE counter >= NC * (f / S)), so fills into one
 // slot stay ordered whichever loader issues them.
-template <int GPT, bool ASYM, int SD, int D>
+template <bool ASYM, int SD, int D>
 __device__ void loader(const EngOp* ops, int n_ops, char* ring, int S, int slot_bytes, uint32_t ctl_a, unsigned* ctl,
                        int lane, int thin, int lw, int NL) {
   constexpr int IPF = FT + SD + (ASYM ? 1 : 0);  // DMA instructions per fill: constant, so vmcnt counts are exact
@@ -245,7 +257,7 @@ __device__ void loader(const EngOp* ops, int n_ops, char* ring, int S, int slot_
             __builtin_amdgcn_raw_ptr_buffer_load_lds(rt, (lds_void_t*)(sb + i * 1024), 16,
                                                      t0 + i < nt ? tbase + (t0 + i) * 1024 : kOOB, 0, 0, kNT);
           int g0, ngc;
-          fill_groups<GPT>(o, t0, g0, ngc);
+          fill_groups_rt(o, od.gpt, t0, g0, ngc);
           const int sbytes = ngc * 16 * ssz, soff = (s * ng + g0) * 16 * ssz;
 #pragma unroll
           for (int j = 0; j < SD; j++) {
@@ -390,12 +402,17 @@ __device__ __forceinline__ void cbar(uint32_t a, unsigned& epoch, unsigned* ctl,
   }
 }
 
-template <int BITS, int GPT, bool ASYM, int SD, bool X8>
+template <int V>
+using IC = std::integral_constant<int, V>;
+
+// One launch holds ops of at most two weight formats (B0, G0) and (B1, G1) (bits, groups per tile; EngOp::fmt picks
+// one), e.g. Mistral's int2 g64 projections beside its int4 g64 wv / w2 (llama_utils.cpp:269-287)
+template <int B0, int G0, int B1, int G1, bool ASYM, int SD, bool X8>
 __global__ __launch_bounds__(kEngMaxThreads, 1) void woq_engine_kernel(const EngOp* __restrict__ ops, int n_ops,
                                                                        unsigned* ctl, int S, int slot_bytes, int Kp,
                                                                        int bump, int thin, int nl, int depth) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int KT = BITS == 4 ? 128 : 256, SPT = KT / 32, SPG = SPT / GPT, BIAS = BITS == 4 ? 8 : 2;
+  constexpr bool MIXED = B0 != B1 || G0 != G1;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));
   const uint32_t ctl_a = lds_addr(smem);
@@ -410,9 +427,9 @@ __global__ __launch_bounds__(kEngMaxThreads, 1) void woq_engine_kernel(const Eng
   if (wave >= NC) {
     const int lw = wave - NC;
     if (depth == 1)
-      loader<GPT, ASYM, SD, 1>(ops, n_ops, ring, S, slot_bytes, ctl_a, ctl, lane, thin, lw, nl);
+      loader<ASYM, SD, 1>(ops, n_ops, ring, S, slot_bytes, ctl_a, ctl, lane, thin, lw, nl);
     else
-      loader<GPT, ASYM, SD, 2>(ops, n_ops, ring, S, slot_bytes, ctl_a, ctl, lane, thin, lw, nl);
+      loader<ASYM, SD, 2>(ops, n_ops, ring, S, slot_bytes, ctl_a, ctl, lane, thin, lw, nl);
     return;
   }
 
@@ -428,7 +445,6 @@ __global__ __launch_bounds__(kEngMaxThreads, 1) void woq_engine_kernel(const Eng
   const int m = lane & 15, kq = lane >> 4;
   const uint32_t mk0 = 0x000F000Fu, mk1 = 0x00F000F0u, mag = 0x64006400u;
   const h2_t s16 = splat(1.f / 16.f);
-  const h2_t zc0 = splat(-(1024.f + BIAS)), zc1 = splat(-(64.f + BIAS));
   // this lane's A operand: MFMA rows 0-7 read hi, rows 8-15 lo (rows 0 and 8 are the result); k unit u = k / 8 at byte
   // 32 u (+16: lo), so step d of tile t starts at byte t * KT * 4 + d * 128 + kq * 32
   const uint32_t a_lane = lds_addr(act) + (m >= 8 ? 16 : 0) + kq * 32;
@@ -436,7 +452,11 @@ __global__ __launch_bounds__(kEngMaxThreads, 1) void woq_engine_kernel(const Eng
   const uint32_t ring_a = lds_addr(ring);
   int f = 0, slot = 0;
 
-  for (int op = 0; op < n_ops; op++) {
+  // one op, for the op's weight format (a generic lambda: the format is a compile-time constant inside)
+  auto op_body = [&](auto bits_c, auto gpt_c, int op) {
+    constexpr int BITS = decltype(bits_c)::value, GPT = decltype(gpt_c)::value;
+    constexpr int KT = BITS == 4 ? 128 : 256, SPT = KT / 32, SPG = SPT / GPT, BIAS = BITS == 4 ? 8 : 2;
+    const h2_t zc0 = splat(-(1024.f + BIAS)), zc1 = splat(-(64.f + BIAS));
     const EngOp& od = ops[op];
     const OpGeom o = op_geom(od);
     const int K = od.K;
@@ -1062,6 +1082,12 @@ __global__ __launch_bounds__(kEngMaxThreads, 1) void woq_engine_kernel(const Eng
       ETRACE(20, op, wall_clock64());
     }
 #endif
+  };
+  for (int op = 0; op < n_ops; op++) {
+    if (MIXED && ops[op].fmt)
+      op_body(IC<B1>(), IC<G1>(), op);
+    else
+      op_body(IC<B0>(), IC<G0>(), op);
   }
   // the launch generation moves on once this workgroup is done: every workgroup read it before publishing anything,
   // and workgroup 0 got here only after gathering results of every workgroup (bump is set only when an op reads a
@@ -1089,10 +1115,10 @@ bool engine_geometry(EngGeometry& g, int kp) {
   return true;
 }
 
-template <int BITS, int GPT, bool ASYM, int SD, bool X8>
+template <int B0, int G0, int B1, int G1, bool ASYM, int SD, bool X8>
 static hipError_t engine_launch5(const EngOp* ops, int n_ops, const EngGeometry& g, unsigned* ctl, int grid, int bump,
                                  hipStream_t st) {
-  auto k = eng::woq_engine_kernel<BITS, GPT, ASYM, SD, X8>;
+  auto k = eng::woq_engine_kernel<B0, G0, B1, G1, ASYM, SD, X8>;
   static bool attr = false;
   if (!attr) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1105,37 +1131,48 @@ static hipError_t engine_launch5(const EngOp* ops, int n_ops, const EngGeometry&
   return hipGetLastError();
 }
 
-template <int BITS, int GPT, bool ASYM, int SD>
+template <int B0, int G0, int B1, int G1>
 static hipError_t engine_launch4(const EngOp* ops, int n_ops, const EngGeometry& g, unsigned* ctl, int grid, int bump,
                                  hipStream_t st) {
-  return g.x8 ? engine_launch5<BITS, GPT, ASYM, SD, true>(ops, n_ops, g, ctl, grid, bump, st)
-              : engine_launch5<BITS, GPT, ASYM, SD, false>(ops, n_ops, g, ctl, grid, bump, st);
-}
-
-template <int BITS, int GPT>
-static hipError_t engine_launch2(const EngOp* ops, int n_ops, const EngGeometry& g, unsigned* ctl, int grid, int bump,
-                                 hipStream_t st) {
-  if (g.sd == 1)
-    return g.asym ? engine_launch4<BITS, GPT, true, 1>(ops, n_ops, g, ctl, grid, bump, st)
-                  : engine_launch4<BITS, GPT, false, 1>(ops, n_ops, g, ctl, grid, bump, st);
-  if (g.sd == 2)
-    return g.asym ? engine_launch4<BITS, GPT, true, 2>(ops, n_ops, g, ctl, grid, bump, st)
-                  : engine_launch4<BITS, GPT, false, 2>(ops, n_ops, g, ctl, grid, bump, st);
+  if (g.sd != 1 && g.sd != 2) return hipErrorInvalidValue;
+#define NAD_ENG_L(A, D, X) \
+  if (g.asym == A && g.sd == D && g.x8 == X) return engine_launch5<B0, G0, B1, G1, A, D, X>(ops, n_ops, g, ctl, grid, bump, st);
+  NAD_ENG_L(false, 1, false)
+  NAD_ENG_L(false, 2, false)
+  NAD_ENG_L(true, 1, false)
+  NAD_ENG_L(true, 2, false)
+  NAD_ENG_L(false, 1, true)
+  NAD_ENG_L(false, 2, true)
+  NAD_ENG_L(true, 1, true)
+  NAD_ENG_L(true, 2, true)
+#undef NAD_ENG_L
   return hipErrorInvalidValue;
 }
 
 hipError_t launch_engine(const EngOp* ops, int n_ops, const EngGeometry& g, unsigned* ctl, int grid, int bump,
                          hipStream_t st) {
   static_assert(kEngConsumers == 8, "the partial-sum order below is written for 8 consumers");
-  if (g.bits == 4) {
-    if (g.gpt == 1) return engine_launch2<4, 1>(ops, n_ops, g, ctl, grid, bump, st);
-    if (g.gpt == 2) return engine_launch2<4, 2>(ops, n_ops, g, ctl, grid, bump, st);
-  } else if (g.bits == 2) {
-    if (g.gpt == 1) return engine_launch2<2, 1>(ops, n_ops, g, ctl, grid, bump, st);
-    if (g.gpt == 2) return engine_launch2<2, 2>(ops, n_ops, g, ctl, grid, bump, st);
-    if (g.gpt == 4) return engine_launch2<2, 4>(ops, n_ops, g, ctl, grid, bump, st);
+  const int f0 = g.bits * 16 + g.gpt, f1 = g.bits1 * 16 + g.gpt1;
+  if (f0 == f1) {
+    switch (f0) {
+      case 4 * 16 + 1: return engine_launch4<4, 1, 4, 1>(ops, n_ops, g, ctl, grid, bump, st);
+      case 4 * 16 + 2: return engine_launch4<4, 2, 4, 2>(ops, n_ops, g, ctl, grid, bump, st);
+      case 2 * 16 + 1: return engine_launch4<2, 1, 2, 1>(ops, n_ops, g, ctl, grid, bump, st);
+      case 2 * 16 + 2: return engine_launch4<2, 2, 2, 2>(ops, n_ops, g, ctl, grid, bump, st);
+      case 2 * 16 + 4: return engine_launch4<2, 4, 2, 4>(ops, n_ops, g, ctl, grid, bump, st);
+      default: return hipErrorInvalidValue;
+    }
   }
+  // mixed launches: the reference's int2 policies keep some weights at int4 with the same group size
+  if (f0 == 2 * 16 + 4 && f1 == 4 * 16 + 2) return engine_launch4<2, 4, 4, 2>(ops, n_ops, g, ctl, grid, bump, st);
+  if (f0 == 2 * 16 + 2 && f1 == 4 * 16 + 1) return engine_launch4<2, 2, 4, 1>(ops, n_ops, g, ctl, grid, bump, st);
   return hipErrorInvalidValue;
+}
+
+bool engine_format_pair_ok(int bits0, int gpt0, int bits1, int gpt1) {
+  const int f0 = bits0 * 16 + gpt0, f1 = bits1 * 16 + gpt1;
+  if (f0 == f1) return f0 == 65 || f0 == 66 || f0 == 33 || f0 == 34 || f0 == 36;
+  return (f0 == 36 && f1 == 66) || (f0 == 34 && f1 == 65);
 }
 
 }  // namespace nad

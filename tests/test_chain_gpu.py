@@ -266,3 +266,52 @@ def test_chain_rejects_ineligible():
     with pytest.raises(RuntimeError, match="m = 1"):
         bestla.Chain([dict(kind=CHAIN_LINEAR, w=[w4], act=torch.zeros((2, 256), device="cuda"),
                            out=[torch.empty((2, 128), device="cuda")])], 2)
+
+
+def test_chain_mixed_formats_mistral_policy():
+    """Two weight formats in one launch (Mistral-7B's int2 policy: q, k, o, gate, up, lm_head int2 g64; wv, w2 int4 g64;
+    GQA so {Q, K} is one op and V its own): bit-identical across launch forms (whole token, cut at attention, one op
+    per launch), every op within 1e-6 of the per-op kernels fed the chain's own inputs, and the oracle bar on the
+    format boundary (int4 V and down) through those kernels' own oracle tests."""
+    import bench
+    cfg = dict(bench.MISTRAL, hidden=1024, ffn=2048, layers=2, vocab=1000, kv=256)
+    st = bench.Stack(cfg, 0, 1, seed=17)
+    forms = {}
+    for name, cut in (("whole", False), ("cut", True)):
+        cr = bench.ChainRunner(st, "cuda", cut=cut)
+        for c in cr.chains:
+            c.run()
+        torch.cuda.synchronize()
+        assert cr.status() == 0
+        forms[name] = [t.clone() for t in cr.xs + cr.q + cr.k + cr.v + cr.h + cr.t + [cr.logits]]
+        if name == "whole":
+            keep = cr
+    _same(forms["whole"], forms["cut"])
+    cr = keep
+    assert all(torch.isfinite(t).all() for t in forms["whole"])
+
+    def norm(x):
+        return x / torch.sqrt((x * x).mean(dim=1, keepdim=True) + 1e-5)
+    for li, Lw in enumerate(st.layers):
+        x = cr.xs[li]
+        xn = norm(x)
+        refs = [(cr.q[li], Lw["wq"].forward(xn)), (cr.k[li], Lw["wk"].forward(xn)), (cr.v[li], Lw["wv"].forward(xn)),
+                (cr.h[li], Lw["wo"].forward(cr.o_in[li], epilogue=EPI_RES_ADD, residual=x)),
+                (cr.t[li], bestla.ffn_gate_up(norm(cr.h[li]), Lw["w1"], Lw["w3"])),
+                (cr.xs[li + 1], Lw["w2"].forward(cr.t[li], epilogue=EPI_RES_ADD, residual=cr.h[li]))]
+        for i, (got, ref) in enumerate(refs):
+            err = ((got - ref).abs().max() / ref.abs().max()).item()
+            assert err <= 1e-6, (li, i, err)
+    lg = st.lm_head.forward(norm(cr.xs[-1]))
+    assert ((cr.logits - lg).abs().max() / lg.abs().max()).item() <= 1e-6
+
+
+def test_chain_rejects_format_pairs_it_has_no_kernel_for():
+    """int4 g128 beside int2 g64 in one launch has no instantiation: refused at creation with the formats named."""
+    x = torch.zeros((1, 512), device="cuda")
+    a, b = torch.empty((1, 128), device="cuda"), torch.empty((1, 128), device="cuda")
+    w4 = _w(128, 512, 1, bs=128, bits=4)
+    w2 = _w(128, 512, 2, bs=64, bits=2)
+    with pytest.raises(RuntimeError, match="cannot join"):
+        bestla.Chain([dict(kind=CHAIN_LINEAR, w=[w4], act=x, out=[a]), dict(kind=CHAIN_LINEAR, w=[w2], act=x, out=[b])],
+                     1)
