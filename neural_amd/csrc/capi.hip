@@ -1405,6 +1405,7 @@ extern "C" void* nad_chain_create(const nad_chain_op* ops, int n_ops, int m) {
   g.x8 = env_int("NAD_ENGINE_X8", 0) ? 1 : 0;
   g.sd = int((sd_bytes + 1023) / 1024);
   if (g.sd < 1) g.sd = 1;
+  g.max_slots = env_int("NAD_ENGINE_SLOTS", 16);  // ring slots at most (A/B of the ring's size)
   if (g.sd > 2 || !engine_geometry(g, kp)) {
     set_err("nad_chain_create: the engine's LDS ring does not fit (K up to %d, %zu scale bytes per fill)", kp,
             sd_bytes);

@@ -64,6 +64,7 @@ struct EngGeometry {
   size_t slot_bytes;
   int thin;                     // thin the loader to one fill in flight while the consumers gather (NAD_ENGINE_THIN)
   int loaders, depth;           // loader waves, fills in flight per loader wave
+  int max_slots;                // cap on the ring's slots (A/B; 16 = as many as fit)
   int x8;                       // consumer arithmetic: 0 fp16 hi + lo (default), 1 int8 limbs on i8 MFMA (NAD_ENGINE_X8)
 };
 

@@ -1108,6 +1108,7 @@ bool engine_geometry(EngGeometry& g, int kp) {
   if (fixed >= budget) return false;
   int s = int((budget - fixed) / g.slot_bytes);
   if (s > 16) s = 16;
+  if (g.max_slots > 0 && s > g.max_slots) s = g.max_slots;
   if (g.loaders < 1 || g.loaders > kEngMaxLoaders || g.depth < 1 || g.depth > 2) return false;
   if (s < g.loaders * g.depth + 2) return false;  // fills in flight + at least two published ones for the consumers
   g.slots = s;
