@@ -14,7 +14,7 @@ stack = bench.Stack(cfg, 0, 1)
 dec = bench.Runner(stack, 1, None, "cuda")
 for _ in range(3):
     dec.step()
-ch = bench.ChainRunner(stack, 1, "cuda")
+ch = bench.ChainRunner(stack, "cuda", cut=True)
 for _ in range(2):
     ch.step()
 pre = bench.Runner(stack, 2048, None, "cuda")
