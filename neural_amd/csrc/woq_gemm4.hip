@@ -189,7 +189,7 @@ __device__ __forceinline__ uint32_t lds_addr(const char* p) {
   return uint32_t(reinterpret_cast<uintptr_t>((const __attribute__((address_space(3))) char*)p));
 }
 
-template <int BITS, bool G32, bool ASYM>
+template <int BITS, bool G32, bool ASYM, bool FOLD = false>
 __global__ __launch_bounds__(512, 1) void woq_gemm4_kernel(GemmArgs a, const _Float16* __restrict__ A16, int lda16,
                                                            int gh_log2) {
   constexpr int HPT = hpt<BITS>();
@@ -335,6 +335,15 @@ __global__ __launch_bounds__(512, 1) void woq_gemm4_kernel(GemmArgs a, const _Fl
     const float f16or = st == kScaleBF16 ? fb : fh;
     return st == kScaleF32 ? __uint_as_float(x) : f16or;
   };
+  // FOLD (G32): the scale as an fp16 pair -- fp16 scales are the stored bits, exact; bf16 / f32 ones are rounded once
+  auto scale_h8 = [&](uint32_t x) {
+    _Float16 hs;
+    if (st == kScaleF16)
+      hs = __builtin_bit_cast(_Float16, uint16_t((x >> ssh) & 0xFFFFu));
+    else
+      hs = _Float16(scale_f32(x));
+    return h8_t{hs, hs, hs, hs, hs, hs, hs, hs};
+  };
 
   auto hand_over = [&](auto Hc, int u) {
     constexpr int H = decltype(Hc)::value;
@@ -442,6 +451,19 @@ __global__ __launch_bounds__(512, 1) void woq_gemm4_kernel(GemmArgs a, const _Fl
           bf[j] = dq4(bw[j][dd], s16, zc0 - splat(zf), zc1 - splat(zf));
         else
           bf[j] = dq2(bw[j][0], dd * 8, zc0 - splat(zf));
+      }
+      if constexpr (G32 && FOLD) {
+        // the group scale folded into the fp16 B fragment (q * s rounded once; DeviceWeight::fold_ok checked that every
+        // q * s is an fp16 normal): the MFMAs accumulate straight into the result, no per-step scaling FMAs
+#pragma unroll
+        for (int j = 0; j < 2; j++) bf[j] = bf[j] * scale_h8(sg[dd][j]);
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+          const h8_t af = dd == 0 ? af0[i] : af1[i];
+#pragma unroll
+          for (int j = 0; j < 2; j++) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, bf[j], acc[i][j], 0, 0, 0);
+        }
+        continue;
       }
       if constexpr (G32) {
         const float sf[2] = {scale_f32(sg[dd][0]), scale_f32(sg[dd][1])};
@@ -570,16 +592,20 @@ hipError_t launch_gemm4(const GemmArgs& a, int bits, const _Float16* A16, int ld
     return hipGetLastError();
   };
 #define NAD_G4(B, G, A) go(g4::woq_gemm4_kernel<B, G, A>, g4::lds_bytes<B, G, A>())
+#define NAD_G4F(B, A) go(g4::woq_gemm4_kernel<B, true, A, true>, g4::lds_bytes<B, true, A>())
   if (bits == 4) {
+    if (g32 && a.fold) return asym ? NAD_G4F(4, true) : NAD_G4F(4, false);
     if (g32) return asym ? NAD_G4(4, true, true) : NAD_G4(4, true, false);
     return asym ? NAD_G4(4, false, true) : NAD_G4(4, false, false);
   }
   if (bits == 8) {
+    if (g32 && a.fold) return asym ? NAD_G4F(8, true) : NAD_G4F(8, false);
     if (g32) return asym ? NAD_G4(8, true, true) : NAD_G4(8, true, false);
     return asym ? NAD_G4(8, false, true) : NAD_G4(8, false, false);
   }
   return asym ? NAD_G4(2, false, true) : NAD_G4(2, false, false);
 #undef NAD_G4
+#undef NAD_G4F
 }
 
 }  // namespace nad

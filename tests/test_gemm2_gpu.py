@@ -165,7 +165,31 @@ def test_gemm4_parity(oracle, cfg, act):
         x = x.to(torch.float16 if act == "fp16" else torch.bfloat16)
     ref = oracle.forward(x.float().cpu().numpy(), blob, n, k)
     y = w.forward(x).cpu().numpy()
-    assert _rel_err(y, ref) <= TOL[act], (_rel_err(y, ref), act)
+    # groups of 32 fold the scale into the fp16 weights (q * s rounded once to fp16): the north_star-side bar of a
+    # product with fp16 weights, FOLD_TOL, instead of the exact-weight bars (test_gemm4_g32_scale_fold)
+    tol = max(TOL[act], FOLD_TOL) if bs == 32 else TOL[act]
+    assert _rel_err(y, ref) <= tol, (_rel_err(y, ref), act)
+
+
+FOLD_TOL = 5e-4
+
+
+@pytest.mark.parametrize("cfg", [c for c in GEMM4_CASES if c[3] == 32])
+def test_gemm4_g32_scale_fold(oracle, monkeypatch, cfg):
+    """Groups of 32 fold the group scale into the fp16 B fragment by default (q * s rounded once to fp16; every q * s of
+    these blobs is an fp16 normal, DeviceWeight::fold_ok): against the oracle at the prefill bar, and against the exact
+    fp32 per-step scaling (NAD_GEMM4_FOLD=0) within the fp16 rounding of q * s (2^-11 relative per weight)."""
+    m, n, k, bs, qt, st, asym, comp = cfg
+    blob = _blob(oracle, n, k, bs, qt, st, asym, comp, seed=m + 5 * n + k)
+    w = bestla.DeviceWeight(blob)
+    x = torch.from_numpy(np.random.default_rng(m + n).uniform(-0.5, 0.5, size=(m, k)).astype(np.float32)).cuda().half()
+    ref = oracle.forward(x.float().cpu().numpy(), blob, n, k)
+    yf = w.forward(x).cpu().numpy()
+    monkeypatch.setenv("NAD_GEMM4_FOLD", "0")
+    ye = w.forward(x).cpu().numpy()
+    assert _rel_err(yf, ref) <= FOLD_TOL
+    assert _rel_err(ye, ref) <= TOL["fp16"]
+    assert _rel_err(yf, ye) <= FOLD_TOL
 
 
 def test_gemm4_takes_the_fallback_configs(oracle, monkeypatch):
