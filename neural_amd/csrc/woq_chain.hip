@@ -68,7 +68,7 @@ constexpr int NC = kEngConsumers;
 constexpr int FT = kEngFillTiles;
 constexpr int TPC = FT / NC;  // tiles per consumer per fill
 static_assert(FT % NC == 0, "every consumer takes the same number of tiles of a fill");
-constexpr int PJ = 12;                      // granule pairs per consumer lane per gather pass (one pass up to K = 12288)
+constexpr int PJ = 8;                       // granule pairs per consumer lane per gather pass (12 = one pass for K = 11008 measured 1-3 % slower: 168 VGPRs)
 constexpr int kOOB = 0x7FFF0000;            // buffer offset past every resource: no memory access, returns 0
 constexpr int kSC1 = 16;                    // buffer-load aux: sc1 (bypass this CU's L1)
 constexpr int kNT = 2;                      // buffer-load aux: non-temporal (weights, read once per token)

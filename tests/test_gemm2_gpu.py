@@ -283,7 +283,8 @@ def test_gemm4_splitk_parity(oracle, monkeypatch, cfg):
         x = x.to(torch.float16 if act == "fp16" else torch.bfloat16)
     ref = oracle.forward(x.float().cpu().numpy(), blob, n, k)
     y = w.forward(x).cpu().numpy()
-    assert _rel_err(y, ref) <= TOL[act], (_rel_err(y, ref), act)
+    tol = max(TOL[act], FOLD_TOL) if bs == 32 else TOL[act]  # g32: scale folded into the fp16 weights
+    assert _rel_err(y, ref) <= tol, (_rel_err(y, ref), act)
     monkeypatch.setenv("NAD_SPLITK_DISABLE", "1")
     y1 = w.forward(x).cpu().numpy()
     assert _rel_err(y, y1.astype(np.float64)) <= 2e-5
