@@ -418,6 +418,13 @@ __global__ __launch_bounds__(512, 1) void woq_gemm4_kernel(GemmArgs a, const _Fl
       sg[0][1] = lds_b32v(sa + 64);
       sg[1][0] = lds_b32v(sa + 512);
       sg[1][1] = lds_b32v(sa + 512 + 64);
+    } else if constexpr (FOLD) {  // the half step's group: its scales fold into the B fragments of both steps
+      // (each register its own LDS read: a C++ copy of an inline-asm LDS result would run before the lgkmcnt wait)
+      const uint32_t sa = bl + soff + slot * 512;
+      sg[0][0] = lds_b32v(sa);
+      sg[0][1] = lds_b32v(sa + 64);
+      sg[1][0] = lds_b32v(sa);
+      sg[1][1] = lds_b32v(sa + 64);
     }
     h8_t af0[8], af1[8];
     lds_frags(af0, al + roff[0], std::make_index_sequence<8>{});
@@ -452,9 +459,10 @@ __global__ __launch_bounds__(512, 1) void woq_gemm4_kernel(GemmArgs a, const _Fl
         else
           bf[j] = dq2(bw[j][0], dd * 8, zc0 - splat(zf));
       }
-      if constexpr (G32 && FOLD) {
+      if constexpr (FOLD) {
         // the group scale folded into the fp16 B fragment (q * s rounded once; DeviceWeight::fold_ok checked that every
-        // q * s is an fp16 normal): the MFMAs accumulate straight into the result, no per-step scaling FMAs
+        // q * s is an fp16 normal): the MFMAs accumulate straight into the result -- no per-step (g32) or group-end
+        // (g >= 64) scaling FMAs
 #pragma unroll
         for (int j = 0; j < 2; j++) bf[j] = bf[j] * scale_h8(sg[dd][j]);
 #pragma unroll
@@ -592,17 +600,20 @@ hipError_t launch_gemm4(const GemmArgs& a, int bits, const _Float16* A16, int ld
     return hipGetLastError();
   };
 #define NAD_G4(B, G, A) go(g4::woq_gemm4_kernel<B, G, A>, g4::lds_bytes<B, G, A>())
-#define NAD_G4F(B, A) go(g4::woq_gemm4_kernel<B, true, A, true>, g4::lds_bytes<B, true, A>())
+#define NAD_G4F(B, G, A) go(g4::woq_gemm4_kernel<B, G, A, true>, g4::lds_bytes<B, G, A>())
   if (bits == 4) {
-    if (g32 && a.fold) return asym ? NAD_G4F(4, true) : NAD_G4F(4, false);
+    if (g32 && a.fold) return asym ? NAD_G4F(4, true, true) : NAD_G4F(4, true, false);
     if (g32) return asym ? NAD_G4(4, true, true) : NAD_G4(4, true, false);
+    if (a.fold) return asym ? NAD_G4F(4, false, true) : NAD_G4F(4, false, false);
     return asym ? NAD_G4(4, false, true) : NAD_G4(4, false, false);
   }
   if (bits == 8) {
-    if (g32 && a.fold) return asym ? NAD_G4F(8, true) : NAD_G4F(8, false);
+    if (g32 && a.fold) return asym ? NAD_G4F(8, true, true) : NAD_G4F(8, true, false);
     if (g32) return asym ? NAD_G4(8, true, true) : NAD_G4(8, true, false);
+    if (a.fold) return asym ? NAD_G4F(8, false, true) : NAD_G4F(8, false, false);
     return asym ? NAD_G4(8, false, true) : NAD_G4(8, false, false);
   }
+  if (a.fold) return asym ? NAD_G4F(2, false, true) : NAD_G4F(2, false, false);
   return asym ? NAD_G4(2, false, true) : NAD_G4(2, false, false);
 #undef NAD_G4
 #undef NAD_G4F

@@ -167,11 +167,28 @@ def test_gemm4_parity(oracle, cfg, act):
     y = w.forward(x).cpu().numpy()
     # groups of 32 fold the scale into the fp16 weights (q * s rounded once to fp16): the north_star-side bar of a
     # product with fp16 weights, FOLD_TOL, instead of the exact-weight bars (test_gemm4_g32_scale_fold)
-    tol = max(TOL[act], FOLD_TOL) if bs == 32 else TOL[act]
+    tol = max(TOL[act], FOLD_TOL) if bs in (32, 64) else TOL[act]
     assert _rel_err(y, ref) <= tol, (_rel_err(y, ref), act)
 
 
 FOLD_TOL = 5e-4
+
+
+@pytest.mark.parametrize("cfg", [c for c in GEMM4_CASES if c[3] == 64])
+def test_gemm4_g64_scale_fold(oracle, monkeypatch, cfg):
+    """Groups of 64 fold the group scale into the fp16 B fragment too (int4 / int2 / int8): against the oracle and the
+    exact fp32 group-end scaling (NAD_GEMM4_FOLD=0)."""
+    m, n, k, bs, qt, st, asym, comp = cfg
+    blob = _blob(oracle, n, k, bs, qt, st, asym, comp, seed=m + 9 * n + k)
+    w = bestla.DeviceWeight(blob)
+    x = torch.from_numpy(np.random.default_rng(m + n + 1).uniform(-0.5, 0.5, size=(m, k)).astype(np.float32)).cuda().half()
+    ref = oracle.forward(x.float().cpu().numpy(), blob, n, k)
+    yf = w.forward(x).cpu().numpy()
+    monkeypatch.setenv("NAD_GEMM4_FOLD", "0")
+    ye = w.forward(x).cpu().numpy()
+    assert _rel_err(ye, ref) <= TOL["fp16"]
+    assert _rel_err(yf, ref) <= FOLD_TOL
+    assert _rel_err(yf, ye) <= FOLD_TOL
 
 
 @pytest.mark.parametrize("cfg", [c for c in GEMM4_CASES if c[3] == 32])
@@ -283,7 +300,7 @@ def test_gemm4_splitk_parity(oracle, monkeypatch, cfg):
         x = x.to(torch.float16 if act == "fp16" else torch.bfloat16)
     ref = oracle.forward(x.float().cpu().numpy(), blob, n, k)
     y = w.forward(x).cpu().numpy()
-    tol = max(TOL[act], FOLD_TOL) if bs == 32 else TOL[act]  # g32: scale folded into the fp16 weights
+    tol = max(TOL[act], FOLD_TOL) if bs in (32, 64) else TOL[act]  # g32 / g64: scale folded into the fp16 weights
     assert _rel_err(y, ref) <= tol, (_rel_err(y, ref), act)
     monkeypatch.setenv("NAD_SPLITK_DISABLE", "1")
     y1 = w.forward(x).cpu().numpy()
