@@ -13,13 +13,14 @@
 //
 // Shape (MI355X_MICROARCH.md rows ldsdma-fill, prefetch-credit, handoff-1to1, allgather; the engine-vs-launches row
 // measured the same structure at 0.87-0.89x of separate launches for a bf16 layer):
-//   * one workgroup per CU (the LDS request admits no second one), all co-resident; 9 waves: 8 consumers + 1 loader;
+//   * one workgroup per CU (the LDS request admits no second one), all co-resident; 10 waves: 8 consumers + 2 loaders
+//     (one loader wave tops out near 20 GB/s per CU, two reach 27: tools/dma_probe.hip);
 //   * every op's units (16-column stripes; {gate, up} stripe pairs for the dual SiLU*mul op) are split into balanced
 //     runs per workgroup, exactly as the single-op stripe stream splits them;
-//   * the LOADER wave walks the workgroup's fills for ALL ops of the launch in order -- a fill is 16 consecutive
-//     1 KiB K tiles of one stripe + their group scales (+ zero points) -- and moves each by LDS-DMA
-//     (buffer_load_dwordx4 ... lds, non-temporal: read once per token) into a ring of LDS slots: at most 3 fills in
-//     flight (counted s_waitcnt vmcnt), a FULL word per slot published when its fill has landed, a slot re-filled only
+//   * the LOADER waves walk the workgroup's fills for ALL ops of the launch in order (fill f by loader f mod 2) -- a
+//     fill is 16 consecutive 1 KiB K tiles of one stripe + their group scales (+ zero points) -- and move each by LDS-DMA
+//     (buffer_load_dwordx4 ... lds, non-temporal: read once per token) into a ring of LDS slots: one fill in flight per
+//     loader (counted s_waitcnt vmcnt), a FULL word per slot published when its fill has landed, a slot re-filled only
 //     when all 8 consumers have released it (FREE counter).  It never waits for activations, so it keeps streaming the
 //     next op's weights while the consumers wait for that op's input;
 //   * the 8 CONSUMER waves: per op, stage the input vector into LDS as MFMA-ready fp16 hi/lo rows (hi = fp16(x),
@@ -34,7 +35,11 @@
 //     sc1 buffer loads and re-reads every granule whose tag is not yet the expected one -- the data is the flag, no
 //     fence, no counter.  The generation is a per-chain device word bumped by workgroup 0 at its end, so stale
 //     granules of the previous run never match (graph replay safe, nothing to reset per call);
-//   * every spin is bounded (~1 s); a give-up records a code in ctl[1] and the launch still terminates.
+//   * every spin is bounded (~1 s); a give-up records a code in ctl[1] and the launch still terminates;
+//   * one launch may hold two weight formats (the op body is a generic lambda over (bits, groups per tile)): Mistral's
+//     int2 policy keeps wv / w2 at int4 (llama_utils.cpp:269-287);
+//   * opt-in (NAD_ENGINE_X8=1): int8-limb consumers on v_mfma_i32_16x16x64_i8 (see X8 below), each consumer staging
+//     exactly the tiles it reads, no barrier.
 // Arithmetic per op is the same for every position of the op in a launch: a one-op launch of it gives bit-identical
 // outputs (tests/test_chain_gpu.py).
 #include <hip/hip_runtime.h>
