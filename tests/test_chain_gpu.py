@@ -268,7 +268,7 @@ def test_chain_rejects_ineligible():
                            out=[torch.empty((2, 128), device="cuda")])], 2)
 
 
-def test_chain_mixed_formats_mistral_policy():
+def test_chain_mixed_formats_mistral_policy(engine_form):
     """Two weight formats in one launch (Mistral-7B's int2 policy: q, k, o, gate, up, lm_head int2 g64; wv, w2 int4 g64;
     GQA so {Q, K} is one op and V its own): bit-identical across launch forms (whole token, cut at attention, one op
     per launch), every op within 1e-6 of the per-op kernels fed the chain's own inputs, and the oracle bar on the
