@@ -1400,7 +1400,9 @@ extern "C" void* nad_chain_create(const nad_chain_op* ops, int n_ops, int m) {
                                    : size_t(kEngFillTiles) * gpt;
     sd_bytes = std::max(sd_bytes, std::min(groups, size_t(w0.ng)) * 16 * ssz);
   }
-  g.thin = env_int("NAD_ENGINE_THIN", 0);  // measured slower on every edge (trace_chain.py): off
+  g.thin = env_int("NAD_ENGINE_THIN", 0) ? 1 : 0;  // bit 0: loader thinned during gathers (measured slower: off)
+  // bit 1: the loaders start after every consumer issued the first op's input loads (woq_chain.hip start sync)
+  if (env_int("NAD_ENGINE_START_SYNC", 0)) g.thin |= 2;  // measured 2 % slower (profiles/r03_engine_start_sync.txt)
   g.loaders = env_int("NAD_ENGINE_LOADERS", 2);  // loader waves (tools/dma_probe.hip: 2 x 2 fills in flight best)
   g.depth = env_int("NAD_ENGINE_DEPTH", 1);      // fills in flight per loader wave (1 measured faster than 2)
   // consumer arithmetic: fp16 hi + lo (default) or the int8-limb form (woq_chain.hip X8, NAD_ENGINE_X8=1): X8 streams

@@ -62,7 +62,8 @@ struct EngGeometry {
   int kp;                       // activation row length (max over ops of nt * KT)
   size_t lds;                   // dynamic LDS bytes
   size_t slot_bytes;
-  int thin;                     // thin the loader to one fill in flight while the consumers gather (NAD_ENGINE_THIN)
+  int thin;                     // bit 0: no fill in flight while the consumers gather (NAD_ENGINE_THIN); bit 1: the
+                                // loaders wait for the consumers' first input loads (NAD_ENGINE_START_SYNC)
   int loaders, depth;           // loader waves, fills in flight per loader wave
   int max_slots;                // cap on the ring's slots (A/B; 16 = as many as fit)
   int x8;                       // consumer arithmetic: 0 fp16 hi + lo (default), 1 int8 limbs on i8 MFMA (NAD_ENGINE_X8)

@@ -78,8 +78,9 @@ constexpr int kOOB = 0x7FFF0000;            // buffer offset past every resource
 constexpr int kSC1 = 16;                    // buffer-load aux: sc1 (bypass this CU's L1)
 constexpr int kNT = 2;                      // buffer-load aux: non-temporal (weights, read once per token)
 constexpr unsigned kSpinMax = 1u << 24;     // ~1 s of s_sleep(1) polls
-// LDS control words (u32 index): FULL[16], FREE[16], consumer barrier, RMS partial sums[2][8], gather phase
-constexpr int kFull = 0, kFree = 16, kBar = 32, kNsum = 36, kPhase = 52, kCtlBytes = 256;
+// LDS control words (u32 index): FULL[16], FREE[16], consumer barrier, RMS partial sums[2][8], gather phase,
+// consumers that issued the launch's first gather (start sync)
+constexpr int kFull = 0, kFree = 16, kBar = 32, kNsum = 36, kPhase = 52, kStart = 53, kCtlBytes = 256;
 constexpr int kPartBytes = kEngMaxStripes * NC * 16 * 4;
 
 typedef __attribute__((address_space(3))) void lds_void_t;
@@ -188,6 +189,18 @@ __device__ void loader(const EngOp* ops, int n_ops, char* ring, int S, int slot_
   int pub_f = lw, pub_slot = lw;  // the next own fill to publish and its slot
   while (pub_slot >= S) pub_slot -= S;
   bool failed = false;
+  // start sync (thin bit 1): the first op's input loads go out before this launch's first DMA burst, which they would
+  // otherwise queue behind (the first op's gather is on the launch's critical path; its weights are not yet)
+  if (thin & 2) {
+    unsigned spins = 0;
+    while (!failed && lds_ld(ctl_a + kStart * 4) < unsigned(NC)) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > kSpinMax) {
+        give_up(ctl, 6);
+        failed = true;
+      }
+    }
+  }
   auto publish_one = [&]() {
     lds_st(full_a + pub_slot * 4, unsigned(pub_f + 1));
     mpub++;
@@ -251,7 +264,7 @@ __device__ void loader(const EngOp* ops, int n_ops, char* ring, int S, int slot_
 #endif
           // while the consumers gather an input, keep no fill in flight: their loads queue behind this wave's DMAs
           // (MI355X_MICROARCH.md gather-pass: 0.3-0.65 us with the own DMA quiet vs 1.0-1.7 behind a refill burst)
-          if (thin && lds_ld(ctl_a + kPhase * 4) != 0u) {
+          if ((thin & 1) && lds_ld(ctl_a + kPhase * 4) != 0u) {
             wait_vm<0>();
             while (mpub < mine) publish_one();
           }
@@ -485,7 +498,7 @@ __global__ __launch_bounds__(kEngMaxThreads, 1) void woq_engine_kernel(const Eng
     const int vpu = o.dual ? 2 : 1;
     const int nout = nv / vpu * 16;
 
-    if (thin && cw == 0 && lane == 0) lds_st(ctl_a + kPhase * 4, 1u);  // gathering: loader thinned
+    if ((thin & 1) && cw == 0 && lane == 0) lds_st(ctl_a + kPhase * 4, 1u);  // gathering: loader thinned
     // 0) this lane's residual (one output per lane at most: nout <= 256), issued now, used in the epilogue
     float res_v = 0.f;
     unsigned long long res_g = 0;
@@ -589,6 +602,7 @@ __global__ __launch_bounds__(kEngMaxThreads, 1) void woq_engine_kernel(const Eng
             g[j] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(ra, in ? q * 8 : kOOB, 0, 0));
           }
           __builtin_amdgcn_sched_barrier(0);
+          if ((thin & 2) && op == 0 && i0 == 0 && lane == 0) lds_add(ctl_a + kStart * 4, 1u);  // start sync
           if (cw == 0 && i0 == 0) ETRACE(11, op, wall_clock64());
 #pragma unroll
           for (int j = 0; j < 2 * QJ; j++) {
@@ -631,6 +645,7 @@ __global__ __launch_bounds__(kEngMaxThreads, 1) void woq_engine_kernel(const Eng
           if ((lane & 31) == 0) sblk[qi[j] >> 5] = amax * (1.f / 127.f) * (1.f / 16384.f);
         }
       }
+      if ((thin & 2) && op == 0 && nqc == 0 && lane == 0) lds_add(ctl_a + kStart * 4, 1u);  // no tiles: start sync
     } else {
       const int npair = (K + 1) / 2;  // granule / element pairs: one 16-B (8-B external) load per pair
       const bool gw = o_norm && o_norm_w;
@@ -700,6 +715,7 @@ __global__ __launch_bounds__(kEngMaxThreads, 1) void woq_engine_kernel(const Eng
             g[j] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(ra, q < npair ? q * 8 : kOOB, 0, 0));
           }
           __builtin_amdgcn_sched_barrier(0);
+          if ((thin & 2) && op == 0 && q0 == 0 && lane == 0) lds_add(ctl_a + kStart * 4, 1u);  // start sync
           if (cw == 0 && q0 == 0) ETRACE(11, op, wall_clock64());
 #pragma unroll
           for (int j = 0; j < PJ; j++) {
@@ -730,7 +746,7 @@ __global__ __launch_bounds__(kEngMaxThreads, 1) void woq_engine_kernel(const Eng
     // fp16: every consumer staged a share of the whole vector, so all meet before the stream.  (Staging only the
     // consumer's own tiles with no barrier measured 2-3 % slower per whole-token launch; X8 does that.)
     if constexpr (!X8) cbar(bar_a, bar_epoch, ctl, lane, failed);
-    if (thin && cw == 0 && lane == 0) lds_st(ctl_a + kPhase * 4, 0u);
+    if ((thin & 1) && cw == 0 && lane == 0) lds_st(ctl_a + kPhase * 4, 0u);
     if (cw == 0) ETRACE(2, op, wall_clock64());
 
     // 2) the weight stream: consumer cw takes tiles cw and cw + 8 of every fill.  One LDS round trip per fill: the FULL
