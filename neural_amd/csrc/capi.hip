@@ -1309,7 +1309,8 @@ extern "C" void* nad_chain_create(const nad_chain_op* ops, int n_ops, int m) {
         g.bits1 = w0.bits;
         g.gpt1 = gpt;
       }
-      if (g.bits1 != w0.bits || g.gpt1 != gpt || !engine_format_pair_ok(g.bits, g.gpt, g.bits1, g.gpt1)) {
+      if (g.bits1 != w0.bits || g.gpt1 != gpt || !(engine_format_pair_ok(g.bits, g.gpt, g.bits1, g.gpt1) ||
+                                                     engine_format_pair_ok(g.bits1, g.gpt1, g.bits, g.gpt))) {
         set_err("nad_chain_create: op %d's format (bits %d, %d groups per tile) cannot join the launch's (bits %d / %d, "
                 "%d / %d groups per tile)", i, w0.bits, gpt, g.bits, g.bits1, g.gpt, g.gpt1);
         return nullptr;
@@ -1399,6 +1400,12 @@ extern "C" void* nad_chain_create(const nad_chain_op* ops, int n_ops, int m) {
     const size_t groups = gpt == 1 ? size_t((kEngFillTiles + std::max(tpg, 1) - 1) / std::max(tpg, 1) + 1)
                                    : size_t(kEngFillTiles) * gpt;
     sd_bytes = std::max(sd_bytes, std::min(groups, size_t(w0.ng)) * 16 * ssz);
+  }
+  // a mixed launch is instantiated with the int2 member as format 0: swap when the first op was the other one
+  if ((g.bits != g.bits1 || g.gpt != g.gpt1) && !engine_format_pair_ok(g.bits, g.gpt, g.bits1, g.gpt1)) {
+    std::swap(g.bits, g.bits1);
+    std::swap(g.gpt, g.gpt1);
+    for (EngOp& e : host) e.fmt ^= 1;
   }
   g.thin = env_int("NAD_ENGINE_THIN", 0) ? 1 : 0;  // bit 0: loader thinned during gathers (measured slower: off)
   // bit 1: the loaders start after every consumer issued the first op's input loads (woq_chain.hip start sync)

@@ -22,7 +22,7 @@ pytestmark = pytest.mark.gpu
 
 from neural_amd import bestla  # noqa: E402
 from neural_amd.bestla import CHAIN_GATE_UP, CHAIN_LINEAR, CHAIN_QKV, EPI_RES_ADD  # noqa: E402
-from tests.oracle_lib import F16, S4  # noqa: E402
+from tests.oracle_lib import F16, S2, S4  # noqa: E402
 from tests.test_gpu_parity import _rel_err  # noqa: E402
 
 
@@ -304,6 +304,30 @@ def test_chain_mixed_formats_mistral_policy(engine_form):
             assert err <= 1e-6, (li, i, err)
     lg = st.lm_head.forward(norm(cr.xs[-1]))
     assert ((cr.logits - lg).abs().max() / lg.abs().max()).item() <= 1e-6
+
+
+def test_chain_mixed_launch_may_start_with_either_format(oracle):
+    """A mixed launch whose first op is the int4 member (format roles swapped at creation): each op against the oracle."""
+    rng = np.random.default_rng(21)
+
+    def blob(n, k, bits):
+        lo, hi = (-8, 8) if bits == 4 else (-2, 2)
+        q = rng.integers(lo, hi, size=(k, n), dtype=np.int8)
+        s = rng.uniform(0.001, 0.005, size=(k // 64, n)).astype(np.float32)
+        qt = S4 if bits == 4 else S2
+        return oracle.pack_q(q, s, None, n, k, 64, qt, F16, False, oracle.lib.orc_select_core(4, qt, 64, 0, 0))
+    k, n = 512, 256
+    b4, b2 = blob(n, k, 4), blob(n, k, 2)
+    w4, w2 = bestla.DeviceWeight(b4), bestla.DeviceWeight(b2)
+    x = (torch.rand((1, k), device="cuda") - 0.5)
+    y4, y2 = torch.empty((1, n), device="cuda"), torch.empty((1, n), device="cuda")
+    ch = bestla.Chain([dict(kind=CHAIN_LINEAR, w=[w4], act=x, out=[y4]), dict(kind=CHAIN_LINEAR, w=[w2], act=x, out=[y2])], 1)
+    ch.run()
+    torch.cuda.synchronize()
+    assert ch.status() == 0
+    xa = x.cpu().numpy()
+    assert _rel_err(y4.cpu().numpy(), oracle.forward(xa, b4, n, k)) <= 2e-5
+    assert _rel_err(y2.cpu().numpy(), oracle.forward(xa, b2, n, k)) <= 2e-5
 
 
 def test_chain_rejects_format_pairs_it_has_no_kernel_for():
