@@ -968,6 +968,7 @@ static int run_gemm(const void* act, int act_t, int lda, int m, int k, const Dev
   a.ld_aux = ld_aux;
   a.prio = env_int("NAD_GEMM3_PRIO", 0);
   a.stagger = env_int("NAD_GEMM3_STAGGER", 1);  // measured +3-7 % (profiles/r02_gemm3_stagger.txt)
+  a.stagger2 = env_int("NAD_GEMM4_STAGGER2", 0);
   // scale folding measured 1-5 % SLOWER on gemm3 (profiles/r03_gemm3_fold.txt) and it rounds q * s to fp16: opt-in
   a.fold = w.fold_ok && env_int("NAD_GEMM_FOLD", 0) ? 1 : 0;
   a.w = view(w, out, ldo, bias, bias_ld);

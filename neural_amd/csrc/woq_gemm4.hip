@@ -591,7 +591,8 @@ hipError_t launch_gemm4(const GemmArgs& a, int bits, const _Float16* A16, int ld
   const int nbm = (a.M + g4::BM - 1) / g4::BM, nbn = (a.w.ns + 7) / 8;
   const bool asym = a.w.zps != nullptr;
   GemmArgs ga = a;
-  if (bits == 2) ga.stagger = 0;  // measured neutral to -5 % for int2 (profiles/r02_gemm4_stagger.txt), +4-14 % else
+  // measured neutral to -5 % for int2 (profiles/r02_gemm4_stagger.txt), +4-14 % else; NAD_GEMM4_STAGGER2 re-tests int2
+  if (bits == 2 && !(ga.stagger && a.stagger2)) ga.stagger = 0;
   auto go = [&](auto k, int lds) -> hipError_t {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
                                        lds);
