@@ -591,8 +591,9 @@ hipError_t launch_gemm4(const GemmArgs& a, int bits, const _Float16* A16, int ld
   const int nbm = (a.M + g4::BM - 1) / g4::BM, nbn = (a.w.ns + 7) / 8;
   const bool asym = a.w.zps != nullptr;
   GemmArgs ga = a;
-  // measured neutral to -5 % for int2 (profiles/r02_gemm4_stagger.txt), +4-14 % else; NAD_GEMM4_STAGGER2 re-tests int2
-  if (bits == 2 && !(ga.stagger && a.stagger2)) ga.stagger = 0;
+  // the stagger measured +4-14 % for int4 / int8 and neutral to -5 % for int2 (profiles/r02_gemm4_stagger.txt); with
+  // the scale fold int2 gains too, +5-11 % (profiles/r03_gemm4_int2_stagger_fold.txt): off only for unfolded int2
+  if (bits == 2 && !a.fold && !a.stagger2) ga.stagger = 0;
   auto go = [&](auto k, int lds) -> hipError_t {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
                                        lds);
