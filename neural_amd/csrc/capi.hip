@@ -974,7 +974,9 @@ static int run_gemm(const void* act, int act_t, int lda, int m, int k, const Dev
   a.w = view(w, out, ldo, bias, bias_ld);
   const int pg = pipelined_gemm(w, m);
   // gemm4 at groups of 32 / 64 scales the products into the result every 32 / 64 k (4 / 2 FMAs per MFMA): there the
-  // fold pays, +14-23 % (NAD_GEMM4_FOLD=0 restores the exact fp32 per-group path; DESIGN.md, gemm4 scale folding)
+  // fold pays, +14-23 %; at groups of 128 (int2 / int8: int4 g128 runs gemm3) it measured +6-21 % with the int2 stagger
+  // it enables (profiles/r03_gemm4_g128_fold.txt) but is opt-in (NAD_GEMM4_FOLD_ALL=1) until the full GPU suite has run
+  // with it; NAD_GEMM4_FOLD=0 restores the exact fp32 per-group path (gemm4 scale folding)
   if (pg == 4 && (w.blocksize == 32 || w.blocksize == 64 || env_int("NAD_GEMM4_FOLD_ALL", 0)))
     a.fold = w.fold_ok && env_int("NAD_GEMM4_FOLD", 1) ? 1 : 0;
   if (h16) {
