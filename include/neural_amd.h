@@ -137,6 +137,10 @@ void nad_pc_destroy(parallel_context* p);
 #define NAD_ACT_F32 0
 #define NAD_ACT_F16 1
 #define NAD_ACT_BF16 2
+/* device scale codes (nad_synthetic_weight, nad_plan_forward, nad_weight_info[8]) */
+#define NAD_SCALE_F32 0
+#define NAD_SCALE_BF16 1
+#define NAD_SCALE_F16 2
 #define NAD_EPI_NONE 0
 #define NAD_EPI_BIAS 1
 #define NAD_EPI_SILU_MUL 2
@@ -152,14 +156,35 @@ void nad_clear_error(void);
 size_t nad_device_weight_size(const void* hostblob);
 /* bestla_device_load_storage with an explicit capacity check and a status return */
 int nad_device_load(const void* hostblob, void* devstor, void* deviceptr, size_t capacity, void* queue);
-/* descriptor summary: [magic, bits, n, k, blocksize, ns, nt, ng, scale_t, asym, has_shuffle, bytes, fold_ok] */
-int nad_weight_info(const void* devstor, int64_t* out13);
+/* descriptor summary: [magic, bits, n, k, blocksize, ns, nt, ng, scale_t, asym, has_shuffle, bytes] */
+int nad_weight_info(const void* devstor, int64_t* out12);
+/* the same, versioned by the caller's buffer: writes min(n, 13) values ([12] = fold_ok: every q * scale is an fp16
+ * normal, the prefill GEMM may fold the scale into the fp16 weights), returns the number written or -1 */
+int nad_weight_info2(const void* devstor, int64_t* out, int n);
+/* re-read the NAD_* tuning / A-B switches from the environment (they are read once when the library loads, never per
+ * call); not thread-safe against forwards running at the same time */
+void nad_reload_knobs(void);
 /* blob header summary (same fields as the oracle's orc_blob_info) */
 int nad_blob_info(const void* hostblob, int64_t* out27);
 /* Y = epi(X . W^T): X in fp32/fp16/bf16 (act_dtype), Y fp32.  bias: bias[m*bias_ld + n] (bias_ld 0 = broadcast);
  * res: residual[m*ld_res + n] for NAD_EPI_RES_ADD. */
 int nad_device_forward(const void* act, int act_dtype, const void* devstor, float* out, int m, int n, int k, int lda,
                        int ldo, int epi, const float* bias, int bias_ld, const float* res, int ld_res, void* queue);
+/* Dry run of nad_device_forward for a weight geometry (bits 2 / 4 / 8, blocksize <= 0 = per-channel, scale_t
+ * NAD_SCALE_*, m rows of act_dtype): the whole host side of the call -- validation, kernel choice, geometry,
+ * workspace sizing -- with every launch recorded instead of issued; no device memory is touched and no GPU is needed.
+ * out (versioned by nout): [kernel NAD_KERNEL_*, grid, threads per workgroup, split-K runs, scale folded into the fp16
+ * weights (0/1), launches including pre-passes].  Returns the number of values written or -1. */
+#define NAD_KERNEL_GEMV_M1 1   /* woq_gemv_m1_kernel: M = 1 decode */
+#define NAD_KERNEL_GEMV 2      /* woq_gemv_kernel: the stripe-stream GEMV, M <= 16 */
+#define NAD_KERNEL_SKINNY 3    /* woq_skinny_kernel: decode geometries the stream does not take */
+#define NAD_KERNEL_I8 4        /* woq_i8_kernel: int8-compute mode */
+#define NAD_KERNEL_GEMM3 5     /* woq_gemm3_kernel: prefill, int4 groups of 128 * 2^j */
+#define NAD_KERNEL_GEMM4 6     /* woq_gemm4_kernel: prefill, int4 g32 / g64, int2, int8 */
+#define NAD_KERNEL_GEMM2 7     /* woq_gemm2_kernel (NAD_GEMM_KERNEL=2) */
+#define NAD_KERNEL_GEMM 8      /* woq_gemm_kernel: register-staged prefill fallback */
+int nad_plan_forward(int bits, int n, int k, int blocksize, int scale_t, int asym, int m, int act_dtype, int64_t* out,
+                     int nout);
 /* fused Q/K/V (ip_fusion_qkv.cpp:22-93): out_i = X . W_i^T, one launch; W_i share K, blocksize, bits, scale dtype */
 int nad_device_qkv_forward(const void* act, int act_dtype, const void* wq, const void* wk, const void* wv, float* oq,
                            float* ok, float* ov, int m, int k, int lda, int ldo_q, int ldo_k, int ldo_v, void* queue);
@@ -192,7 +217,9 @@ size_t nad_synthetic_weight_size(int bits, int n, int k, int blocksize, int scal
  * bestla_packweight_copyattr, nad_blob_split) drops the copy of the buffer it writes, so a rewrite through the pack
  * API is always seen.  The cache is bounded (least recently used first out) by NAD_HOST_CACHE_MB, default 64 GiB. */
 void nad_host_cache_clear(void);
-/* drop the device copy of one blob (call before freeing or rewriting it outside the pack API) */
+/* drop the device copy of one blob.  MUST be called before a blob is freed, or rewritten in place by anything other
+ * than this library's pack entries: the per-call key samples the blob, so a partial rewrite (a few groups
+ * re-quantized) is not guaranteed to change it, and the forward would use the stale device copy. */
 void nad_host_cache_evict(const void* blob);
 /* cap on the cached device bytes (0 = the default); returns the previous cap */
 size_t nad_host_cache_set_limit(size_t bytes);
@@ -234,8 +261,12 @@ int nad_device_unpack_fp32(const void* devstor, float* host_out, void* queue);
 /* ===== decode chain: one decode step's WOQ matmuls as ONE persistent launch.  Replaces the sequence of device WOQ
  * nodes of a decode graph (ne_layers.c:7219-7316, fused QKV/FFN nodes ne_layers.c:8050-8170) -- a dependency-aware
  * BTLAGemmBatchDriver (bestla_gemm.cpp:508-624).  Ops run in order; op i may read any output of ops < i (written and
- * read through the device-wide hand-off inside the launch).  Constraints: int4, group size a multiple of 128, no
- * act-order shuffle, one activation dtype and symmetry for all ops, 1 <= m <= 8. */
+ * read through the device-wide hand-off inside the launch).  Constraints (nad_chain_create fails with a message
+ * otherwise): m = 1; fp32 activations; stripe-major int4 weights with groups of 64 or >= 128, or int2 with groups of
+ * 64, 128 or >= 256, at most two formats per chain and only the pairs (int2 g64, int4 g64) / (int2 g128, int4 g128);
+ * one symmetry; no act-order shuffle; fp arithmetic (not int8 compute); LINEAR epilogues NONE / RES_ADD, GATE_UP
+ * SILU_MUL / GELU_MUL; no op may write a vector (out or aux) that an earlier op of the chain reads from outside the
+ * chain (act, res, norm_w) or that it reads itself. */
 #define NAD_CHAIN_LINEAR 0   /* out[0] = epi(act . w[0]^T)                         (bestla_device_f32f32_forward) */
 #define NAD_CHAIN_QKV 1      /* out[j] = act . w[j]^T, j = 0..2                    (bestla_fusion_QKV_f32f32_forward) */
 #define NAD_CHAIN_GATE_UP 2  /* out[0] = silu/gelu(act . w[0]^T) * (act . w[1]^T) (ip_fusion_ffn.cpp:407-433); aux = act1 */
@@ -246,7 +277,7 @@ typedef struct nad_chain_op {
   int act_dtype, lda;
   float* out[3];
   int ldo[3];
-  int epi;                 /* NAD_EPI_*: LINEAR any single-output epilogue; GATE_UP SILU_MUL / GELU_MUL */
+  int epi;                 /* NAD_EPI_*: LINEAR NONE / RES_ADD; GATE_UP SILU_MUL / GELU_MUL */
   const float* bias;
   int bias_ld;
   const float* res;        /* NAD_EPI_RES_ADD residual [m][ld_res] (may be an earlier op's output) */
@@ -259,7 +290,7 @@ typedef struct nad_chain_op {
 } nad_chain_op;
 void* nad_chain_create(const nad_chain_op* ops, int n_ops, int m);
 int nad_chain_run(void* chain, void* queue);  /* asynchronous on queue; graph-capturable */
-int nad_chain_status(void* chain);            /* 0, or 1 if a hand-off wait timed out (synchronous) */
+int nad_chain_status(void* chain);            /* 0, or the first give-up code of a bounded wait (synchronous) */
 void nad_chain_destroy(void* chain);
 
 #ifdef __cplusplus

@@ -64,6 +64,9 @@ SIGNATURES = {
     "nad_device_weight_size": (_sz, [_p]),
     "nad_device_load": (_i, [_p, _p, _p, _sz, _p]),
     "nad_weight_info": (_i, [_p, _p]),
+    "nad_weight_info2": (_i, [_p, _p, _i]),
+    "nad_reload_knobs": (None, []),
+    "nad_plan_forward": (_i, [_i, _i, _i, _i, _i, _i, _i, _i, _p, _i]),
     "nad_blob_info": (_i, [_p, _p]),
     "nad_device_forward": (_i, [_p, _i, _p, _p, _i, _i, _i, _i, _i, _i, _p, _i, _p, _i, _p]),
     "nad_device_qkv_forward": (_i, [_p, _i, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _p]),
@@ -165,6 +168,11 @@ def header_symbols():
     names = re.findall(r"\b([A-Za-z_][A-Za-z0-9_]*)\s*\(", text)
     skip = {"if", "defined", "sizeof", "extern", "void"}
     return sorted({n for n in names if n not in skip and not n.isupper()})
+
+
+def reload_knobs():
+    """The library reads its NAD_* switches once; tests and A/B tools that change them at run time call this."""
+    lib().nad_reload_knobs()
 
 
 def last_error():

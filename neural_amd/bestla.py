@@ -165,6 +165,23 @@ def split_range(blob, axis, rank, world, unit=1):
 
 
 # ---------------------------------------------------------------------------------------------------- device
+KERNELS = {1: "woq_gemv_m1_kernel", 2: "woq_gemv_kernel", 3: "woq_skinny_kernel", 4: "woq_i8_kernel",
+           5: "woq_gemm3_kernel", 6: "woq_gemm4_kernel", 7: "woq_gemm2_kernel", 8: "woq_gemm_kernel"}
+
+
+def plan_forward(bits, n, k, group_size=128, scale_dtype="fp16", asym=False, m=1, act="fp32"):
+    """Which kernel a forward of this geometry launches, with what grid (nad_plan_forward: the host side of the call
+    with every launch recorded instead of issued -- no GPU needed)."""
+    o = np.zeros(6, np.int64)
+    st = {"fp32": 0, "bf16": 1, "fp16": 2}[scale_dtype]
+    at = {"fp32": 0, "fp16": 1, "bf16": 2}[act]
+    r = lib().nad_plan_forward(bits, n, k, group_size, st, int(asym), m, at, _ptr(o), 6)
+    if r != 6:
+        raise RuntimeError(f"nad_plan_forward failed: {last_error()}")
+    return dict(kernel=KERNELS.get(int(o[0]), str(int(o[0]))), grid=int(o[1]), threads=int(o[2]), ksplit=int(o[3]),
+                fold=bool(o[4]), launches=int(o[5]))
+
+
 def _torch():
     import torch
     if not torch.cuda.is_available():
@@ -210,7 +227,8 @@ class DeviceWeight:
             self.mem = _mem
             C.memmove(self.desc, _desc, len(self.desc))
         o = np.zeros(13, np.int64)
-        check(L.nad_weight_info(self.desc, _ptr(o)), "nad_weight_info")
+        if L.nad_weight_info2(self.desc, _ptr(o), 13) != 13:
+            raise RuntimeError(f"nad_weight_info2 failed: {last_error()}")
         (_, self.bits, self.n, self.k, self.blocksize, self.ns, self.nt, self.ng, self.scale_t, self.asym,
          self.has_shuffle, self.bytes, self.fold_ok) = (int(v) for v in o)
 

@@ -44,6 +44,81 @@ static void report(const char* where) { fprintf(stderr, "neural_amd: %s: %s\n", 
 extern "C" const char* nad_last_error(void) { return g_err.c_str(); }
 extern "C" void nad_clear_error(void) { g_err.clear(); }
 
+// ------------------------------------------------------------------------------------------------ knobs
+static int env_int(const char* name, int def) {
+  const char* v = getenv(name);
+  return (v && *v) ? atoi(v) : def;
+}
+
+// Tuning / A-B switches.  Read from the environment ONCE (at the first forward, or by nad_reload_knobs), never per
+// launch: the eager path an NE graph takes (one bestla_device_f32f32_forward per node) must not scan the environment.
+struct Knobs {
+  int gemv_wpc, gemv_grid, gemv_waves, gemv_pre, gemv_lean, gemv_ks, gemv_spw, gemv_disable;
+  int compute_int8;
+  int gemm2_disable, gemm4_all, gemm4_disable, ffn_f32, gemm_kernel, splitk_disable;
+  int gemm3_prio, gemm3_stagger, gemm4_stagger2, gemm_fold, gemm4_fold_all, gemm4_fold;
+  int engine_thin, engine_start_sync, engine_loaders, engine_depth, engine_slots;
+  int host_cache_mb, tile_kmajor;
+};
+static Knobs read_knobs() {
+  Knobs k{};
+  k.gemv_wpc = std::max(1, env_int("NAD_GEMV_WPC", 1));
+  k.gemv_grid = env_int("NAD_GEMV_GRID", 0);    // tests / tuning: cap the workgroups of a stripe-stream launch
+  k.gemv_waves = env_int("NAD_GEMV_WAVES", 0);  // tests / tuning: waves of a stripe-stream launch
+  k.gemv_pre = std::min(3, std::max(1, env_int("NAD_GEMV_PRE", 1)));
+  k.gemv_lean = env_int("NAD_GEMV_LEAN", 1);
+  k.gemv_ks = env_int("NAD_GEMV_KS", 2);        // K-slice width (tiles) of the M = 1 kernel's single-op launches
+  k.gemv_spw = env_int("NAD_GEMV_SPW", 4);
+  k.gemv_disable = env_int("NAD_GEMV_DISABLE", 0);
+  k.compute_int8 = env_int("NAD_COMPUTE_INT8", 0);
+  k.gemm2_disable = env_int("NAD_GEMM2_DISABLE", 0);
+  k.gemm4_all = env_int("NAD_GEMM4_ALL", 0);
+  k.gemm4_disable = env_int("NAD_GEMM4_DISABLE", 0);
+  k.ffn_f32 = env_int("NAD_FFN_F32", 0);
+  k.gemm_kernel = env_int("NAD_GEMM_KERNEL", 3);
+  k.splitk_disable = env_int("NAD_SPLITK_DISABLE", 0);
+  k.gemm3_prio = env_int("NAD_GEMM3_PRIO", 0);
+  k.gemm3_stagger = env_int("NAD_GEMM3_STAGGER", 1);  // measured +3-7 % (profiles/r02_gemm3_stagger.txt)
+  k.gemm4_stagger2 = env_int("NAD_GEMM4_STAGGER2", 0);
+  k.gemm_fold = env_int("NAD_GEMM_FOLD", 0);
+  k.gemm4_fold_all = env_int("NAD_GEMM4_FOLD_ALL", 0);
+  k.gemm4_fold = env_int("NAD_GEMM4_FOLD", 1);
+  k.engine_thin = env_int("NAD_ENGINE_THIN", 0);
+  k.engine_start_sync = env_int("NAD_ENGINE_START_SYNC", 0);
+  k.engine_loaders = env_int("NAD_ENGINE_LOADERS", 2);
+  k.engine_depth = env_int("NAD_ENGINE_DEPTH", 1);
+  k.engine_slots = env_int("NAD_ENGINE_SLOTS", 16);
+  k.host_cache_mb = env_int("NAD_HOST_CACHE_MB", 64 * 1024);
+  k.tile_kmajor = env_int("NAD_TILE_KMAJOR", 0);
+  return k;
+}
+static Knobs g_knobs = read_knobs();  // library load
+static const Knobs& knobs() { return g_knobs; }
+// re-read the NAD_* switches (tests and A/B tools that change the environment at run time; not thread-safe against
+// concurrent forwards)
+extern "C" void nad_reload_knobs(void) { g_knobs = read_knobs(); }
+
+// ------------------------------------------------------------------------------------------------ dry runs
+// nad_plan_forward runs the whole host side of a forward (validation, kernel choice, geometry, workspace sizing) with
+// every launch replaced by a record of it: which kernel would serve the call, and what the host path costs per call.
+struct NadPlan {
+  int kernel = 0, grid = 0, block = 0, ksplit = 1, fold = 0, launches = 0;
+};
+static thread_local NadPlan* t_plan = nullptr;
+// true (and the launch recorded) in a dry run; main = false for pre-passes (conversions, activation quantizers)
+static bool planned(int kernel, int grid, int block, int ksplit = 1, int fold = 0, bool main = true) {
+  if (!t_plan) return false;
+  t_plan->launches++;
+  if (main) {
+    t_plan->kernel = kernel;
+    t_plan->grid = grid;
+    t_plan->block = block;
+    t_plan->ksplit = ksplit;
+    t_plan->fold = fold;
+  }
+  return true;
+}
+
 // ------------------------------------------------------------------------------------------------ device context
 struct NadDevice {
   int device;
@@ -196,9 +271,8 @@ extern "C" int nad_device_load(const void* hostblob, void* devstor, void* device
   DeviceWeight w{};
   // per-channel (group >= K) is one group covering all tiles
   const int bs = b.blocksize >= b.k ? b.kpad : b.blocksize;
-  const char* km = getenv("NAD_TILE_KMAJOR");  // layout A/B switch (development); default K-major
   const uint64_t need = layout_geometry(w, device_bits(b.qtype), b.n, b.k, bs, scale_code(b.scale_t), b.asym,
-                                        b.has_shuffle, (km && *km) ? atoi(km) : 0, b.has_reduce);
+                                        b.has_shuffle, knobs().tile_kmajor, b.has_reduce);
   if (need > capacity) {
     set_err("device buffer too small for the tile layout: need %llu bytes, have %zu (see nad_device_weight_size)",
             (unsigned long long)need, capacity);
@@ -271,17 +345,21 @@ extern "C" void bestla_device_load_storage(void* hoststor, void* devstor, void* 
   if (nad_device_load(hoststor, devstor, deviceptr, b.size, queue) != 0) report("bestla_device_load_storage");
 }
 
-extern "C" int nad_weight_info(const void* devstor, int64_t* o) {
+// descriptor summary, versioned by the caller's buffer length: writes min(n, 13) values, returns the count written
+extern "C" int nad_weight_info2(const void* devstor, int64_t* o, int n) {
   const auto* w = static_cast<const DeviceWeight*>(devstor);
-  if (!w || w->magic != kWeightMagic) {
-    set_err("not a neural_amd device weight descriptor");
+  if (!w || w->magic != kWeightMagic || !o || n < 0) {
+    set_err("not a neural_amd device weight descriptor (or no output buffer)");
     return -1;
   }
-  int64_t v[13] = {w->magic, w->bits, w->n, w->k, w->blocksize, w->ns, w->nt, w->ng, w->scale_t, w->asym,
-                   w->has_shuffle, int64_t(w->bytes), w->fold_ok};
-  std::memcpy(o, v, sizeof(v));
-  return 0;
+  const int64_t v[13] = {w->magic, w->bits, w->n, w->k, w->blocksize, w->ns, w->nt, w->ng, w->scale_t, w->asym,
+                         w->has_shuffle, int64_t(w->bytes), w->fold_ok};
+  const int c = n < 13 ? n : 13;
+  std::memcpy(o, v, sizeof(int64_t) * size_t(c));
+  return c;
 }
+// the original 12-value form (callers built against the round-1 header)
+extern "C" int nad_weight_info(const void* devstor, int64_t* o) { return nad_weight_info2(devstor, o, 12) == 12 ? 0 : -1; }
 
 extern "C" int nad_blob_info(const void* hostblob, int64_t* o) {
   Blob b;
@@ -346,10 +424,6 @@ static void skinny_geometry(int total_stripes, int nt, int nwi, int* ks, int* tp
   *ch = t <= 4 ? 4 : 8;
 }
 
-static int env_int(const char* name, int def) {
-  const char* v = getenv(name);
-  return (v && *v) ? atoi(v) : def;
-}
 
 static int device_cus() {
   static int n = 0;
@@ -412,22 +486,22 @@ static int prepare_gemv(GemvArgs& a, int& waves, int& grid, int& gpt_out, const 
   }
   for (int i = nw; i < 3; i++) a.w[i] = a.w[0];
   a.units = a.dual ? ws[0]->ns : stripes;
-  const int wpc = std::max(1, env_int("NAD_GEMV_WPC", 1));
+  const Knobs& kn = knobs();
+  const int wpc = kn.gemv_wpc;
   grid = std::max(1, std::min(a.units, device_cus() * wpc));
-  if (env_int("NAD_GEMV_GRID", 0) > 0) grid = std::min(a.units, env_int("NAD_GEMV_GRID", 0));  // tests / tuning
+  if (kn.gemv_grid > 0) grid = std::min(a.units, kn.gemv_grid);  // tests / tuning
   waves = gemv_waves(w0.bits, w0.nt, w0.ng, w0.blocksize);
-  if (env_int("NAD_GEMV_WAVES", 0) > 0) waves = std::min(gpt > 1 ? 8 : 16, env_int("NAD_GEMV_WAVES", 0));
+  if (kn.gemv_waves > 0) waves = std::min(gpt > 1 ? 8 : 16, kn.gemv_waves);
   a.dq_mask = 0x000F000Fu;
   a.dq_magic = 0x64006400u;
-  a.pre_stages = std::min(3, std::max(1, env_int("NAD_GEMV_PRE", 1)));
+  a.pre_stages = kn.gemv_pre;
   a.u_q = a.units / grid;
   a.u_r = a.units % grid;
-  a.lean = env_int("NAD_GEMV_LEAN", 1);
-  a.valu = env_int("NAD_GEMV_VALU", 0);  // A/B: the M = 1 kernel's VALU dot-product body
+  a.lean = kn.gemv_lean;
   // M = 1 single-op launches may stream 2-tile K-slices, one per wave (up to 16 waves); the chain keeps 4-tile ones
   if (single_op)
-    gemv_lean_slices(a, w0.bits, &waves, env_int("NAD_GEMV_WAVES", 0) > 0 ? 4 : env_int("NAD_GEMV_KS", 2));
-  if (env_int("NAD_GEMV_SPW", 4) != 4) a.lean_spw = 2;  // A/B: long K back on the general stream kernel
+    gemv_lean_slices(a, w0.bits, &waves, kn.gemv_waves > 0 ? 4 : kn.gemv_ks);
+  if (kn.gemv_spw != 4) a.lean_spw = 2;  // A/B: long K back on the general stream kernel
   const size_t lds = gemv_lds_layout(a, w0.bits, waves, grid);
   if (lds > 160 * 1024) return 0;
   // buffer-resource offsets are 32-bit: every tile array, scale array and the activations must stay below 2 GiB
@@ -443,14 +517,16 @@ static int prepare_gemv(GemvArgs& a, int& waves, int& grid, int& gpt_out, const 
 static int try_gemv(const void* act, int act_t, int lda, int m, int k, int nw, const DeviceWeight* const* ws,
                     float* const* outs, const int* ldos, int epi, const float* bias, int bias_ld, const float* res,
                     int ld_res, float* aux, int ld_aux, hipStream_t st) {
-  if (env_int("NAD_GEMV_DISABLE", 0)) return 0;
+  if (knobs().gemv_disable) return 0;
   GemvArgs a{};
   int waves = 0, grid = 0, gpt = 0;
   if (!prepare_gemv(a, waves, grid, gpt, act, act_t, lda, m, k, nw, ws, outs, ldos, epi, bias, bias_ld, res, ld_res,
                     aux, ld_aux))
     return 0;
   const size_t lds = gemv_lds_layout(a, ws[0]->bits, waves, grid);
-  hipError_t e = launch_gemv(a, ws[0]->bits, waves, grid, lds, st);
+  hipError_t e = planned(gemv_uses_m1(a, ws[0]->bits, waves) ? NAD_KERNEL_GEMV_M1 : NAD_KERNEL_GEMV, grid, waves * 64)
+                     ? hipSuccess
+                     : launch_gemv(a, ws[0]->bits, waves, grid, lds, st);
   if (e != hipSuccess) {
     set_err("gemv kernel launch failed: %s", hipGetErrorString(e));
     return -1;
@@ -515,7 +591,9 @@ static int run_skinny(const void* act, int act_t, int lda, int m, int k, int nw,
   a.tiles_per_wave = tpw;
   a.steps_per_group = ws[0]->blocksize / 32;
   a.a_fast = (a.vec_ok && ws[0]->shuffle == nullptr && k % (act_t == kActF32 ? 4 : 8) == 0) ? 1 : 0;
-  hipError_t e = launch_skinny(a, ws[0]->bits, act_t, ks * (dual ? 2 : 1), stripes, ch, st);
+  hipError_t e = planned(NAD_KERNEL_SKINNY, stripes, ks * (dual ? 2 : 1) * 64)
+                     ? hipSuccess
+                     : launch_skinny(a, ws[0]->bits, act_t, ks * (dual ? 2 : 1), stripes, ch, st);
   if (e != hipSuccess) {
     set_err("skinny kernel launch failed: %s", hipGetErrorString(e));
     return -1;
@@ -560,6 +638,7 @@ extern "C" int nad_bind_workspace(void* queue, void* ptr, size_t bytes) {
 }
 
 static void* workspace_for(size_t bytes, hipStream_t st) {
+  if (t_plan) return reinterpret_cast<void*>(uintptr_t(1) << 40);  // dry run: sized, never touched
   if (t_call_ws.ptr && t_call_ws.bytes >= bytes) return t_call_ws.ptr;
   std::lock_guard<std::mutex> lk(g_ws_mu);
   auto b = g_bound_ws.find(st);
@@ -598,7 +677,7 @@ static int compute_mode() {
   if (t_compute_mode >= 0) return t_compute_mode;
   int m = g_compute_mode.load(std::memory_order_relaxed);
   if (m < 0) {
-    int init = env_int("NAD_COMPUTE_INT8", 0) ? 1 : 0, expect = -1;
+    int init = knobs().compute_int8 ? 1 : 0, expect = -1;
     g_compute_mode.compare_exchange_strong(expect, init);
     m = g_compute_mode.load(std::memory_order_relaxed);
   }
@@ -675,7 +754,7 @@ static int i8_quantize(I8Act& r, char* ws, const void* act, int act_t, int lda, 
     q.ldq = kp;
     q.kp = kp;
     q.sa = reinterpret_cast<float2*>(ws + align256(size_t(m) * kp));
-    hipError_t e = launch_q8_0_quant(q, act_t, st);
+    hipError_t e = planned(0, 0, 0, 1, 0, false) ? hipSuccess : launch_q8_0_quant(q, act_t, st);
     if (e != hipSuccess) {
       set_err("Q8_0 activation quantization launch failed: %s", hipGetErrorString(e));
       return -1;
@@ -697,7 +776,7 @@ static int i8_quantize(I8Act& r, char* ws, const void* act, int act_t, int lda, 
   q.ldq = kp;
   q.kp = kp;
   q.sa = reinterpret_cast<float2*>(ws + align256(size_t(m) * kp));
-  hipError_t e = launch_quant_u8(q, act_t, st);
+  hipError_t e = planned(0, 0, 0, 1, 0, false) ? hipSuccess : launch_quant_u8(q, act_t, st);
   if (e != hipSuccess) {
     set_err("activation quantization launch failed: %s", hipGetErrorString(e));
     return -1;
@@ -727,7 +806,7 @@ static int i8_gemm(const I8Act& x, int m, int k, const DeviceWeight& w, float* o
   a.aux = aux;
   a.ld_aux = ld_aux;
   a.w = view(w, out, ldo, bias, bias_ld);
-  hipError_t e = launch_i8(a, w.bits, st);
+  hipError_t e = planned(NAD_KERNEL_I8, 0, 0) ? hipSuccess : launch_i8(a, w.bits, st);
   if (e != hipSuccess) {
     set_err("int8-compute kernel launch failed: %s", hipGetErrorString(e));
     return -1;
@@ -876,12 +955,13 @@ struct A16 {
 
 // 3: gemm3 (int4, groups of 128 * 2^j); 4: gemm4 (int4 g32 / g64, int2 groups >= 64); 0: register-staged fallback
 static int pipelined_gemm(const DeviceWeight& w, int m) {
-  if (env_int("NAD_GEMM2_DISABLE", 0) || w.kmajor || w.f4kind >= 0 || m <= 16 ||
+  const Knobs& kn = knobs();
+  if (kn.gemm2_disable || w.kmajor || w.f4kind >= 0 || m <= 16 ||
       uint64_t(m) * uint64_t(w.nt) * 512 >= (1ull << 32))
     return 0;
   const int tpg = w.blocksize / 128;
-  if (w.bits == 4 && w.blocksize % 128 == 0 && (tpg & (tpg - 1)) == 0 && !env_int("NAD_GEMM4_ALL", 0)) return 3;
-  if (!env_int("NAD_GEMM4_DISABLE", 0) && gemm4_mode(w.bits, w.blocksize, w.ng, w.nt * tile_k(w.bits), w.asym)) return 4;
+  if (w.bits == 4 && w.blocksize % 128 == 0 && (tpg & (tpg - 1)) == 0 && !kn.gemm4_all) return 3;
+  if (!kn.gemm4_disable && gemm4_mode(w.bits, w.blocksize, w.ng, w.nt * tile_k(w.bits), w.asym)) return 4;
   return 0;
 }
 static bool gemm2_ok(const DeviceWeight& w, int m) { return pipelined_gemm(w, m) != 0; }
@@ -892,7 +972,7 @@ static bool ffn16_ok(const DeviceWeight& w1, const DeviceWeight& w2, const Devic
   auto ok = [&](const DeviceWeight& w) {
     return pipelined_gemm(w, m) && !w.shuffle && !int8_compute(w);
   };
-  return !env_int("NAD_FFN_F32", 0) && env_int("NAD_GEMM_KERNEL", 3) != 2 && ok(w1) && ok(w2) && ok(w3) &&
+  return !knobs().ffn_f32 && knobs().gemm_kernel != 2 && ok(w1) && ok(w2) && ok(w3) &&
          w2.nt * k_tile(w2) == fmid && fmid % 8 == 0;
 }
 
@@ -909,7 +989,7 @@ static int prepare_a16(A16& r, const void* act, int act_t, int lda, int m, int k
   }
   _Float16* buf = static_cast<_Float16*>(workspace_for(size_t(m) * kp * 2, st));
   if (!buf) return -1;
-  hipError_t e = launch_cvt_act(act, act_t, lda, m, k, kp, w.shuffle, buf, st);
+  hipError_t e = planned(0, 0, 0, 1, 0, false) ? hipSuccess : launch_cvt_act(act, act_t, lda, m, k, kp, w.shuffle, buf, st);
   if (e != hipSuccess) {
     set_err("activation conversion launch failed: %s", hipGetErrorString(e));
     return -1;
@@ -924,7 +1004,7 @@ static int prepare_a16(A16& r, const void* act, int act_t, int lda, int m, int k
 // count (1 = no split) and the K tiles per run.
 static int splitk_plan(const DeviceWeight& w, int m, int* ktiles) {
   *ktiles = w.nt;
-  if (env_int("NAD_SPLITK_DISABLE", 0)) return 1;
+  if (knobs().splitk_disable) return 1;
   const int tiles = ((m + 255) / 256) * ((w.ns + 7) / 8);
   if (tiles > 128) return 1;
   const int tpg = std::max(1, w.blocksize / k_tile(w));
@@ -966,19 +1046,20 @@ static int run_gemm(const void* act, int act_t, int lda, int m, int k, const Dev
   a.ld_res = ld_res;
   a.aux = aux;
   a.ld_aux = ld_aux;
-  a.prio = env_int("NAD_GEMM3_PRIO", 0);
-  a.stagger = env_int("NAD_GEMM3_STAGGER", 1);  // measured +3-7 % (profiles/r02_gemm3_stagger.txt)
-  a.stagger2 = env_int("NAD_GEMM4_STAGGER2", 0);
+  const Knobs& kn = knobs();
+  a.prio = kn.gemm3_prio;
+  a.stagger = kn.gemm3_stagger;  // measured +3-7 % (profiles/r02_gemm3_stagger.txt)
+  a.stagger2 = kn.gemm4_stagger2;
   // scale folding measured 1-5 % SLOWER on gemm3 (profiles/r03_gemm3_fold.txt) and it rounds q * s to fp16: opt-in
-  a.fold = w.fold_ok && env_int("NAD_GEMM_FOLD", 0) ? 1 : 0;
+  a.fold = w.fold_ok && kn.gemm_fold ? 1 : 0;
   a.w = view(w, out, ldo, bias, bias_ld);
   const int pg = pipelined_gemm(w, m);
   // gemm4 at groups of 32 / 64 scales the products into the result every 32 / 64 k (4 / 2 FMAs per MFMA): there the
   // fold pays, +14-23 %; at groups of 128 (int2 / int8: int4 g128 runs gemm3) it measured +6-21 % with the int2 stagger
   // it enables (profiles/r03_gemm4_g128_fold.txt) but is opt-in (NAD_GEMM4_FOLD_ALL=1) until the full GPU suite has run
   // with it; NAD_GEMM4_FOLD=0 restores the exact fp32 per-group path (gemm4 scale folding)
-  if (pg == 4 && (w.blocksize == 32 || w.blocksize == 64 || env_int("NAD_GEMM4_FOLD_ALL", 0)))
-    a.fold = w.fold_ok && env_int("NAD_GEMM4_FOLD", 1) ? 1 : 0;
+  if (pg == 4 && (w.blocksize == 32 || w.blocksize == 64 || kn.gemm4_fold_all))
+    a.fold = w.fold_ok && kn.gemm4_fold ? 1 : 0;
   if (h16) {
     if (!pg) {
       set_err("fp16 GEMM output needs the pipelined GEMM");
@@ -994,7 +1075,7 @@ static int run_gemm(const void* act, int act_t, int lda, int m, int k, const Dev
       if (prepare_a16(own, act, act_t, lda, m, k, w, st) < 0) return -1;
       pre = &own;
     }
-    const bool g2 = pg == 3 && env_int("NAD_GEMM_KERNEL", 3) == 2;
+    const bool g2 = pg == 3 && kn.gemm_kernel == 2;
     int ktiles = w.nt;
     const int ks = !g2 ? splitk_plan(w, m, &ktiles) : 1;
     if (ks > 1) {  // partials after the fp16 activations in the same workspace (stream-ordered reuse)
@@ -1006,6 +1087,11 @@ static int run_gemm(const void* act, int act_t, int lda, int m, int k, const Dev
       if (!base) return -1;
       a.part = reinterpret_cast<float*>(base + a16);
     }
+    const int tiles = ((m + 255) / 256) * ((w.n + 127) / 128);
+    if (planned(pg == 4 ? NAD_KERNEL_GEMM4 : (g2 ? NAD_KERNEL_GEMM2 : NAD_KERNEL_GEMM3), tiles * ks, 512, ks, a.fold)) {
+      if (ks > 1) planned(0, 0, 0, 1, 0, false);  // the split-K reduce
+      return 0;
+    }
     hipError_t e = pg == 4 ? launch_gemm4(a, w.bits, pre->p, pre->ld, st)
                    : g2    ? launch_gemm2(a, pre->p, pre->ld, st)
                            : launch_gemm3(a, pre->p, pre->ld, st);
@@ -1016,7 +1102,7 @@ static int run_gemm(const void* act, int act_t, int lda, int m, int k, const Dev
     }
     return 0;
   }
-  hipError_t e = launch_gemm(a, w.bits, act_t, st);
+  hipError_t e = planned(NAD_KERNEL_GEMM, 0, 0) ? hipSuccess : launch_gemm(a, w.bits, act_t, st);
   if (e != hipSuccess) {
     set_err("gemm kernel launch failed: %s", hipGetErrorString(e));
     return -1;
@@ -1067,6 +1153,32 @@ extern "C" void bestla_device_f32f32_forward(float* activation, void* weiptr, fl
   if (nad_device_forward(activation, kActF32, weiptr, output, _m, _n, _k, lda, ldo, kEpiNone, nullptr, 0, nullptr, 0,
                          queue) != 0)
     report("bestla_device_f32f32_forward");
+}
+
+extern "C" int nad_plan_forward(int bits, int n, int k, int blocksize, int scale_t, int asym, int m, int act_dtype,
+                                int64_t* out, int nout) {
+  if ((bits != 2 && bits != 4 && bits != 8) || n <= 0 || k <= 0 || m <= 0 || !out || nout < 0) {
+    set_err("nad_plan_forward: bad arguments (bits=%d n=%d k=%d m=%d)", bits, n, k, m);
+    return -1;
+  }
+  if (blocksize <= 0) blocksize = k;
+  DeviceWeight w{};
+  layout_geometry(w, bits, n, k, blocksize, scale_t, asym != 0, false, knobs().tile_kmajor);
+  layout_assign(w, reinterpret_cast<void*>(uintptr_t(1) << 41));  // never dereferenced on the host
+  w.f4kind = -1;
+  w.fold_ok = 1;
+  w.owner = nullptr;
+  NadPlan plan;
+  t_plan = &plan;
+  const void* act = reinterpret_cast<const void*>(uintptr_t(1) << 42);
+  float* y = reinterpret_cast<float*>(uintptr_t(1) << 43);
+  const int rc = nad_device_forward(act, act_dtype, &w, y, m, n, k, k, n, kEpiNone, nullptr, 0, nullptr, 0, nullptr);
+  t_plan = nullptr;
+  if (rc) return -1;
+  const int64_t v[6] = {plan.kernel, plan.grid, plan.block, plan.ksplit, plan.fold, plan.launches};
+  const int c = nout < 6 ? nout : 6;
+  std::memcpy(out, v, sizeof(int64_t) * size_t(c));
+  return c;
 }
 
 static bool same_kind(const DeviceWeight& a, const DeviceWeight& b) {
@@ -1225,7 +1337,7 @@ extern "C" int nad_device_ffn_forward(const void* act, int act_dtype, const void
 // GELU_MUL.  The reference graph cuts such a segment at every attention node (ne_layers.c:11915-12028).
 struct NadChain {
   EngOp* dev_ops = nullptr;
-  unsigned* ctl = nullptr;              // [0] generation, [1] status
+  unsigned* ctl = nullptr;              // [0] generation, [1] status, [2] workgroup arrivals (monotonic)
   unsigned long long* gran = nullptr;   // granule arrays of the results read inside the launch
   int n_ops = 0, grid = 0, bump = 0;
   EngGeometry g{};
@@ -1235,6 +1347,11 @@ namespace {
 struct ChainOut {
   const float* p;
   int n, op, wi;
+};
+struct ChainWrite {
+  std::pair<const char*, const char*> range;
+  int op;
+  bool aux;
 };
 }  // namespace
 
@@ -1246,6 +1363,7 @@ extern "C" void* nad_chain_create(const nad_chain_op* ops, int n_ops, int m) {
   const int grid = device_cus();
   std::vector<EngOp> host(static_cast<size_t>(n_ops));
   std::vector<ChainOut> outs;                       // every result of the launch, in op order
+  std::vector<ChainWrite> writes, ext_reads;        // byte ranges written (results, aux) / read from outside the chain
   std::vector<std::vector<int>> need_gran(static_cast<size_t>(n_ops), std::vector<int>(3, 0));
   EngGeometry g{};
   g.bits = 0;
@@ -1395,6 +1513,42 @@ extern "C" void* nad_chain_create(const nad_chain_op* ops, int n_ops, int m) {
       }
       e.res = o.res;
     }
+    // write-after-read: the engine orders only the hand-offs that go through granules, so a vector read from outside
+    // the chain (an external act / res, norm_w) must not be written by this or any later op while slower workgroups
+    // may still read it, and nothing may read an op's aux (it has no granules)
+    {
+      auto span = [](const void* p, size_t n) { return std::make_pair(static_cast<const char*>(p),
+                                                                       static_cast<const char*>(p) + 4 * n); };
+      auto hit = [](std::pair<const char*, const char*> x, std::pair<const char*, const char*> y) {
+        return x.first < y.second && y.first < x.second;
+      };
+      std::vector<std::pair<const char*, const char*>> rd;
+      if (!e.act_tag) rd.push_back(span(o.act, size_t(e.K)));
+      if (epi == kEpiResAdd && !e.res_tag) rd.push_back(span(o.res, size_t(w0.n)));
+      if (o.norm && o.norm_w) rd.push_back(span(o.norm_w, size_t(e.K)));
+      for (const auto& r0 : rd) {
+        for (const ChainWrite& wv : writes)
+          if (hit(r0, wv.range)) {
+            set_err("nad_chain_create: op %d reads a vector from outside the chain that overlaps op %d's %s", i, wv.op,
+                    wv.aux ? "aux (aux has no in-launch hand-off)" : "result without being it");
+            return nullptr;
+          }
+        ext_reads.push_back(ChainWrite{r0, i, false});
+      }
+      std::vector<ChainWrite> mine;
+      for (int j = 0; j < nw; j++)
+        if (e.w[j].out) mine.push_back(ChainWrite{span(e.w[j].out, size_t(e.w[j].n)), i, false});
+      if (e.aux) mine.push_back(ChainWrite{span(e.aux, size_t(w0.n)), i, true});
+      for (const ChainWrite& wv : mine) {
+        for (const ChainWrite& r0 : ext_reads)
+          if (hit(wv.range, r0.range)) {
+            set_err("nad_chain_create: op %d writes its %s over a vector op %d reads from outside the chain "
+                    "(write-after-read inside one launch)", i, wv.aux ? "aux" : "result", r0.op);
+            return nullptr;
+          }
+        writes.push_back(wv);
+      }
+    }
     for (int j = 0; j < nw; j++)
       if (e.w[j].out) outs.push_back(ChainOut{e.w[j].out, e.w[j].n, i, j});
     kp = std::max(kp, w0.nt * KT);
@@ -1410,18 +1564,15 @@ extern "C" void* nad_chain_create(const nad_chain_op* ops, int n_ops, int m) {
     std::swap(g.gpt, g.gpt1);
     for (EngOp& e : host) e.fmt ^= 1;
   }
-  g.thin = env_int("NAD_ENGINE_THIN", 0) ? 1 : 0;  // bit 0: loader thinned during gathers (measured slower: off)
+  const Knobs& kn = knobs();
+  g.thin = kn.engine_thin ? 1 : 0;  // bit 0: loader thinned during gathers (measured slower: off)
   // bit 1: the loaders start after every consumer issued the first op's input loads (woq_chain.hip start sync)
-  if (env_int("NAD_ENGINE_START_SYNC", 0)) g.thin |= 2;  // measured 2 % slower (profiles/r03_engine_start_sync.txt)
-  g.loaders = env_int("NAD_ENGINE_LOADERS", 2);  // loader waves (tools/dma_probe.hip: 2 x 2 fills in flight best)
-  g.depth = env_int("NAD_ENGINE_DEPTH", 1);      // fills in flight per loader wave (1 measured faster than 2)
-  // consumer arithmetic: fp16 hi + lo (default) or the int8-limb form (woq_chain.hip X8, NAD_ENGINE_X8=1): X8 streams
-  // the weights 22-25 % faster per tile but stages each input 0.6-1.1 us slower, which is on every hand-off's critical
-  // path -- measured 3-10 % slower per token
-  g.x8 = env_int("NAD_ENGINE_X8", 0) ? 1 : 0;
+  if (kn.engine_start_sync) g.thin |= 2;  // measured 2 % slower (profiles/r03_engine_start_sync.txt)
+  g.loaders = kn.engine_loaders;  // loader waves (tools/dma_probe.hip: 2 x 2 fills in flight best)
+  g.depth = kn.engine_depth;      // fills in flight per loader wave (1 measured faster than 2)
   g.sd = int((sd_bytes + 1023) / 1024);
   if (g.sd < 1) g.sd = 1;
-  g.max_slots = env_int("NAD_ENGINE_SLOTS", 16);  // ring slots at most (A/B of the ring's size)
+  g.max_slots = kn.engine_slots;  // ring slots at most (A/B of the ring's size)
   if (g.sd > 2 || !engine_geometry(g, kp)) {
     set_err("nad_chain_create: the engine's LDS ring does not fit (K up to %d, %zu scale bytes per fill)", kp,
             sd_bytes);
@@ -1539,8 +1690,7 @@ extern "C" int nad_synthetic_weight(void* devstor, void* deviceptr, size_t capac
     return -1;
   }
   DeviceWeight w{};
-  const char* km = getenv("NAD_TILE_KMAJOR");
-  uint64_t need = layout_geometry(w, bits, n, k, blocksize, scale_t, asym != 0, false, (km && *km) ? atoi(km) : 0);
+  uint64_t need = layout_geometry(w, bits, n, k, blocksize, scale_t, asym != 0, false, knobs().tile_kmajor);
   if (need > capacity) {
     set_err("capacity %zu < needed %llu", capacity, (unsigned long long)need);
     return -1;
@@ -1680,7 +1830,7 @@ NadDevice* host_device() {
 uint64_t cache_limit() {
   HostCtx& c = hctx();
   if (c.limit) return c.limit;
-  const uint64_t mb = uint64_t(env_int("NAD_HOST_CACHE_MB", 64 * 1024));
+  const uint64_t mb = uint64_t(knobs().host_cache_mb);
   return (mb ? mb : 1) << 20;
 }
 // one host-ABI call (holds the context lock): the weights it fetches stay cached until it returns

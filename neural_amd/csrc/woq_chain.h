@@ -66,12 +66,12 @@ struct EngGeometry {
                                 // loaders wait for the consumers' first input loads (NAD_ENGINE_START_SYNC)
   int loaders, depth;           // loader waves, fills in flight per loader wave
   int max_slots;                // cap on the ring's slots (A/B; 16 = as many as fit)
-  int x8;                       // consumer arithmetic: 0 fp16 hi + lo (default), 1 int8 limbs on i8 MFMA (NAD_ENGINE_X8)
 };
 
 // fills g.kp/slots/lds from g.bits/gpt/asym/sd and the ops' largest padded K; false if the ring does not fit
 bool engine_geometry(EngGeometry& g, int kp);
-// ops: device array; ctl: [0] launch generation (tags), [1] status (0 ok, else the first give-up code); bump: some op
+// ops: device array; ctl: [0] launch generation (tags), [1] status (0 ok, else the first give-up code), [2] workgroup
+// arrivals (the last one of a launch bumps [0]); bump: some op
 // reads a result of this launch (the generation then moves on after the launch)
 // the (bits, groups per tile) formats one launch may hold: one of int4 g >= 128 / g64, int2 g >= 256 / g128 / g64, or the
 // mixed pairs (int2 g64, int4 g64) and (int2 g128, int4 g128)

@@ -38,8 +38,6 @@
 //   * every spin is bounded (~1 s); a give-up records a code in ctl[1] and the launch still terminates;
 //   * one launch may hold two weight formats (the op body is a generic lambda over (bits, groups per tile)): Mistral's
 //     int2 policy keeps wv / w2 at int4 (llama_utils.cpp:269-287);
-//   * opt-in (NAD_ENGINE_X8=1): int8-limb consumers on v_mfma_i32_16x16x64_i8 (see X8 below), each consumer staging
-//     exactly the tiles it reads, no barrier.
 // Arithmetic per op is the same for every position of the op in a launch: a one-op launch of it gives bit-identical
 // outputs (tests/test_chain_gpu.py).
 #include <hip/hip_runtime.h>
@@ -343,69 +341,6 @@ __device__ __forceinline__ float lds_scale(const char* p, int st) {
   return st == kScaleBF16 ? bf16_bits_to_f32(h) : f16_bits_to_f32(h);
 }
 
-// ---- int8-limb arithmetic (X8, the default): the input vector as three int8 limbs per element, exact integer products
-// on v_mfma_i32_16x16x64_i8.  Per 128-k block b of the input: S_b = amax_b / 127 and x = S_b (a0 + a1 / 128 + a2 / 128^2)
-// + e with |a0| <= 127, |a1|, |a2| <= 64 and |e| <= S_b 2^-15 (~2.4e-7 amax_b: the precision of the fp16 hi + lo split).
-// Limb j is MFMA row j (rows 3..15 read duplicates and are ignored).  B = the stored codes as bytes (q + bias: int4
-// 0..15, int2 0..3 -- one and + one shift per four weights, against nine VALU per eight weights for the fp16 form), and a
-// second MFMA per 64 k with B = splat(-(bias + zp)) folds the offset in, so the int32 result of a segment is exactly
-// sum_k (q_k - zp) a_j[k].  The limb results meet once per segment (one group, at most one block) in fp32.
-// LDS image of the limbs: block b at 384 b, MFMA u (64 k) of the block at +192 u, limb row j at +64 j, lane group kq at
-// +16 kq; inside those 16 bytes the byte order of the B operand the tile layout yields (woq_layout.h), i.e. dword di of
-// an int4 MFMA u holds elements {0, 4, 1, 5} (+2 for odd di) of 32-k step 2u + di / 2, of an int2 one the crumbs at
-// bit 2 di of steps 2u / 2u + 1, elements {0, 0, 1, 1} + 2 di.
-typedef int i4v_t __attribute__((ext_vector_type(4)));
-constexpr int kX8Rows = 3;          // limbs per element
-constexpr int kX8BlockBytes = 384;  // LDS bytes of one 128-k block: 2 MFMAs x 3 rows x 4 lane groups x 16 B
-__host__ __device__ constexpr int x8_act_bytes(int kp) { return 3 * kp + ((kp / 128 * 4 + 15) & ~15); }
-
-// quad Qi (four elements: pairs q1 = (2 q1, 2 q1 + 1) and q2) of the limb image, and the byte offset of its dword
-template <int BITS>
-__device__ __forceinline__ void x8_quad(int Qi, int& q1, int& q2, uint32_t& off) {
-  const int b = Qi >> 5, r = Qi & 31, uu = r >> 4, kq = (r >> 2) & 3, di = r & 3;
-  if constexpr (BITS == 4) {
-    q1 = 64 * b + 16 * (2 * uu + (di >> 1)) + 4 * kq + (di & 1);
-    q2 = q1 + 2;
-  } else {
-    q1 = 128 * (b >> 1) + 32 * (2 * (b & 1) + uu) + 4 * kq + di;
-    q2 = q1 + 16;
-  }
-  off = uint32_t(b * kX8BlockBytes + uu * 192 + kq * 16 + di * 4);
-}
-// max over the 32 lanes of this half-wave, all in VALU: DPP within each 16-lane row (quad xor 1, quad xor 2, half-row
-// mirror, row mirror), then v_permlane16_swap pairs rows 0/1 and 2/3 (a ds_swizzle chain would be five LDS round trips)
-__device__ __forceinline__ float max32(float v) {
-  int x = __float_as_int(v);
-  x = __float_as_int(fmaxf(__int_as_float(x), __int_as_float(__builtin_amdgcn_update_dpp(x, x, 0xB1, 0xF, 0xF, false))));
-  x = __float_as_int(fmaxf(__int_as_float(x), __int_as_float(__builtin_amdgcn_update_dpp(x, x, 0x4E, 0xF, 0xF, false))));
-  x = __float_as_int(fmaxf(__int_as_float(x), __int_as_float(__builtin_amdgcn_update_dpp(x, x, 0x141, 0xF, 0xF, false))));
-  x = __float_as_int(fmaxf(__int_as_float(x), __int_as_float(__builtin_amdgcn_update_dpp(x, x, 0x140, 0xF, 0xF, false))));
-  const auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
-  return fmaxf(__int_as_float(int(r[0])), __int_as_float(int(r[1])));
-}
-// MFMA u's B operand (16 bytes = 16 k per lane) from the lane's 16-byte tile slice
-template <int BITS>
-__device__ __forceinline__ i4v_t x8_bytes(const u4_t& w, int u) {
-  i4v_t r;
-  if constexpr (BITS == 4) {
-    const uint32_t m = 0x0F0F0F0Fu, w0 = w[2 * u], w1 = w[2 * u + 1];
-    r[0] = int(w0 & m);
-    r[1] = int((w0 >> 4) & m);
-    r[2] = int(w1 & m);
-    r[3] = int((w1 >> 4) & m);
-  } else {
-    const uint32_t m = 0x03030303u, x = w[u];
-    r[0] = int(x & m);
-    r[1] = int((x >> 2) & m);
-    r[2] = int((x >> 4) & m);
-    r[3] = int((x >> 6) & m);
-  }
-  return r;
-}
-__device__ __forceinline__ uint32_t pack4(int a, int b, int c, int d) {
-  return (uint32_t(a) & 0xFFu) | ((uint32_t(b) & 0xFFu) << 8) | ((uint32_t(c) & 0xFFu) << 16) | (uint32_t(d) << 24);
-}
-
 // consumer-only barrier: an LDS arrival counter (the loader never joins)
 __device__ __forceinline__ void cbar(uint32_t a, unsigned& epoch, unsigned* ctl, int lane, bool& failed) {
   epoch += NC;
@@ -425,7 +360,7 @@ using IC = std::integral_constant<int, V>;
 
 // One launch holds ops of at most two weight formats (B0, G0) and (B1, G1) (bits, groups per tile; EngOp::fmt picks
 // one), e.g. Mistral's int2 g64 projections beside its int4 g64 wv / w2 (llama_utils.cpp:269-287)
-template <int B0, int G0, int B1, int G1, bool ASYM, int SD, bool X8>
+template <int B0, int G0, int B1, int G1, bool ASYM, int SD>
 __global__ __launch_bounds__(kEngMaxThreads, 1) void woq_engine_kernel(const EngOp* __restrict__ ops, int n_ops,
                                                                        unsigned* ctl, int S, int slot_bytes, int Kp,
                                                                        int bump, int thin, int nl, int depth) {
@@ -435,9 +370,8 @@ __global__ __launch_bounds__(kEngMaxThreads, 1) void woq_engine_kernel(const Eng
   const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));
   const uint32_t ctl_a = lds_addr(smem);
   float* part = reinterpret_cast<float*>(smem + kCtlBytes);          // [stripe][consumer][16]
-  // fp16: [Kp / 8] units of {hi[8], lo[8]}; X8: the limb image (3 Kp bytes) + the block scales S_b 2^-14 (Kp / 128)
-  char* act = smem + kCtlBytes + kPartBytes;
-  char* zrows = act + (X8 ? size_t(x8_act_bytes(Kp)) : size_t(Kp) * 4);  // kEngZeroBytes of zeros (never written)
+  char* act = smem + kCtlBytes + kPartBytes;             // [Kp / 8] units of {hi[8], lo[8]}
+  char* zrows = act + size_t(Kp) * 4;                   // kEngZeroBytes of zeros (never written)
   char* ring = zrows + kEngZeroBytes;
   if (threadIdx.x < kCtlBytes / 4) reinterpret_cast<unsigned*>(smem)[threadIdx.x] = 0u;
   if (threadIdx.x < kEngZeroBytes / 4) reinterpret_cast<unsigned*>(zrows)[threadIdx.x] = 0u;
@@ -452,9 +386,6 @@ __global__ __launch_bounds__(kEngMaxThreads, 1) void woq_engine_kernel(const Eng
   }
 
   const int cw = wave, cl = wave * 64 + lane;  // consumer wave, consumer lane
-#ifdef NAD_EXP_PRIO  // experiment: the younger half of the consumers at a higher issue priority
-  if (cw >= NC / 2) __builtin_amdgcn_s_setprio(NAD_EXP_PRIO);
-#endif
   const uint32_t full_a = ctl_a + kFull * 4, free_a = ctl_a + kFree * 4, bar_a = ctl_a + kBar * 4;
   float* nsum = reinterpret_cast<float*>(smem) + kNsum;
   const unsigned gen = __builtin_amdgcn_readfirstlane(__hip_atomic_load(ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
@@ -523,130 +454,7 @@ __global__ __launch_bounds__(kEngMaxThreads, 1) void woq_engine_kernel(const Eng
     //    u = q / 4 -> hi at byte 32 u + 4 (q & 3), lo 16 bytes further.  An RMSNorm of the input is applied as
     //    x * g here and the scalar 1 / rms(x) on the results (y = W (x * g) / rms: the same products, no second pass)
     float s2 = 0.f;
-    if constexpr (X8) {
-      // 1') this consumer's tiles of the input as int8 limbs (see x8_quad): each lane takes quads of four elements (two
-      //     pairs = two granule loads), one 32-lane half-wave exactly one 128-k block, so the block's amax is a
-      //     half-wave reduction; like the fp16 form, a consumer stages exactly the tiles it reads (no barrier)
-      constexpr int QJ = 4, QPT = KT / 4;  // quads per lane per pass, quads per tile
-      constexpr float kMagic = 12582912.f;  // 1.5 * 2^23: RN(v + kMagic) holds rint(v) in its low mantissa bits
-      const int npair = (K + 1) / 2;
-      const int nqc = (nt > cw ? (nt - cw + NC - 1) / NC : 0) * QPT;  // this consumer's quads
-      const bool gw = o_norm && o_norm_w;
-      float* sblk = reinterpret_cast<float*>(act + 3 * Kp);
-      for (int i0 = 0; i0 < nqc; i0 += 64 * QJ) {
-        int qa[QJ], qb[QJ], qi[QJ];
-        uint32_t off[QJ];
-        float xv[QJ][4];  // byte order: x[2 qa], x[2 qb], x[2 qa + 1], x[2 qb + 1]
-        float nw[QJ][4];  // RMSNorm weights, loaded before the input arrives (not a round trip after it)
-#pragma unroll
-        for (int j = 0; j < QJ; j++) {
-          const int i = i0 + lane + 64 * j;
-          qi[j] = i < nqc ? (cw + NC * (i / QPT)) * QPT + (i % QPT) : -1;
-          x8_quad<BITS>(max(qi[j], 0), qa[j], qb[j], off[j]);
-          const int ks[4] = {2 * qa[j], 2 * qb[j], 2 * qa[j] + 1, 2 * qb[j] + 1};
-#pragma unroll
-          for (int e = 0; e < 4; e++) {
-            xv[j][e] = 0.f;
-            nw[j][e] = gw && qi[j] >= 0 && ks[e] < K ? o_norm_w[ks[e]] : 0.f;
-          }
-        }
-        auto take = [&](int j, int side, float x0, float x1) {  // side 0: pair qa, 1: pair qb
-          xv[j][side] = x0;
-          xv[j][2 + side] = x1;
-        };
-        if (o_act_gran) {
-          const unsigned want = gen * 256u + o_act_tag;
-          const auto rg = rsrc(o_act_gran, unsigned(K) * 8u);
-          uint32_t pend = 0;
-#pragma unroll
-          for (int j = 0; j < QJ; j++) {
-            if (qi[j] >= 0) {
-              if (qa[j] < npair) pend |= 1u << (2 * j);
-              if (qb[j] < npair) pend |= 2u << (2 * j);
-            }
-          }
-          unsigned spins = 0;
-          while (true) {
-            uint4 g[2 * QJ];
-#pragma unroll
-            for (int j = 0; j < 2 * QJ; j++) {
-              const int q = (j & 1) ? qb[j >> 1] : qa[j >> 1];
-              g[j] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rg, (pend >> j) & 1u ? q * 16 : kOOB,
-                                                                                      0, kSC1));
-            }
-            __builtin_amdgcn_sched_barrier(0);  // every load of the pass in flight before the first tag check
-#pragma unroll
-            for (int j = 0; j < 2 * QJ; j++) {
-              const int q = (j & 1) ? qb[j >> 1] : qa[j >> 1];
-              const bool ok1 = 2 * q + 1 >= K || g[j].w == want;  // odd K: the second granule is never written
-              if (((pend >> j) & 1u) && g[j].y == want && ok1) {
-                take(j >> 1, j & 1, __uint_as_float(g[j].x), 2 * q + 1 < K ? __uint_as_float(g[j].z) : 0.f);
-                pend &= ~(1u << j);
-              }
-            }
-            if (cw == 0 && spins == 0 && i0 == 0) ETRACE(11, op, wall_clock64());  // first pass returned
-            if (__all(pend == 0u) || failed) break;
-            __builtin_amdgcn_s_sleep(1);
-            if (++spins > kSpinMax) {
-              if (lane == 0) give_up(ctl, 3);
-              failed = true;
-            }
-          }
-        } else {  // an external vector (written before this launch): plain loads, all of a pass in flight at once
-          const auto ra = rsrc(o_act, unsigned(K) * 4u);
-          uint2 g[2 * QJ];
-#pragma unroll
-          for (int j = 0; j < 2 * QJ; j++) {
-            const int q = (j & 1) ? qb[j >> 1] : qa[j >> 1];
-            const bool in = qi[j >> 1] >= 0 && q < npair;
-            g[j] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(ra, in ? q * 8 : kOOB, 0, 0));
-          }
-          __builtin_amdgcn_sched_barrier(0);
-          if ((thin & 2) && op == 0 && i0 == 0 && lane == 0) lds_add(ctl_a + kStart * 4, 1u);  // start sync
-          if (cw == 0 && i0 == 0) ETRACE(11, op, wall_clock64());
-#pragma unroll
-          for (int j = 0; j < 2 * QJ; j++) {
-            const int q = (j & 1) ? qb[j >> 1] : qa[j >> 1];
-            // out-of-range bytes read 0 (K tail, odd K)
-            take(j >> 1, j & 1, __uint_as_float(g[j].x), 2 * q + 1 < K ? __uint_as_float(g[j].y) : 0.f);
-          }
-        }
-        // the pass is complete: squares in slot order, then the limbs of every quad
-#pragma unroll
-        for (int j = 0; j < QJ; j++) {
-          if (i0 + 64 * j >= nqc) break;  // whole half-waves (nqc is a multiple of 32)
-          if (qi[j] < 0) continue;
-          float* x = xv[j];
-          s2 += __builtin_fmaf(x[3], x[3], __builtin_fmaf(x[2], x[2], __builtin_fmaf(x[1], x[1], x[0] * x[0])));
-          if (gw) {
-#pragma unroll
-            for (int e = 0; e < 4; e++) x[e] *= nw[j][e];
-          }
-          const float amax = max32(fmaxf(fmaxf(fabsf(x[0]), fabsf(x[1])), fmaxf(fabsf(x[2]), fabsf(x[3]))));
-          const float inv = amax > 0.f ? 127.f * __builtin_amdgcn_rcpf(amax) : 0.f;
-          // limbs by magic-number rounding: t = RN(v + kMagic) carries rint(v) in its low byte (two's complement),
-          // t - kMagic is that integer exactly, and one fma gives the next residual
-          uint32_t t[kX8Rows][4];
-#pragma unroll
-          for (int e = 0; e < 4; e++) {
-            const float t0 = __builtin_fmaf(x[e], inv, kMagic);
-            const float r1 = __builtin_fmaf(x[e], inv, -(t0 - kMagic));
-            const float t1 = __builtin_fmaf(r1, 128.f, kMagic);
-            const float r2 = __builtin_fmaf(r1, 128.f, -(t1 - kMagic));
-            t[0][e] = __float_as_uint(t0);
-            t[1][e] = __float_as_uint(t1);
-            t[2][e] = __float_as_uint(__builtin_fmaf(r2, 128.f, kMagic));
-          }
-          char* base = act + off[j];
-#pragma unroll
-          for (int row = 0; row < kX8Rows; row++)
-            *reinterpret_cast<uint32_t*>(base + row * 64) = __builtin_amdgcn_perm(t[row][1], t[row][0], 0x0c0c0400u) |
-                                                             __builtin_amdgcn_perm(t[row][3], t[row][2], 0x04000c0cu);
-          if ((lane & 31) == 0) sblk[qi[j] >> 5] = amax * (1.f / 127.f) * (1.f / 16384.f);
-        }
-      }
-      if ((thin & 2) && op == 0 && nqc == 0 && lane == 0) lds_add(ctl_a + kStart * 4, 1u);  // no tiles: start sync
-    } else {
+    {
       const int npair = (K + 1) / 2;  // granule / element pairs: one 16-B (8-B external) load per pair
       const bool gw = o_norm && o_norm_w;
       float sq[PJ];  // per-slot squares, summed in slot order once the pass is complete (arrival order varies)
@@ -743,9 +551,9 @@ __global__ __launch_bounds__(kEngMaxThreads, 1) void woq_engine_kernel(const Eng
       for (int sh = 32; sh > 0; sh >>= 1) s2 += __shfl_xor(s2, sh, 64);
       if (lane == 0) nsum_op[cw] = s2;
     }
-    // fp16: every consumer staged a share of the whole vector, so all meet before the stream.  (Staging only the
-    // consumer's own tiles with no barrier measured 2-3 % slower per whole-token launch; X8 does that.)
-    if constexpr (!X8) cbar(bar_a, bar_epoch, ctl, lane, failed);
+    // every consumer staged a share of the whole vector, so all meet before the stream.  (Staging only the consumer's
+    // own tiles with no barrier measured 2-3 % slower per whole-token launch.)
+    cbar(bar_a, bar_epoch, ctl, lane, failed);
     if ((thin & 1) && cw == 0 && lane == 0) lds_st(ctl_a + kPhase * 4, 0u);
     if (cw == 0) ETRACE(2, op, wall_clock64());
 
@@ -757,148 +565,6 @@ __global__ __launch_bounds__(kEngMaxThreads, 1) void woq_engine_kernel(const Eng
     unsigned long long tr_fw = 0;
 #endif
     const int gsh = st == kScaleF32 ? 0 : (m & 1) * 16;  // this lane's scale bits within the dword read
-    if constexpr (X8) {
-      // X8 per tile: NU = KT / 64 MFMAs of 64 k; a segment (one group, at most one 128-k block) is UPS of them
-      constexpr int NU = KT / 64, SEG = (BITS == 4 ? GPT == 2 : GPT == 4) ? 64 : 128, UPS = SEG / 64, NSEG = NU / UPS;
-      constexpr int NBLK = KT / 128;
-      static_assert(GPT == 1 || GPT == NSEG, "segments are the groups of a tile when a tile holds several");
-      const uint32_t a8_lane = lds_addr(act) + uint32_t(min(m & 3, kX8Rows - 1) * 64 + kq * 16);
-      const uint32_t z8_lane = lds_addr(zrows) + uint32_t(min(m & 3, kX8Rows - 1) * 64 + kq * 16);
-      const uint32_t sblk_a = lds_addr(act) + uint32_t(3 * Kp);
-      const uint32_t bsym = BITS == 4 ? 0xF8F8F8F8u : 0xFEFEFEFEu;  // splat(-bias)
-      for (int jl = 0; jl < nv; jl++) {
-        float accf = 0.f;
-        for (int c = 0; c < nch; c++) {
-          const int t0 = c * FT;
-          int g0, ngc;
-          fill_groups<GPT>(o, t0, g0, ngc);
-          const uint32_t sb = ring_a + slot * slot_bytes;
-          int tt[TPC];
-          uint32_t sca[TPC][GPT], zpa[TPC][GPT];
-          bool valid[TPC];
-#pragma unroll
-          for (int h = 0; h < TPC; h++) {
-            const int p = cw + h * NC, t = t0 + p;
-            valid[h] = t < nt;
-            tt[h] = min(t, nt - 1);
-#pragma unroll
-            for (int g = 0; g < GPT; g++) {
-              const int gi = GPT == 1 ? (tt[h] >> o.tpg_shift) - g0 : p * GPT + g;
-              sca[h][g] = sb + FT * 1024 + ((gi * 16 + m) * ssz & ~3);
-              zpa[h][g] = sb + FT * 1024 + SD * 1024 + ((gi * 16 + m) & ~3);
-            }
-          }
-          u4_t bq[TPC];
-          i4v_t ax[TPC][NU];
-          uint32_t scw[TPC][GPT], zpw[TPC][GPT], sbw[TPC][NBLK];
-          unsigned full;
-#ifdef NAD_CHAIN_TRACE
-          const unsigned long long tf0 = wall_clock64();
-#endif
-          auto rd_ops = [&](int skip_first_tile) {
-#pragma unroll
-            for (int h = 0; h < TPC; h++) {
-              const uint32_t tb = sb + (cw + h * NC) * 1024 + lane * 16;
-              if (h > 0 || !skip_first_tile) asm volatile("ds_read_b128 %0, %1" : "=v"(bq[h]) : "v"(tb) : "memory");
-              // a ragged last fill's missing tile reads zero rows (tile nt - 1 belongs to another consumer)
-              const uint32_t ab = valid[h] ? a8_lane + uint32_t(tt[h] * 3 * KT) : z8_lane;
-#pragma unroll
-              for (int u = 0; u < NU; u++) asm volatile("ds_read_b128 %0, %1" : "=v"(ax[h][u]) : "v"(ab + u * 192) : "memory");
-#pragma unroll
-              for (int b = 0; b < NBLK; b++)
-                asm volatile("ds_read_b32 %0, %1" : "=v"(sbw[h][b]) : "v"(sblk_a + uint32_t((tt[h] * NBLK + b) * 4)) : "memory");
-#pragma unroll
-              for (int g = 0; g < GPT; g++) {
-                asm volatile("ds_read_b32 %0, %1" : "=v"(scw[h][g]) : "v"(sca[h][g]) : "memory");
-                if constexpr (ASYM) asm volatile("ds_read_b32 %0, %1" : "=v"(zpw[h][g]) : "v"(zpa[h][g]) : "memory");
-              }
-            }
-          };
-          // the FULL word and the first tile in ONE asm statement: as two, hipcc put an lgkmcnt(0) between them
-          asm volatile("ds_read_b32 %0, %2\n\tds_read_b128 %1, %3"
-                       : "=&v"(full), "=&v"(bq[0])
-                       : "v"(full_a + slot * 4), "v"(sb + cw * 1024 + lane * 16)
-                       : "memory");
-          rd_ops(1);
-          asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(full) : : "memory");
-          if (__builtin_amdgcn_readfirstlane(full) < unsigned(f + 1) && !failed) {
-            for (unsigned spins = 0;; spins++) {
-              __builtin_amdgcn_s_sleep(1);
-              if (lds_ld(full_a + slot * 4) >= unsigned(f + 1) || failed) break;
-              if (spins > kSpinMax) {
-                if (lane == 0) give_up(ctl, 1);
-                failed = true;
-              }
-            }
-            rd_ops(0);
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-          }
-#pragma unroll
-          for (int h = 0; h < TPC; h++) {
-            asm volatile("" : "+v"(bq[h]));
-#pragma unroll
-            for (int u = 0; u < NU; u++) asm volatile("" : "+v"(ax[h][u]));
-#pragma unroll
-            for (int b = 0; b < NBLK; b++) asm volatile("" : "+v"(sbw[h][b]));
-#pragma unroll
-            for (int g = 0; g < GPT; g++) {
-              asm volatile("" : "+v"(scw[h][g]));
-              if constexpr (ASYM) asm volatile("" : "+v"(zpw[h][g]));
-            }
-          }
-          if (lane == 0) lds_add(free_a + slot * 4, 1u);  // operands in registers: the slot may be refilled
-#ifdef NAD_CHAIN_TRACE
-          tr_fw += wall_clock64() - tf0;
-          if (cw == 0 && jl == 0 && c == 0) ETRACE(3, op, wall_clock64());
-#endif
-          float scf[TPC][GPT];
-          i4v_t bb[TPC][GPT];
-#pragma unroll
-          for (int h = 0; h < TPC; h++)
-#pragma unroll
-            for (int g = 0; g < GPT; g++) {
-              const uint32_t x = scw[h][g];
-              const uint32_t hb = (x >> gsh) & 0xFFFFu;
-              const float fb = __uint_as_float(hb << 16), fh = f16_bits_to_f32(uint16_t(hb));
-              const float sv = st == kScaleF32 ? __uint_as_float(x) : (st == kScaleBF16 ? fb : fh);
-              scf[h][g] = valid[h] ? sv : 0.f;  // a ragged last fill: the missing tile contributes nothing
-              uint32_t bz = bsym;
-              if constexpr (ASYM) {
-                const int z = int(int8_t((zpw[h][g] >> ((m & 3) * 8)) & 0xFFu));
-                bz = __builtin_amdgcn_perm(0u, uint32_t(-(BIAS + z)), 0x00000000u);  // splat(-(bias + zp)) bytes
-              }
-              bb[h][g] = i4v_t{int(bz), int(bz), int(bz), int(bz)};
-            }
-#pragma unroll
-          for (int sg = 0; sg < NSEG; sg++) {
-            const int g = GPT == 1 ? 0 : sg;
-            i4v_t ai[TPC];
-#pragma unroll
-            for (int h = 0; h < TPC; h++) ai[h] = i4v_t{0, 0, 0, 0};
-#pragma unroll
-            for (int uu = 0; uu < UPS; uu++) {
-              const int u = sg * UPS + uu;
-#pragma unroll
-              for (int h = 0; h < TPC; h++) {
-                ai[h] = __builtin_amdgcn_mfma_i32_16x16x64_i8(ax[h][u], x8_bytes<BITS>(bq[h], u), ai[h], 0, 0, 0);
-                ai[h] = __builtin_amdgcn_mfma_i32_16x16x64_i8(ax[h][u], bb[h][g], ai[h], 0, 0, 0);
-              }
-            }
-#pragma unroll
-            for (int h = 0; h < TPC; h++) {
-              // rows 0..2 of column m (lanes 0..15): the limb dot products, exact; they meet once per segment
-              const float fsum = __builtin_fmaf(float(ai[h][0]), 16384.f, __builtin_fmaf(float(ai[h][1]), 128.f, float(ai[h][2])));
-              // (a missing tile's block scale belongs to another consumer's stale rows: select, do not multiply)
-              const float sc = valid[h] ? scf[h][g] * __uint_as_float(sbw[h][(sg * UPS) / 2]) : 0.f;
-              accf = __builtin_fmaf(fsum, sc, accf);
-            }
-          }
-          f++;
-          slot = slot + 1 == S ? 0 : slot + 1;
-        }
-        if (lane < 16) part[(jl * NC + cw) * 16 + lane] = accf;
-      }
-    } else
     for (int jl = 0; jl < nv; jl++) {
       f4_t acc = {0.f, 0.f, 0.f, 0.f};
       for (int c = 0; c < nch; c++) {
@@ -924,13 +590,8 @@ __global__ __launch_bounds__(kEngMaxThreads, 1) void woq_engine_kernel(const Eng
             zpa[h][g] = sb + FT * 1024 + SD * 1024 + ((gi * 16 + m) & ~3);
           }
         }
-#if defined(NAD_EXP_NOOPS) || defined(NAD_EXP_NOACT)
-        u4_t bq[TPC] = {};
-        h8_t af[TPC][SPT] = {};
-#else
         u4_t bq[TPC];
         h8_t af[TPC][SPT];
-#endif
         uint32_t scw[TPC][GPT], zpw[TPC][GPT];
         unsigned full;
 #ifdef NAD_CHAIN_TRACE
@@ -943,14 +604,9 @@ __global__ __launch_bounds__(kEngMaxThreads, 1) void woq_engine_kernel(const Eng
 #pragma unroll
           for (int h = 0; h < TPC; h++) {
             const uint32_t tb = sb + (cw + h * NC) * 1024 + lane * 16;
-#ifdef NAD_EXP_NOOPS  // timing experiment: no operand reads at all (wrong results)
-            continue;
-#endif
             asm volatile("ds_read_b128 %0, %1" : "=v"(bq[h]) : "v"(tb) : "memory");
-#ifndef NAD_EXP_NOACT  // timing experiment: no activation reads (wrong results)
 #pragma unroll
             for (int d = 0; d < SPT; d++) asm volatile("ds_read_b128 %0, %1" : "=v"(af[h][d]) : "v"(ab[h] + d * 128) : "memory");
-#endif
 #pragma unroll
             for (int g = 0; g < GPT; g++) {
               asm volatile("ds_read_b32 %0, %1" : "=v"(scw[h][g]) : "v"(sca[h][g]) : "memory");
@@ -1110,11 +766,17 @@ __global__ __launch_bounds__(kEngMaxThreads, 1) void woq_engine_kernel(const Eng
     else
       op_body(IC<B0>(), IC<G0>(), op);
   }
-  // the launch generation moves on once this workgroup is done: every workgroup read it before publishing anything,
-  // and workgroup 0 got here only after gathering results of every workgroup (bump is set only when an op reads a
-  // result of this launch)
-  if (bump && blockIdx.x == 0 && cw == 0 && lane == 0)
-    __hip_atomic_fetch_add(ctl, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // the launch generation moves on once EVERY workgroup is past its last granule read (bump is set only when an op
+  // reads a result of this launch): the consumers of a workgroup meet, one lane arrives on a monotonic counter
+  // (ctl[2]), and the last arrival of this launch bumps the generation -- a workgroup that owns no stripes, or is
+  // scheduled late, can never read the next generation at its start
+  if (bump) {
+    cbar(bar_a, bar_epoch, ctl, lane, failed);
+    if (cw == 0 && lane == 0) {
+      const unsigned old = __hip_atomic_fetch_add(ctl + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (old == gridDim.x * (gen + 1u) - 1u) __hip_atomic_fetch_add(ctl, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
 }
 
 }  // namespace eng
@@ -1123,7 +785,7 @@ __global__ __launch_bounds__(kEngMaxThreads, 1) void woq_engine_kernel(const Eng
 bool engine_geometry(EngGeometry& g, int kp) {
   g.kp = (kp + 15) / 16 * 16;
   g.slot_bytes = size_t(kEngFillTiles) * 1024 + size_t(g.sd) * 1024 + (g.asym ? 1024 : 0);
-  const size_t act = g.x8 ? size_t(eng::x8_act_bytes(g.kp)) : size_t(g.kp) * 4;
+  const size_t act = size_t(g.kp) * 4;
   const size_t fixed = size_t(eng::kCtlBytes) + eng::kPartBytes + act + kEngZeroBytes;
   const size_t budget = 160 * 1024;
   if (fixed >= budget) return false;
@@ -1137,10 +799,10 @@ bool engine_geometry(EngGeometry& g, int kp) {
   return true;
 }
 
-template <int B0, int G0, int B1, int G1, bool ASYM, int SD, bool X8>
+template <int B0, int G0, int B1, int G1, bool ASYM, int SD>
 static hipError_t engine_launch5(const EngOp* ops, int n_ops, const EngGeometry& g, unsigned* ctl, int grid, int bump,
                                  hipStream_t st) {
-  auto k = eng::woq_engine_kernel<B0, G0, B1, G1, ASYM, SD, X8>;
+  auto k = eng::woq_engine_kernel<B0, G0, B1, G1, ASYM, SD>;
   static bool attr = false;
   if (!attr) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1157,16 +819,12 @@ template <int B0, int G0, int B1, int G1>
 static hipError_t engine_launch4(const EngOp* ops, int n_ops, const EngGeometry& g, unsigned* ctl, int grid, int bump,
                                  hipStream_t st) {
   if (g.sd != 1 && g.sd != 2) return hipErrorInvalidValue;
-#define NAD_ENG_L(A, D, X) \
-  if (g.asym == A && g.sd == D && g.x8 == X) return engine_launch5<B0, G0, B1, G1, A, D, X>(ops, n_ops, g, ctl, grid, bump, st);
-  NAD_ENG_L(false, 1, false)
-  NAD_ENG_L(false, 2, false)
-  NAD_ENG_L(true, 1, false)
-  NAD_ENG_L(true, 2, false)
-  NAD_ENG_L(false, 1, true)
-  NAD_ENG_L(false, 2, true)
-  NAD_ENG_L(true, 1, true)
-  NAD_ENG_L(true, 2, true)
+#define NAD_ENG_L(A, D) \
+  if (g.asym == A && g.sd == D) return engine_launch5<B0, G0, B1, G1, A, D>(ops, n_ops, g, ctl, grid, bump, st);
+  NAD_ENG_L(false, 1)
+  NAD_ENG_L(false, 2)
+  NAD_ENG_L(true, 1)
+  NAD_ENG_L(true, 2)
 #undef NAD_ENG_L
   return hipErrorInvalidValue;
 }

@@ -577,7 +577,7 @@ static bool lean_ok(const GemvArgs& a, int bits, int waves) {
   return a.lean && a.M == 1 && inst && a.a_fast && nsl <= waves * lean_spw(a);
 }
 
-template <int BITS, int GPT, int AT, bool ASYM, int KSN, int SPW, bool VD = false>
+template <int BITS, int GPT, int AT, bool ASYM, int KSN, int SPW>
 __global__ __launch_bounds__((m1_max_threads<GPT, KSN>())) void woq_gemv_m1_kernel(GemvArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int KT = BITS == 4 ? 128 : 256, SPT = KT / 32, SPG = SPT / GPT;
@@ -656,9 +656,8 @@ __global__ __launch_bounds__((m1_max_threads<GPT, KSN>())) void woq_gemv_m1_kern
 
   // 3) the stream: MFMA row 0 = hi (lane m 0), row 8 = lo (lane m 8), every other row reads the zero row
   const int m = lane & 15, kq = lane >> 4;
-  const bool isrow = VD || m == 0 || (HL && m == 8);
-  // VD: every lane reads its k-quarter's hi row (and lo row RB further) for its own dot products
-  const char* abase = wrow + (isrow ? (VD || m == 0 ? RB : 2 * RB) : 0) + kq * 16;
+  const bool isrow = m == 0 || (HL && m == 8);
+  const char* abase = wrow + (isrow ? (m == 0 ? RB : 2 * RB) : 0) + kq * 16;
   const int slice_step = isrow ? 2 * RB : 0;
   const int ssh = a.scale_t == kScaleF32 ? 0 : (lane & 1) * 16;
   Dq4 dq;
@@ -693,39 +692,19 @@ __global__ __launch_bounds__((m1_max_threads<GPT, KSN>())) void woq_gemv_m1_kern
                          : dequant_step<BITS>(S.b[i], d, zp_const(BIAS + S.zp[i][g]));
         }
         const h8_t af = *reinterpret_cast<const h8_t*>(ab + i * KT * 2 + d * 64);
-        if constexpr (VD) {
-          // VALU body: this lane's 8 weights against its 8 activations, hi then lo, v_dot2_f32_f16 (fp32 accumulate)
-          const h8_t al = *reinterpret_cast<const h8_t*>(ab + RB + i * KT * 2 + d * 64);
-          float v = d % SPG == 0 ? 0.f : accg[i][0];
-#pragma unroll
-          for (int e = 0; e < 8; e += 2) {
-            v = __builtin_amdgcn_fdot2(h2_t{bf[e], bf[e + 1]}, h2_t{af[e], af[e + 1]}, v, false);
-            if constexpr (HL) v = __builtin_amdgcn_fdot2(h2_t{bf[e], bf[e + 1]}, h2_t{al[e], al[e + 1]}, v, false);
-          }
-          accg[i][0] = v;
-        } else {
-          accg[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, bf, d % SPG == 0 ? f4_t{0.f, 0.f, 0.f, 0.f} : accg[i],
-                                                           0, 0, 0);
-        }
+        accg[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, bf, d % SPG == 0 ? f4_t{0.f, 0.f, 0.f, 0.f} : accg[i],
+                                                         0, 0, 0);
       }
       if ((d + 1) % SPG == 0) {  // group end: scale each tile's group partial into the stripe sum, in tile order
 #pragma unroll
-        for (int i = 0; i < KSN; i++) {
-          if constexpr (VD)
-            acc[0] += accg[i][0] * scale_bits_to_f32(S.sc[i][g], a.scale_t, ssh);
-          else
-            acc += accg[i] * scale_bits_to_f32(S.sc[i][g], a.scale_t, ssh);
-        }
+        for (int i = 0; i < KSN; i++) acc += accg[i] * scale_bits_to_f32(S.sc[i][g], a.scale_t, ssh);
       }
     }
     cq += NW;
     cs++;
     if (cq >= nsl) {  // this wave's last slice of stripe cj: publish its partial (row 0 + row 8 = hi + lo)
       float r = acc[0];
-      if constexpr (VD) {  // the four k-quarters of column m: lanes m, m + 16, m + 32, m + 48
-        r += __shfl_xor(r, 16, 64);
-        r += __shfl_xor(r, 32, 64);
-      } else if constexpr (HL) {
+      if constexpr (HL) {
         r += __shfl_down(r, 32, 64);
       }
       if (lane < 16) part[(size_t(cj) * NW + wave) * 16 + lane] = r;
@@ -834,9 +813,9 @@ static hipError_t gemv_launch4(const GemvArgs& a, dim3 g, dim3 b, size_t lds, hi
   return hipGetLastError();
 }
 
-template <int BITS, int GPT, int AT, bool ASYM, int KSN, int SPW, bool VD>
-static hipError_t gemv_m1_launch6(const GemvArgs& a, dim3 g, dim3 b, size_t lds, hipStream_t st) {
-  auto k = woq_gemv_m1_kernel<BITS, GPT, AT, ASYM, KSN, SPW, VD>;
+template <int BITS, int GPT, int AT, bool ASYM, int KSN, int SPW>
+static hipError_t gemv_m1_launch5(const GemvArgs& a, dim3 g, dim3 b, size_t lds, hipStream_t st) {
+  auto k = woq_gemv_m1_kernel<BITS, GPT, AT, ASYM, KSN, SPW>;
   static bool attr_set = false;
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -846,12 +825,6 @@ static hipError_t gemv_m1_launch6(const GemvArgs& a, dim3 g, dim3 b, size_t lds,
   }
   hipLaunchKernelGGL(k, g, b, lds, st, a);
   return hipGetLastError();
-}
-template <int BITS, int GPT, int AT, bool ASYM, int KSN, int SPW>
-static hipError_t gemv_m1_launch5(const GemvArgs& a, dim3 g, dim3 b, size_t lds, hipStream_t st) {
-  if constexpr (AT == kActF32 && !ASYM)  // the VALU body is instantiated for the headline form only (A/B)
-    if (a.valu) return gemv_m1_launch6<BITS, GPT, AT, ASYM, KSN, SPW, true>(a, g, b, lds, st);
-  return gemv_m1_launch6<BITS, GPT, AT, ASYM, KSN, SPW, false>(a, g, b, lds, st);
 }
 template <int BITS, int GPT, int AT, bool ASYM>
 static hipError_t gemv_m1_launch4(const GemvArgs& a, dim3 g, dim3 b, size_t lds, hipStream_t st) {
@@ -976,6 +949,8 @@ int gemv_groups_per_tile(int bits, int nt, int ng, int bs, int* tpg) {
   }
   return 0;
 }
+
+bool gemv_uses_m1(const GemvArgs& a, int bits, int waves) { return lean_ok(a, bits, waves); }
 
 hipError_t launch_gemv(const GemvArgs& a, int bits, int waves, int grid, size_t lds, hipStream_t stream) {
   const int hilo = a.act_t == kActF16 ? 0 : (a.M <= 8 ? 1 : 2);

@@ -123,7 +123,6 @@ struct GemvArgs {
   int lean;             // M = 1 int4 single-group-per-tile launches may take woq_gemv_m1_kernel (NAD_GEMV_LEAN)
   int lean_ks;          // woq_gemv_m1_kernel: K tiles per K-slice (4, or 1 / 2 where that gives each of up to 16 waves one)
   int lean_spw;         // woq_gemv_m1_kernel: K-slices per wave at most (2, or 4 for long K)
-  int valu;             // woq_gemv_m1_kernel, fp32 activations: v_dot2_f32_f16 + lane reductions instead of MFMA (A/B)
   SkinnyWeight w[3];
 };
 
@@ -199,5 +198,7 @@ int gemv_waves(int bits, int nt, int ng, int bs);
 // 4 = never)
 void gemv_lean_slices(GemvArgs& a, int bits, int* waves, int ks_pref);
 hipError_t launch_gemv(const GemvArgs& a, int bits, int waves, int grid, size_t lds, hipStream_t stream);
+// whether launch_gemv would take woq_gemv_m1_kernel for these arguments
+bool gemv_uses_m1(const GemvArgs& a, int bits, int waves);
 
 }  // namespace nad

@@ -24,3 +24,27 @@ def gpu_available():
 def oracle():
     from tests.oracle_lib import Oracle
     return Oracle.get()
+
+
+@pytest.fixture
+def knob(monkeypatch):
+    """Set one NAD_* switch for this test: the library reads them once (never per call), so re-read after setting."""
+    from neural_amd import _lib
+
+    def set_(name, value):
+        if value is None:
+            monkeypatch.delenv(name, raising=False)
+        else:
+            monkeypatch.setenv(name, str(value))
+        _lib.reload_knobs()
+    return set_
+
+
+@pytest.fixture(autouse=True)
+def _knobs_follow_environment():
+    """Autouse fixtures tear down last: by then monkeypatch has restored the environment, so the library's switches go
+    back to it too."""
+    yield
+    from neural_amd import _lib
+    if _lib._LIB is not None:
+        _lib.reload_knobs()

@@ -208,3 +208,44 @@ def test_host_cache_key_is_constant_time_at_lm_head_shape():
         assert L.nad_host_blob_key(p) != keys[-1]
     assert per_call[0] < 10e-6, per_call
     assert per_call[0] < 4 * per_call[1] + 2e-6, per_call     # size-independent (ctypes call overhead included)
+
+
+def test_plan_forward_kernel_choice():
+    """nad_plan_forward (the host side of nad_device_forward with every launch recorded, no GPU): the decode shapes take
+    the M = 1 / stripe-stream GEMVs, prefill takes gemm3 (int4 g128) or gemm4 (g32 / g64 with the scale folded, int2,
+    int8), and few output tiles split K."""
+    p = bestla.plan_forward
+    assert p(4, 4096, 4096, 128, m=1)["kernel"] == "woq_gemv_m1_kernel"
+    assert p(2, 14336, 4096, 64, m=1)["kernel"] == "woq_gemv_m1_kernel"
+    assert p(4, 4096, 4096, 128, m=8)["kernel"] == "woq_gemv_kernel"
+    r = p(4, 4096, 4096, 128, m=2048)
+    assert (r["kernel"], r["fold"], r["ksplit"]) == ("woq_gemm3_kernel", False, 1)
+    assert r["launches"] == 2                       # fp32 activations: one fp16 conversion pass, then the GEMM
+    assert p(4, 4096, 4096, 128, m=2048, act="fp16")["launches"] == 1
+    for bits, g in ((4, 32), (4, 64), (2, 64)):
+        r = p(bits, 4096, 4096, g, m=2048)
+        assert (r["kernel"], r["fold"]) == ("woq_gemm4_kernel", True), (bits, g, r)
+    r = p(4, 4096, 4096, 128, m=64)
+    assert r["kernel"] == "woq_gemm3_kernel" and r["ksplit"] > 1 and r["launches"] == 3   # + the split-K reduce
+
+
+def test_host_cost_per_forward_under_3us():
+    """the per-call host work of a forward (what an NE graph pays per WOQ node on the eager path:
+    validation, kernel choice, geometry; the NAD_* switches are read once at load, not per call) stays under 3 us,
+    ctypes call overhead included.  Timed through nad_plan_forward, which runs exactly that code with the launch
+    recorded instead of issued."""
+    import time
+    L = _lib.lib()
+    o = np.zeros(6, np.int64)
+    ptr = o.ctypes.data
+    for bits, n, k, g, m in ((4, 4096, 4096, 128, 1), (4, 22016, 4096, 128, 1), (2, 4096, 14336, 64, 1),
+                             (4, 4096, 4096, 128, 2048)):
+        assert L.nad_plan_forward(bits, n, k, g, 2, 0, m, 0, ptr, 6) == 6
+        best = 1e9
+        for _ in range(5):
+            reps = 4000
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                L.nad_plan_forward(bits, n, k, g, 2, 0, m, 0, ptr, 6)
+            best = min(best, (time.perf_counter() - t0) / reps)
+        assert best < 3e-6, (bits, n, k, m, best)

@@ -9,9 +9,6 @@ Parity bars:
     split into fp16 hi + lo, fp32 accumulation) -- the same bar as the single-op decode kernels;
   * against the per-op decode kernel (woq_gemv.hip): 1e-6 (only the order of the fp32 partial sums differs);
   * RMSNorm staging against a torch fp32 reference of x / sqrt(mean(x^2) + eps) * g: 1e-5.
-The int8-limb consumer form (NAD_ENGINE_X8=1, opt-in: three int8 limbs per activation on v_mfma_i32_16x16x64_i8, exact
-integer products, fp32 once per segment) is held to the same bars: bit-identical across launch forms, 2e-5 of the
-oracle, 1e-6 of the per-op kernels.
 """
 import numpy as np
 import pytest
@@ -97,18 +94,8 @@ def _same(a, b):
     assert not bad, bad
 
 
-@pytest.fixture(params=["fp16", "x8"])
-def engine_form(request, monkeypatch):
-    """the engine's consumer arithmetic, read at nad_chain_create"""
-    if request.param == "x8":
-        monkeypatch.setenv("NAD_ENGINE_X8", "1")
-    else:
-        monkeypatch.delenv("NAD_ENGINE_X8", raising=False)
-    return request.param
-
-
 @pytest.mark.parametrize("asym", [False, True])
-def test_chain_bit_identical_to_one_op_launches_and_cut_segments(asym, engine_form):
+def test_chain_bit_identical_to_one_op_launches_and_cut_segments(asym):
     hid, ffn = 1024, 2816   # ffn: 22 K tiles -> two fills per stripe, the second ragged
     st = Stack([_layer_weights(hid, ffn, 100 * i, asym) for i in range(2)], hid, ffn, _w(1000, hid, 999, asym),
                norm_w=True)
@@ -142,7 +129,7 @@ def _per_op_kernels(st):
     return outs, logits
 
 
-def test_chain_matches_per_op_kernels(engine_form):
+def test_chain_matches_per_op_kernels():
     hid, ffn = 2048, 5632
     st = Stack([_layer_weights(hid, ffn, 7)], hid, ffn, _w(4000, hid, 77), norm_w=True)
     ops, _ = st.ops()
@@ -156,7 +143,7 @@ def test_chain_matches_per_op_kernels(engine_form):
         assert err <= 1e-6, err
 
 
-def test_chain_matches_oracle(oracle, engine_form):
+def test_chain_matches_oracle(oracle):
     """Weights packed by the oracle (the reference's blob format), each op of a launch against the oracle's fp64
     forward on that op's actual input: 2e-5."""
     hid, ffn = 1024, 2816
@@ -225,7 +212,7 @@ def test_chain_llama_shapes_graph_replay():
         assert c.status() == 0
 
 
-def test_chain_rmsnorm_staging(engine_form):
+def test_chain_rmsnorm_staging():
     hid = 2048
     w = _w(512, hid, 3)
     x = (torch.rand((1, hid), device="cuda") - 0.5) * 3
@@ -240,7 +227,7 @@ def test_chain_rmsnorm_staging(engine_form):
     assert err <= 1e-5, err
 
 
-def test_chain_int2_stack(engine_form):
+def test_chain_int2_stack():
     """int2 weights (KT = 256, two groups of 64 per... one group of 128 per tile here) through the same engine."""
     hid, ffn = 1024, 2048
     st = Stack([_layer_weights(hid, ffn, 11, bits=2, bs=128)], hid, ffn, _w(1024, hid, 12, bits=2), norm_w=True)
@@ -268,7 +255,7 @@ def test_chain_rejects_ineligible():
                            out=[torch.empty((2, 128), device="cuda")])], 2)
 
 
-def test_chain_mixed_formats_mistral_policy(engine_form):
+def test_chain_mixed_formats_mistral_policy():
     """Two weight formats in one launch (Mistral-7B's int2 policy: q, k, o, gate, up, lm_head int2 g64; wv, w2 int4 g64;
     GQA so {Q, K} is one op and V its own): bit-identical across launch forms (whole token, cut at attention, one op
     per launch), every op within 1e-6 of the per-op kernels fed the chain's own inputs, and the oracle bar on the

@@ -41,8 +41,8 @@ GEMM2_CASES = [
 @pytest.mark.parametrize("kernel", ["3", "2"])
 @pytest.mark.parametrize("cfg", GEMM2_CASES)
 @pytest.mark.parametrize("act", ["fp32", "fp16", "bf16"])
-def test_gemm_parity(oracle, monkeypatch, kernel, cfg, act):
-    monkeypatch.setenv("NAD_GEMM_KERNEL", kernel)
+def test_gemm_parity(oracle, knob, kernel, cfg, act):
+    knob("NAD_GEMM_KERNEL", kernel)
     m, n, k, bs, qt, st, asym, comp, shuf = cfg
     blob = _blob(oracle, n, k, bs, qt, st, asym, comp, seed=m + 3 * n + k, gidx=shuf)
     w = bestla.DeviceWeight(blob)
@@ -56,7 +56,7 @@ def test_gemm_parity(oracle, monkeypatch, kernel, cfg, act):
     assert _rel_err(y, ref) <= TOL[act], (_rel_err(y, ref), act)
 
 
-def test_gemm_kernels_agree(oracle, monkeypatch):
+def test_gemm_kernels_agree(oracle, knob):
     """gemm3, gemm2 and the register-staged fallback (NAD_GEMM2_DISABLE=1) on the same fp16 inputs: each within fp32
     accumulation noise of the oracle and of each other; gemm3 repeatable bit for bit."""
     m, n, k = 700, 272, 1536
@@ -67,9 +67,9 @@ def test_gemm_kernels_agree(oracle, monkeypatch):
     y3 = w.forward(x).cpu().numpy()
     for _ in range(3):
         assert np.array_equal(w.forward(x).cpu().numpy(), y3)
-    monkeypatch.setenv("NAD_GEMM_KERNEL", "2")
+    knob("NAD_GEMM_KERNEL", "2")
     y2 = w.forward(x).cpu().numpy()
-    monkeypatch.setenv("NAD_GEMM2_DISABLE", "1")
+    knob("NAD_GEMM2_DISABLE", "1")
     y1 = w.forward(x).cpu().numpy()
     for y in (y3, y2, y1):
         assert _rel_err(y, ref) <= 2e-5
@@ -175,7 +175,7 @@ FOLD_TOL = 5e-4
 
 
 @pytest.mark.parametrize("cfg", [c for c in GEMM4_CASES if c[3] == 64])
-def test_gemm4_g64_scale_fold(oracle, monkeypatch, cfg):
+def test_gemm4_g64_scale_fold(oracle, knob, cfg):
     """Groups of 64 fold the group scale into the fp16 B fragment too (int4 / int2 / int8): against the oracle and the
     exact fp32 group-end scaling (NAD_GEMM4_FOLD=0)."""
     m, n, k, bs, qt, st, asym, comp = cfg
@@ -184,7 +184,7 @@ def test_gemm4_g64_scale_fold(oracle, monkeypatch, cfg):
     x = torch.from_numpy(np.random.default_rng(m + n + 1).uniform(-0.5, 0.5, size=(m, k)).astype(np.float32)).cuda().half()
     ref = oracle.forward(x.float().cpu().numpy(), blob, n, k)
     yf = w.forward(x).cpu().numpy()
-    monkeypatch.setenv("NAD_GEMM4_FOLD", "0")
+    knob("NAD_GEMM4_FOLD", "0")
     ye = w.forward(x).cpu().numpy()
     assert _rel_err(ye, ref) <= TOL["fp16"]
     assert _rel_err(yf, ref) <= FOLD_TOL
@@ -192,7 +192,7 @@ def test_gemm4_g64_scale_fold(oracle, monkeypatch, cfg):
 
 
 @pytest.mark.parametrize("cfg", [c for c in GEMM4_CASES if c[3] == 32])
-def test_gemm4_g32_scale_fold(oracle, monkeypatch, cfg):
+def test_gemm4_g32_scale_fold(oracle, knob, cfg):
     """Groups of 32 fold the group scale into the fp16 B fragment by default (q * s rounded once to fp16; every q * s of
     these blobs is an fp16 normal, DeviceWeight::fold_ok): against the oracle at the prefill bar, and against the exact
     fp32 per-step scaling (NAD_GEMM4_FOLD=0) within the fp16 rounding of q * s (2^-11 relative per weight)."""
@@ -202,14 +202,14 @@ def test_gemm4_g32_scale_fold(oracle, monkeypatch, cfg):
     x = torch.from_numpy(np.random.default_rng(m + n).uniform(-0.5, 0.5, size=(m, k)).astype(np.float32)).cuda().half()
     ref = oracle.forward(x.float().cpu().numpy(), blob, n, k)
     yf = w.forward(x).cpu().numpy()
-    monkeypatch.setenv("NAD_GEMM4_FOLD", "0")
+    knob("NAD_GEMM4_FOLD", "0")
     ye = w.forward(x).cpu().numpy()
     assert _rel_err(yf, ref) <= FOLD_TOL
     assert _rel_err(ye, ref) <= TOL["fp16"]
     assert _rel_err(yf, ye) <= FOLD_TOL
 
 
-def test_gemm4_takes_the_fallback_configs(oracle, monkeypatch):
+def test_gemm4_takes_the_fallback_configs(oracle, knob):
     """With gemm4 disabled the same inputs run the register-staged kernel: both agree within fp32 accumulation noise
     (they see identical fp16 A and exact weights)."""
     m, n, k = 200, 256, 1024
@@ -217,7 +217,7 @@ def test_gemm4_takes_the_fallback_configs(oracle, monkeypatch):
     w = bestla.DeviceWeight(blob)
     x = (torch.rand((m, k), device="cuda") - 0.5).half()
     y4 = w.forward(x).cpu().numpy()
-    monkeypatch.setenv("NAD_GEMM4_DISABLE", "1")
+    knob("NAD_GEMM4_DISABLE", "1")
     y1 = w.forward(x).cpu().numpy()
     assert _rel_err(y4, y1.astype(np.float64)) <= 2e-5
 
@@ -234,7 +234,7 @@ SPLITK_CASES = [
 
 
 @pytest.mark.parametrize("cfg", SPLITK_CASES)
-def test_gemm_splitk_parity(oracle, monkeypatch, cfg):
+def test_gemm_splitk_parity(oracle, knob, cfg):
     """Split-K gemm3 against the oracle, and against the same GEMM without the split (fp32 sums in another order)."""
     m, n, k, bs, asym, act = cfg
     blob = _blob(oracle, n, k, bs, S4, F16, asym, 4, seed=m + n + k)
@@ -246,7 +246,7 @@ def test_gemm_splitk_parity(oracle, monkeypatch, cfg):
     ref = oracle.forward(x.float().cpu().numpy(), blob, n, k)
     y = w.forward(x).cpu().numpy()
     assert _rel_err(y, ref) <= TOL[act], (_rel_err(y, ref), act)
-    monkeypatch.setenv("NAD_SPLITK_DISABLE", "1")
+    knob("NAD_SPLITK_DISABLE", "1")
     y1 = w.forward(x).cpu().numpy()
     assert _rel_err(y, y1.astype(np.float64)) <= 2e-5
 
@@ -290,7 +290,7 @@ SPLITK4_CASES = [
 
 
 @pytest.mark.parametrize("cfg", SPLITK4_CASES)
-def test_gemm4_splitk_parity(oracle, monkeypatch, cfg):
+def test_gemm4_splitk_parity(oracle, knob, cfg):
     m, n, k, bs, qt, asym, act = cfg
     blob = _blob(oracle, n, k, bs, qt, F16, asym, 4, seed=m + 3 * n + k)
     w = bestla.DeviceWeight(blob)
@@ -302,13 +302,13 @@ def test_gemm4_splitk_parity(oracle, monkeypatch, cfg):
     y = w.forward(x).cpu().numpy()
     tol = max(TOL[act], FOLD_TOL) if bs in (32, 64, 128) else TOL[act]  # g32 / g64: scale folded into the fp16 weights
     assert _rel_err(y, ref) <= tol, (_rel_err(y, ref), act)
-    monkeypatch.setenv("NAD_SPLITK_DISABLE", "1")
+    knob("NAD_SPLITK_DISABLE", "1")
     y1 = w.forward(x).cpu().numpy()
     assert _rel_err(y, y1.astype(np.float64)) <= 2e-5
 
 
 @pytest.mark.parametrize("qt,bs", [(S4, 128), (S2, 64), (S4, 32)])
-def test_ffn_prefill_fp16_intermediates(oracle, monkeypatch, qt, bs):
+def test_ffn_prefill_fp16_intermediates(oracle, knob, qt, bs):
     """The prefill FFN keeps act(x.W1) and act(x.W1)*(x.W3) in fp16 (the down GEMM reads the second one as its operand
     directly): within the fp32-path tolerance of the oracle and of the fp32-intermediate path (NAD_FFN_F32=1)."""
     m, fin, fmid, fout = 160, 1024, 1536, 1024
@@ -322,7 +322,7 @@ def test_ffn_prefill_fp16_intermediates(oracle, monkeypatch, qt, bs):
     h3 = oracle.forward(A, b3, fmid, fin).astype(np.float64)
     ref = oracle.forward((h1 / (1 + np.exp(-h1)) * h3).astype(np.float32), b2, fout, fmid)
     assert _rel_err(y, ref) <= 2 * TOL["fp32"], _rel_err(y, ref)
-    monkeypatch.setenv("NAD_FFN_F32", "1")
+    knob("NAD_FFN_F32", "1")
     y32 = bestla.ffn_forward(x, w1, w2, w3, act="silu").cpu().numpy()
     assert _rel_err(y, y32.astype(np.float64)) <= 2 * TOL["fp32"]
     assert not np.array_equal(y, y32)   # the fp16 path really ran (different rounding of the intermediates)

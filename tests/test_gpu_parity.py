@@ -287,13 +287,13 @@ GEMV_GEOM = [
 
 @pytest.mark.parametrize("cfg", GEMV_GEOM)
 @pytest.mark.parametrize("geom", [(None, None), ("1", "16"), ("3", "5"), ("7", "1"), ("64", "8")])
-def test_gemv_stream_geometry(oracle, monkeypatch, cfg, geom):
+def test_gemv_stream_geometry(oracle, knob, cfg, geom):
     """The persistent stripe-stream GEMV with forced grids / wave counts: workgroups owning many stripes, wave ranges
     crossing stripe and group boundaries, single-wave workgroups.  Same bar as the default launch."""
     grid, waves = geom
     if grid:
-        monkeypatch.setenv("NAD_GEMV_GRID", grid)
-        monkeypatch.setenv("NAD_GEMV_WAVES", waves)
+        knob("NAD_GEMV_GRID", grid)
+        knob("NAD_GEMV_WAVES", waves)
     m, n, k, bs, qt, st, asym, comp = cfg
     blob = _blob(oracle, n, k, bs, qt, st, asym, comp, seed=m + n + bs)
     w = bestla.DeviceWeight(blob)
@@ -320,60 +320,32 @@ M1_SLICES = [
 
 @pytest.mark.parametrize("cfg", M1_SLICES)
 @pytest.mark.parametrize("grid", [None, "1", "7"])
-def test_gemv_m1_two_tile_slices(oracle, monkeypatch, cfg, grid):
+def test_gemv_m1_two_tile_slices(oracle, knob, cfg, grid):
     """M = 1 with 2-tile K-slices (one per wave, up to 16 waves) against the oracle,
     and within 1e-6 of the 4-tile-slice launch (NAD_GEMV_KS=4; only the partial-sum order differs).  Forced grids make
     workgroups stream many stripes through the 3-stage ring."""
     n, k, bs, qt, st, asym, adt = cfg
     if grid:
-        monkeypatch.setenv("NAD_GEMV_GRID", grid)
+        knob("NAD_GEMV_GRID", grid)
     blob = _blob(oracle, n, k, bs, qt, st, asym, 4, seed=n + k)
     w = bestla.DeviceWeight(blob)
     A = np.random.default_rng(k).uniform(-0.5, 0.5, size=(1, k)).astype(np.float32)
     xa = torch.from_numpy(A).cuda().to(dict(f32=torch.float32, f16=torch.float16, bf16=torch.bfloat16)[adt])
     ref = oracle.forward(xa.float().cpu().numpy(), blob, n, k)
     y2 = w.forward(xa).cpu().numpy()
-    monkeypatch.setenv("NAD_GEMV_KS", "4")
+    knob("NAD_GEMV_KS", "4")
     y4 = w.forward(xa).cpu().numpy()
     assert _rel_err(y2, ref) <= TOL_DECODE
     assert _rel_err(y2, y4) <= 1e-6
 
 
-M1_VALU = [
-    # n, k, bs, qtype, stype, ks: the M = 1 kernel's VALU body (v_dot2_f32_f16 + lane reductions; fp32 activations, sym)
-    (4096, 4096, 128, S4, F16, "2"),
-    (520, 3968, 128, S4, F16, "2"),   # K tail
-    (320, 2048, 64, S4, F32, "4"),    # 2 groups per tile, 4-tile slices
-    (1024, 4096, 64, S2, F16, "2"),   # int2 g64 (Mistral): 4 groups per tile
-    (256, 14336, 64, S4, BF16, "2"),  # long K: 4 slices per wave
-]
-
-
-@pytest.mark.parametrize("cfg", M1_VALU)
-def test_gemv_m1_valu_body(oracle, monkeypatch, cfg):
-    """NAD_GEMV_VALU=1 (the decode A/B of DESIGN.md section 4): the VALU dot-product body against the oracle (2e-5) and
-    within 1e-6 of the MFMA body (only the fp32 summation order differs)."""
-    n, k, bs, qt, st, ks = cfg
-    monkeypatch.setenv("NAD_GEMV_KS", ks)
-    blob = _blob(oracle, n, k, bs, qt, st, False, 4, seed=n + k + 1)
-    w = bestla.DeviceWeight(blob)
-    A = np.random.default_rng(k + 1).uniform(-0.5, 0.5, size=(1, k)).astype(np.float32)
-    xa = torch.from_numpy(A).cuda()
-    ref = oracle.forward(A, blob, n, k)
-    ym = w.forward(xa).cpu().numpy()
-    monkeypatch.setenv("NAD_GEMV_VALU", "1")
-    yv = w.forward(xa).cpu().numpy()
-    assert _rel_err(yv, ref) <= TOL_DECODE
-    assert _rel_err(yv, ym) <= 1e-6
-
-
 @pytest.mark.parametrize("geom", [(None, None), ("2", "3"), ("5", "16")])
-def test_gemv_stream_fused(oracle, monkeypatch, geom):
+def test_gemv_stream_fused(oracle, knob, geom):
     """QKV (three weights in one stream) and the dual gate/up stream with SiLU*mul under forced geometries."""
     grid, waves = geom
     if grid:
-        monkeypatch.setenv("NAD_GEMV_GRID", grid)
-        monkeypatch.setenv("NAD_GEMV_WAVES", waves)
+        knob("NAD_GEMV_GRID", grid)
+        knob("NAD_GEMV_WAVES", waves)
     k = 1024
     blobs = [_blob(oracle, n, k, 128, S4, F16, False, 4, seed=i) for i, n in enumerate((256, 80, 80))]
     ws = [bestla.DeviceWeight(b) for b in blobs]
@@ -393,9 +365,9 @@ def test_gemv_stream_fused(oracle, monkeypatch, geom):
 
 
 @pytest.mark.parametrize("cfg", FWD[:9])
-def test_legacy_skinny_kernel(oracle, monkeypatch, cfg):
+def test_legacy_skinny_kernel(oracle, knob, cfg):
     """The per-stripe woq_skinny_kernel (used when the stream GEMV is not eligible) keeps its own parity."""
-    monkeypatch.setenv("NAD_GEMV_DISABLE", "1")
+    knob("NAD_GEMV_DISABLE", "1")
     m, n, k, bs, qt, st, asym, comp = cfg
     blob = _blob(oracle, n, k, bs, qt, st, asym, comp, seed=m * 7 + n)
     w = bestla.DeviceWeight(blob)
