@@ -251,6 +251,96 @@ def graph_time(fn, reps, torch):
     return e0.elapsed_time(e1) / reps * 1e-3
 
 
+def graph_times(fn, reps, torch):
+    """Device time of each of `reps` replays of fn() captured once in a HIP graph (HIP events on the launch stream)."""
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    out = []
+    with torch.cuda.stream(s):
+        fn(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            fn(s)
+        g.replay()
+        for _ in range(reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(s)
+            g.replay()
+            e1.record(s)
+            e1.synchronize()
+            out.append(e0.elapsed_time(e1) * 1e-3)
+    torch.cuda.synchronize()
+    del g
+    return out
+
+
+SYN_MS = [1, 2, 4, 8, 16, 64, 256, 1024, 2048, 4096]
+
+
+def synthetic_sweep(torch, copies=128, reps=5, batch=64):
+    """north_star's synthetic N x K x M GEMM throughput (bestla_benchmark.cpp:815-824 bytes,
+    bestla_ut.h:69-76 cold-cache batching): K = N = 4096 int4 g128 sym fp16 scales, fp16 activations, M in SYN_MS.
+    `copies` distinct weights (>= 1 GiB) rotated so the 256 MB Infinity Cache cannot serve them; per M one HIP graph
+    of back-to-back launches replayed `reps` times -- min and median per launch.  Bytes per section 8(d) with 2-byte
+    activations (in and out); M <= 64 is priced against HBM, larger M against the dense fp16 MFMA peak.
+    Config 2 (M = 1) is also run as BTLAGemmBatchDriver-style batches (bestla_gemm.cpp:508-624): `batch` independent
+    problems in ONE weight-stream engine launch (no hand-off between them; fp32 activations as the engine takes)."""
+    from neural_amd import bestla
+    K = N = 4096
+    g = 128
+    ws = [bestla.DeviceWeight.synthetic(4, N, K, g, "fp16", False, seed=9000 + i) for i in range(copies)]
+    wb = weight_bytes(N, K, 4, g, 2, False)
+    gen = torch.Generator(device="cpu").manual_seed(11)
+    rows = []
+    for m in SYN_MS:
+        x = (torch.rand((m, K), generator=gen) - 0.5).half().cuda()
+        y = torch.empty((m, N), dtype=torch.float32, device="cuda")
+        n = 256 if m <= 16 else (128 if m <= 256 else 32)
+
+        def fn(st, x=x, y=y, n=n):
+            for i in range(n):
+                ws[i % copies].forward(x, out=y, stream=st)
+        per = sorted(t / n for t in graph_times(fn, reps, torch))
+        t_min, t_med = per[0], per[len(per) // 2]
+        byts = wb + (m * K + m * N) * 2
+        fl = 2.0 * m * N * K
+        hbm = m <= 64
+        gbps, tfl = byts / t_med / 1e9, fl / t_med / 1e12
+        rows.append({"m": m, "us_min": round(t_min * 1e6, 3), "us_median": round(t_med * 1e6, 3),
+                     "GBps": round(gbps, 1), "TFLOPs": round(tfl, 2), "bound": "hbm" if hbm else "mfma",
+                     "frac": round(gbps / HBM_PEAK_GBPS if hbm else tfl / MFMA_F16_PEAK_TFLOPS, 4),
+                     "kernel": bestla.plan_forward(4, N, K, g, "fp16", False, m, "fp16")["kernel"]})
+        del x, y
+    # config 2 as batches of independent problems, one engine launch per batch, two batches per replay
+    sets = copies // batch
+    xs = [(torch.rand((1, K), generator=gen) - 0.5).cuda() for _ in range(batch)]
+    ys = [torch.empty((1, N), dtype=torch.float32, device="cuda") for _ in range(batch)]
+    chains = [bestla.Chain([dict(kind=bestla.CHAIN_LINEAR, w=[ws[j * batch + i]], act=xs[i], out=[ys[i]])
+                            for i in range(batch)], 1) for j in range(sets)]
+
+    def fe(st):
+        for c in chains:
+            c.run(stream=st)
+    per = sorted(t / (sets * batch) for t in graph_times(fe, reps, torch))
+    assert max(c.status() for c in chains) == 0
+    byts = wb + (K + N) * 4
+    t_med = per[len(per) // 2]
+    batched = {"problems_per_launch": batch, "launches_per_replay": sets, "us_per_problem_min": round(per[0] * 1e6, 3),
+               "us_per_problem_median": round(t_med * 1e6, 3), "GBps": round(byts / t_med / 1e9, 1),
+               "frac": round(byts / t_med / 1e9 / HBM_PEAK_GBPS, 4), "bytes_per_problem": byts,
+               "kernel": "woq_engine_kernel (independent ops: no hand-off)", "act": "fp32"}
+    single = next(r for r in rows if r["m"] == 1)
+    del chains, ws
+    torch.cuda.empty_cache()
+    return {"config": "K=N=4096 int4 g128 sym, fp16 scales, fp16 activations; 128 weight copies (1.1 GB) rotated "
+                      "(cold); graph-replayed back-to-back launches, min / median over replays",
+            "bytes_formula": "N*K/2 + N*K/128*2 + (M*K + M*N)*2 (section 8(d), 2-byte activations)",
+            "per_m": rows,
+            "config2_m1_single_launches": {k: single[k] for k in ("us_min", "us_median", "GBps", "frac", "kernel")},
+            "config2_m1_batched_engine": batched,
+            "m4096_mfma_frac": next(r for r in rows if r["m"] == 4096)["frac"]}
+
+
 def time_launches(stack, m, reps, torch):
     """Average device time of each WOQ launch shape: `reps` launches cycling through the 32 layers' distinct weights
     (cold: 3.4 GB of weights defeat the 256 MB Infinity Cache) captured in one HIP graph, timed with HIP events on the
@@ -283,7 +373,7 @@ def time_launches(stack, m, reps, torch):
     return res
 
 
-def decode_workload(cfg, torch, reps=20, prefill=True, prefill_steps=2):
+def decode_workload(cfg, torch, reps=20, prefill=True, prefill_steps=5):
     """Secondary workload (one GPU): decode token time (graph-replayed, HIP events), its algorithmic bytes and
     roofline, and optionally the 2048-token prefill throughput."""
     st = Stack(cfg, 0, 1, seed=4321)
@@ -311,13 +401,7 @@ def decode_workload(cfg, torch, reps=20, prefill=True, prefill_steps=2):
            "launches_per_token": nl if t > te else sum(c for *_, c in L1)}
     if prefill:
         pre = Runner(st, 2048, None, "cuda")
-        pre.step()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(prefill_steps):
-            pre.step()
-        torch.cuda.synchronize()
-        pdt = (time.perf_counter() - t0) / prefill_steps
+        pdt = graph_time(lambda s: pre.step(stream=s), prefill_steps, torch)
         fl = sum(f * c for _, _, f, c in st.launches(2048))
         out["prefill_tflops"] = round(fl / pdt / 1e12, 2)
         out["prefill_ms_per_2048_tokens"] = round(pdt * 1e3, 3)
@@ -426,10 +510,11 @@ def main(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--prefill-steps", type=int, default=3)
+    ap.add_argument("--prefill-steps", type=int, default=10)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the secondary BASELINE workloads")
+    ap.add_argument("--no-synthetic", action="store_true", help="skip the synthetic K=N=4096 M sweep")
     ap.add_argument("--per-op", action="store_true", help="headline from per-op launches instead of the decode chain")
     ap.add_argument("--dry-run", action="store_true", help="print the rank layout and exit (no GPU)")
     args = ap.parse_args(argv)
@@ -510,6 +595,9 @@ def main(argv=None):
     dec = Runner(stack, 1, pc, "cuda")
     dt_op = timed(dec, args.steps, args.warmup, use_graph)
     per_op_tok_s = args.steps / dt_op
+    # the eager drop-in path (what ne_graph_compute does: one host call per WOQ node, no graph)
+    dt_eager = timed(dec, args.steps, args.warmup, False)
+    eager_tok_s = args.steps / dt_eager
     if chain is not None and dt_chain >= dt_op:
         chain = None
     dt = dt_chain if chain is not None else dt_op
@@ -517,7 +605,8 @@ def main(argv=None):
 
     # ---- prefill: M = 2048 tokens
     pre = Runner(stack, 2048, pc, "cuda")
-    pdt = timed(pre, args.prefill_steps, 1, False)
+    # graph-replayed on one GPU (the TP ranks' 32 MiB all-reduces stay eager: RCCL under capture is not exercised)
+    pdt = timed(pre, args.prefill_steps, 1, use_graph and world == 1)
     del pre
     pflops = sum(f * c for _, _, f, c in stack.launches(2048)) * world  # whole-job FLOPs
     prefill_tflops = pflops * args.prefill_steps / pdt / 1e12
@@ -546,6 +635,11 @@ def main(argv=None):
             traffic = int(rec["traffic_over_algorithmic"] * bytes_per_launch)
         except Exception:
             traffic = None
+
+    # ---- north_star's synthetic GEMM sweep (one GPU only)
+    synthetic = None
+    if world == 1 and not args.no_synthetic:
+        synthetic = synthetic_sweep(torch)
 
     # ---- secondary BASELINE workloads (one GPU only)
     extra = None
@@ -590,12 +684,14 @@ def main(argv=None):
                          "avg_launch_us": round(launch_s * 1e6, 3)},
             "decode_engine_cut_tokens_per_s": None if chain_tok_s is None else round(chain_tok_s, 2),
             "decode_engine_whole_token_tokens_per_s": None if uncut_tok_s is None else round(uncut_tok_s, 2),
-            "per_op_launches": {"tokens_per_s": round(per_op_tok_s, 2),
+            "decode_eager_tokens_per_s": round(eager_tok_s, 2),
+            "per_op_launches": {"tokens_per_s": round(per_op_tok_s, 2), "eager_tokens_per_s": round(eager_tok_s, 2),
                                 "gemv_achieved_GBps": round(tot_bytes / per_op_time / 1e9, 1),
                                 "per_shape_us": {k: round(v * 1e6, 3) for k, v in per.items()}},
             "prefill_roofline": {"bound": "mfma", "achieved": round(prefill_tflops / world, 2),
                                  "peak": MFMA_F16_PEAK_TFLOPS, "unit": "TFLOP/s",
                                  "frac": round(prefill_tflops / world / MFMA_F16_PEAK_TFLOPS, 4)},
+            "synthetic": synthetic,
             "workloads": extra,
             "cpu_baseline": cpu,
         }

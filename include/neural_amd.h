@@ -185,6 +185,8 @@ int nad_device_forward(const void* act, int act_dtype, const void* devstor, floa
 #define NAD_KERNEL_GEMM 8      /* woq_gemm_kernel: register-staged prefill fallback */
 int nad_plan_forward(int bits, int n, int k, int blocksize, int scale_t, int asym, int m, int act_dtype, int64_t* out,
                      int nout);
+/* the same dry run for a loaded device weight (its format, act-order, fold range and compute mode included) */
+int nad_plan_weight(const void* devstor, int m, int act_dtype, int64_t* out, int nout);
 /* fused Q/K/V (ip_fusion_qkv.cpp:22-93): out_i = X . W_i^T, one launch; W_i share K, blocksize, bits, scale dtype */
 int nad_device_qkv_forward(const void* act, int act_dtype, const void* wq, const void* wk, const void* wv, float* oq,
                            float* ok, float* ov, int m, int k, int lda, int ldo_q, int ldo_k, int ldo_v, void* queue);

@@ -67,6 +67,7 @@ SIGNATURES = {
     "nad_weight_info2": (_i, [_p, _p, _i]),
     "nad_reload_knobs": (None, []),
     "nad_plan_forward": (_i, [_i, _i, _i, _i, _i, _i, _i, _i, _p, _i]),
+    "nad_plan_weight": (_i, [_p, _i, _i, _p, _i]),
     "nad_blob_info": (_i, [_p, _p]),
     "nad_device_forward": (_i, [_p, _i, _p, _p, _i, _i, _i, _i, _i, _i, _p, _i, _p, _i, _p]),
     "nad_device_qkv_forward": (_i, [_p, _i, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _p]),

@@ -276,6 +276,15 @@ class DeviceWeight:
 
     __call__ = forward
 
+    def plan(self, m, act="fp32"):
+        """which kernel a forward of m rows launches (nad_plan_weight: a dry run, nothing is launched)"""
+        o = np.zeros(6, np.int64)
+        at = {"fp32": 0, "fp16": 1, "bf16": 2}[act]
+        if lib().nad_plan_weight(self.desc, m, at, _ptr(o), 6) != 6:
+            raise RuntimeError(f"nad_plan_weight failed: {last_error()}")
+        return dict(kernel=KERNELS.get(int(o[0]), str(int(o[0]))), grid=int(o[1]), threads=int(o[2]),
+                    ksplit=int(o[3]), fold=bool(o[4]), launches=int(o[5]))
+
     def set_compute(self, mode):
         """Per-weight arithmetic (nad_device_set_compute): None / -1 follow the thread / process mode, COMPUTE_FP or
         COMPUTE_INT8 (integer-core blobs and GGUF Q4_0 only; other weights stay fp)."""

@@ -1155,10 +1155,29 @@ extern "C" void bestla_device_f32f32_forward(float* activation, void* weiptr, fl
     report("bestla_device_f32f32_forward");
 }
 
+static int plan_for(const DeviceWeight& w, int m, int act_dtype, int64_t* out, int nout) {
+  if (!out || nout < 0 || m <= 0) {
+    set_err("nad_plan_*: bad arguments (m=%d)", m);
+    return -1;
+  }
+  NadPlan plan;
+  t_plan = &plan;
+  const void* act = reinterpret_cast<const void*>(uintptr_t(1) << 42);  // aligned, never dereferenced on the host
+  float* y = reinterpret_cast<float*>(uintptr_t(1) << 43);
+  const int rc = nad_device_forward(act, act_dtype, &w, y, m, w.n, w.k, w.k, w.n, kEpiNone, nullptr, 0, nullptr, 0,
+                                    nullptr);
+  t_plan = nullptr;
+  if (rc) return -1;
+  const int64_t v[6] = {plan.kernel, plan.grid, plan.block, plan.ksplit, plan.fold, plan.launches};
+  const int c = nout < 6 ? nout : 6;
+  std::memcpy(out, v, sizeof(int64_t) * size_t(c));
+  return c;
+}
+
 extern "C" int nad_plan_forward(int bits, int n, int k, int blocksize, int scale_t, int asym, int m, int act_dtype,
                                 int64_t* out, int nout) {
-  if ((bits != 2 && bits != 4 && bits != 8) || n <= 0 || k <= 0 || m <= 0 || !out || nout < 0) {
-    set_err("nad_plan_forward: bad arguments (bits=%d n=%d k=%d m=%d)", bits, n, k, m);
+  if ((bits != 2 && bits != 4 && bits != 8) || n <= 0 || k <= 0) {
+    set_err("nad_plan_forward: bad arguments (bits=%d n=%d k=%d)", bits, n, k);
     return -1;
   }
   if (blocksize <= 0) blocksize = k;
@@ -1168,17 +1187,12 @@ extern "C" int nad_plan_forward(int bits, int n, int k, int blocksize, int scale
   w.f4kind = -1;
   w.fold_ok = 1;
   w.owner = nullptr;
-  NadPlan plan;
-  t_plan = &plan;
-  const void* act = reinterpret_cast<const void*>(uintptr_t(1) << 42);
-  float* y = reinterpret_cast<float*>(uintptr_t(1) << 43);
-  const int rc = nad_device_forward(act, act_dtype, &w, y, m, n, k, k, n, kEpiNone, nullptr, 0, nullptr, 0, nullptr);
-  t_plan = nullptr;
-  if (rc) return -1;
-  const int64_t v[6] = {plan.kernel, plan.grid, plan.block, plan.ksplit, plan.fold, plan.launches};
-  const int c = nout < 6 ? nout : 6;
-  std::memcpy(out, v, sizeof(int64_t) * size_t(c));
-  return c;
+  return plan_for(w, m, act_dtype, out, nout);
+}
+
+extern "C" int nad_plan_weight(const void* devstor, int m, int act_dtype, int64_t* out, int nout) {
+  const DeviceWeight* w = as_weight(devstor);
+  return w ? plan_for(*w, m, act_dtype, out, nout) : -1;
 }
 
 static bool same_kind(const DeviceWeight& a, const DeviceWeight& b) {

@@ -165,9 +165,10 @@ def test_gemm4_parity(oracle, cfg, act):
         x = x.to(torch.float16 if act == "fp16" else torch.bfloat16)
     ref = oracle.forward(x.float().cpu().numpy(), blob, n, k)
     y = w.forward(x).cpu().numpy()
-    # groups of 32 fold the scale into the fp16 weights (q * s rounded once to fp16): the north_star-side bar of a
-    # product with fp16 weights, FOLD_TOL, instead of the exact-weight bars (test_gemm4_g32_scale_fold)
-    tol = max(TOL[act], FOLD_TOL) if bs in (32, 64, 128) else TOL[act]
+    # a launch that folds the group scale into the fp16 weights (q * s rounded once to fp16; the library reports it,
+    # nad_plan_weight) is held to FOLD_TOL, the north_star-side bar of a product with fp16 weights; every other launch
+    # keeps the exact-weight bars (test_gemm4_g32_scale_fold)
+    tol = max(TOL[act], FOLD_TOL) if w.plan(m, act)["fold"] else TOL[act]
     assert _rel_err(y, ref) <= tol, (_rel_err(y, ref), act)
 
 
@@ -300,7 +301,7 @@ def test_gemm4_splitk_parity(oracle, knob, cfg):
         x = x.to(torch.float16 if act == "fp16" else torch.bfloat16)
     ref = oracle.forward(x.float().cpu().numpy(), blob, n, k)
     y = w.forward(x).cpu().numpy()
-    tol = max(TOL[act], FOLD_TOL) if bs in (32, 64, 128) else TOL[act]  # g32 / g64: scale folded into the fp16 weights
+    tol = max(TOL[act], FOLD_TOL) if w.plan(m, act)["fold"] else TOL[act]  # scale folded into the fp16 weights
     assert _rel_err(y, ref) <= tol, (_rel_err(y, ref), act)
     knob("NAD_SPLITK_DISABLE", "1")
     y1 = w.forward(x).cpu().numpy()
@@ -321,8 +322,9 @@ def test_ffn_prefill_fp16_intermediates(oracle, knob, qt, bs):
     h1 = oracle.forward(A, b1, fmid, fin).astype(np.float64)
     h3 = oracle.forward(A, b3, fmid, fin).astype(np.float64)
     ref = oracle.forward((h1 / (1 + np.exp(-h1)) * h3).astype(np.float32), b2, fout, fmid)
-    assert _rel_err(y, ref) <= 2 * TOL["fp32"], _rel_err(y, ref)
+    assert _rel_err(y, ref) <= TOL["fp32"], _rel_err(y, ref)
     knob("NAD_FFN_F32", "1")
     y32 = bestla.ffn_forward(x, w1, w2, w3, act="silu").cpu().numpy()
-    assert _rel_err(y, y32.astype(np.float64)) <= 2 * TOL["fp32"]
+    assert _rel_err(y32, ref) <= TOL["fp32"], _rel_err(y32, ref)
+    assert _rel_err(y, y32.astype(np.float64)) <= TOL["fp32"]
     assert not np.array_equal(y, y32)   # the fp16 path really ran (different rounding of the intermediates)

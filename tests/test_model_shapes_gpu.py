@@ -68,7 +68,7 @@ def _check(oracle, blob, n, k, m, act, seed):
     ref = oracle.forward(x[rows].float().cpu().numpy(), blob, n, k)
     err = _rel_err(y[rows].cpu().numpy(), ref)
     tol = TOL[("decode" if m <= 16 else "prefill", act)]
-    if m > 16 and w.blocksize in (32, 64, 128):  # gemm4 folds the group scale into the fp16 weights (test_gemm2_gpu FOLD_TOL)
+    if w.plan(m, act)["fold"]:  # the launch folds the group scale into the fp16 weights (test_gemm2_gpu FOLD_TOL)
         tol = max(tol, 5e-4)
     assert err <= tol, (n, k, m, act, err, tol)
     del w
@@ -127,7 +127,7 @@ def test_mistral_layer_policy_mix(oracle):
         t = (h1 / (1 + np.exp(-h1)) * h3).astype(np.float32)
         ref = oracle.forward(t, b2, fout, fmid)
         # the intermediate is fp32 (decode) / rounded to fp16 for the down GEMM (prefill)
-        assert _rel_err(y, ref) <= (1e-4 if m <= 16 else 2e-3), (m, _rel_err(y, ref))
+        assert _rel_err(y, ref) <= (1e-4 if m <= 16 else 1e-3), (m, _rel_err(y, ref))
 
 
 LLAMA_ASYM = [
@@ -189,3 +189,50 @@ def test_llama_sym_headline_single_launches(oracle, shape):
     name, n, k = shape
     blob = _llama_sym(oracle, n, k, seed=920 + n + k)
     _check(oracle, blob, n, k, 1, "fp32", seed=23)
+
+
+FFN_SHAPES = [
+    # name, fin, fmid, group, gate/up bits, down bits (Llama-2-7B int4 g128; Mistral-7B's int2 policy: w2 int4)
+    ("llama2_7b", 4096, 11008, 128, 4, 4),
+    ("mistral_7b_int2_policy", 4096, 14336, 64, 2, 4),
+]
+
+
+@pytest.mark.parametrize("shape", FFN_SHAPES, ids=[s[0] for s in FFN_SHAPES])
+def test_ffn_prefill_error_at_model_shapes(oracle, shape):
+    """the fused FFN at prefill (M = 64 > 16: the pipelined GEMMs, fp32 activations) at the model
+    shapes, both forms -- nad_device_ffn_forward (fp16 intermediates) and the reference-named host entry
+    bestla_fusion_FFN_SiLu_f32f32_forward (fp32 intermediates returned in tmp1 / tmp2) -- against the oracle chain on the
+    exact fp32 input: held to north_star's 1e-3, and the error reached is recorded (gpurun_out/ffn_prefill_err.txt)."""
+    import ctypes as C
+    import os
+    from neural_amd import _lib
+    name, fin, fmid, g, gb, db = shape
+    m = 64
+    b1 = _qblob(oracle, fmid, fin, g, gb, False, seed=41)
+    b3 = _qblob(oracle, fmid, fin, g, gb, False, seed=43)
+    b2 = _qblob(oracle, fin, fmid, g, db, False, seed=42)
+    A = np.random.default_rng(5).uniform(-1, 1, size=(m, fin)).astype(np.float32)
+    h1 = oracle.forward(A, b1, fmid, fin).astype(np.float64)
+    h3 = oracle.forward(A, b3, fmid, fin).astype(np.float64)
+    t = h1 / (1 + np.exp(-h1)) * h3
+    ref = oracle.forward(t.astype(np.float32), b2, fin, fmid)
+    w1, w2, w3 = (bestla.DeviceWeight(b) for b in (b1, b2, b3))
+    y_dev = bestla.ffn_forward(torch.from_numpy(A).cuda(), w1, w2, w3, act="silu").cpu().numpy()
+    del w1, w2, w3
+    L = _lib.lib()
+    vp = lambda a: a.ctypes.data_as(C.c_void_p)  # noqa: E731
+    tmp1 = np.zeros((m, fmid), np.float32)
+    tmp2 = np.zeros((m, fmid), np.float32)
+    y_host = np.zeros((m, fin), np.float32)
+    L.nad_clear_error()
+    L.bestla_fusion_FFN_SiLu_f32f32_forward(vp(A), vp(b1), vp(b2), vp(b3), vp(tmp1), vp(tmp2), vp(y_host), m, fin, fmid,
+                                            fin, None)
+    assert _lib.last_error() == ""
+    L.nad_host_cache_clear()
+    errs = {"device_fp16_intermediates": _rel_err(y_dev, ref), "host_entry": _rel_err(y_host, ref),
+            "host_entry_tmp2": _rel_err(tmp2, t)}
+    if os.path.isdir("gpurun_out"):
+        with open("gpurun_out/ffn_prefill_err.txt", "a") as f:
+            f.write(f"{name} M={m}: " + ", ".join(f"{k} {v:.3e}" for k, v in errs.items()) + "\n")
+    assert max(errs.values()) <= 1e-3, errs

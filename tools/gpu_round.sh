@@ -6,7 +6,7 @@ mkdir -p gpurun_out
 TAG=${TAG:-r01}
 ok() { local rc=$1; [ "$rc" -eq 0 ] || [ "$rc" -eq 1 ]; }
 echo "== pytest -m gpu"; date
-timeout -k 10 900 python -m pytest tests -m gpu -q -x --timeout 600 > gpurun_out/pytest_gpu_$TAG.log 2>&1; rc=$?
+timeout -k 10 900 python -u -m pytest tests -m gpu -q -x --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu_$TAG.log 2>&1; rc=$?
 tail -25 gpurun_out/pytest_gpu_$TAG.log; echo "pytest rc=$rc"; ok $rc || exit $rc
 if [ "${SKIP_SMOKE:-0}" = 0 ]; then
   echo "== smoke"; timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1; rc=$?
