@@ -56,7 +56,7 @@ struct Knobs {
   int gemv_wpc, gemv_grid, gemv_waves, gemv_pre, gemv_lean, gemv_ks, gemv_spw, gemv_disable;
   int compute_int8;
   int gemm2_disable, gemm4_all, gemm4_disable, ffn_f32, gemm_kernel, splitk_disable;
-  int gemm3_prio, gemm3_stagger, gemm4_stagger2, gemm_fold, gemm4_fold_all, gemm4_fold;
+  int gemm3_prio, gemm3_stagger, gemm4_stagger2, gemm_fold, gemm4_fold_all, gemm4_fold, gemm5, gemm4_ksw;
   int engine_thin, engine_start_sync, engine_loaders, engine_depth, engine_slots;
   int host_cache_mb, tile_kmajor;
 };
@@ -83,6 +83,8 @@ static Knobs read_knobs() {
   k.gemm_fold = env_int("NAD_GEMM_FOLD", 0);
   k.gemm4_fold_all = env_int("NAD_GEMM4_FOLD_ALL", 0);
   k.gemm4_fold = env_int("NAD_GEMM4_FOLD", 1);
+  k.gemm5 = env_int("NAD_GEMM5", 0);
+  k.gemm4_ksw = env_int("NAD_GEMM4_KSW", 0);  // folded gemm4 launches with the waves split over K  // int4 g128 * 2^j prefill on gemm5 (waves split over K, scale folded)
   k.engine_thin = env_int("NAD_ENGINE_THIN", 0);
   k.engine_start_sync = env_int("NAD_ENGINE_START_SYNC", 0);
   k.engine_loaders = env_int("NAD_ENGINE_LOADERS", 2);
@@ -1060,6 +1062,7 @@ static int run_gemm(const void* act, int act_t, int lda, int m, int k, const Dev
   // with it; NAD_GEMM4_FOLD=0 restores the exact fp32 per-group path (gemm4 scale folding)
   if (pg == 4 && (w.blocksize == 32 || w.blocksize == 64 || kn.gemm4_fold_all))
     a.fold = w.fold_ok && kn.gemm4_fold ? 1 : 0;
+  if (pg == 4 && a.fold && kn.gemm4_ksw) a.ksw = 1;
   if (h16) {
     if (!pg) {
       set_err("fp16 GEMM output needs the pipelined GEMM");
@@ -1076,6 +1079,9 @@ static int run_gemm(const void* act, int act_t, int lda, int m, int k, const Dev
       pre = &own;
     }
     const bool g2 = pg == 3 && kn.gemm_kernel == 2;
+    // gemm5 (waves split over K: each B fragment dequantized once per workgroup) needs the fold
+    const bool g5 = pg == 3 && !g2 && kn.gemm5 && w.fold_ok;
+    if (g5) a.fold = 1;
     int ktiles = w.nt;
     const int ks = !g2 ? splitk_plan(w, m, &ktiles) : 1;
     if (ks > 1) {  // partials after the fp16 activations in the same workspace (stream-ordered reuse)
@@ -1088,12 +1094,14 @@ static int run_gemm(const void* act, int act_t, int lda, int m, int k, const Dev
       a.part = reinterpret_cast<float*>(base + a16);
     }
     const int tiles = ((m + 255) / 256) * ((w.n + 127) / 128);
-    if (planned(pg == 4 ? NAD_KERNEL_GEMM4 : (g2 ? NAD_KERNEL_GEMM2 : NAD_KERNEL_GEMM3), tiles * ks, 512, ks, a.fold)) {
+    if (planned(pg == 4 ? NAD_KERNEL_GEMM4 : (g2 ? NAD_KERNEL_GEMM2 : (g5 ? NAD_KERNEL_GEMM5 : NAD_KERNEL_GEMM3)),
+                tiles * ks, 512, ks, a.fold)) {
       if (ks > 1) planned(0, 0, 0, 1, 0, false);  // the split-K reduce
       return 0;
     }
     hipError_t e = pg == 4 ? launch_gemm4(a, w.bits, pre->p, pre->ld, st)
                    : g2    ? launch_gemm2(a, pre->p, pre->ld, st)
+                   : g5    ? launch_gemm5(a, pre->p, pre->ld, st)
                            : launch_gemm3(a, pre->p, pre->ld, st);
     if (e == hipSuccess && ks > 1) e = launch_splitk_reduce(a, st);
     if (e != hipSuccess) {

@@ -176,6 +176,10 @@ template <size_t... I>
 __device__ __forceinline__ void lds_frags(h8_t (&f)[8], uint32_t addr, std::index_sequence<I...>) {
   ((f[I] = lds_b128<int(I) * 16 * ROWB>(addr)), ...);
 }
+template <size_t... I>
+__device__ __forceinline__ void lds_frags16(h8_t (&f)[16], uint32_t addr, std::index_sequence<I...>) {
+  ((f[I] = lds_b128<int(I) * 16 * ROWB>(addr)), ...);
+}
 template <class T>
 __device__ __forceinline__ void tie(T& r) {
   asm volatile("" : "+v"(r));
@@ -189,9 +193,14 @@ __device__ __forceinline__ uint32_t lds_addr(const char* p) {
   return uint32_t(reinterpret_cast<uintptr_t>((const __attribute__((address_space(3))) char*)p));
 }
 
-template <int BITS, bool G32, bool ASYM, bool FOLD = false>
+// KSW (folded launches only): the waves split over K instead of M -- 1 (M) x 4 (N) x 2 (K), wave (wn, wk) owns a
+// 256 x 32 partial over the 32-deep step wk of every half step -- so each B fragment is dequantized (and scaled) once
+// per workgroup instead of by both M-waves (gemm5 in woq_gemm2.hip is the same change for gemm3); the two K-halves meet
+// in the epilogue
+template <int BITS, bool G32, bool ASYM, bool FOLD = false, bool KSW = false>
 __global__ __launch_bounds__(512, 1) void woq_gemm4_kernel(GemmArgs a, const _Float16* __restrict__ A16, int lda16,
                                                            int gh_log2) {
+  static_assert(!KSW || FOLD, "the K-split wave layout keeps no per-group partials: folded launches only");
   constexpr int HPT = hpt<BITS>();
   constexpr int GS = gslots<BITS, G32>();
   constexpr int BSC = GS * 512;
@@ -207,6 +216,7 @@ __global__ __launch_bounds__(512, 1) void woq_gemm4_kernel(GemmArgs a, const _Fl
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));
   const int wm = wave >> 2, wn = wave & 3;
+  const int wk = wave >> 2;  // KSW: this wave's 32-deep step of every half step
   const SkinnyWeight& W = a.w;
   const int M = a.M, nt = W.nt, ng = W.ng, ns = W.ns;
   const int gh = 1 << gh_log2;
@@ -284,14 +294,16 @@ __global__ __launch_bounds__(512, 1) void woq_gemm4_kernel(GemmArgs a, const _Fl
     if constexpr (!B2 && P == 0) issue_tile(ua / HPT);
   };
 
-  f4_t acc[8][2], accg[8][2];
+  constexpr int RB = KSW ? 16 : 8;  // 16-row blocks per wave
+  f4_t acc[RB][2], accg[8][2];
+#pragma unroll
+  for (int i = 0; i < RB; i++)
+#pragma unroll
+    for (int j = 0; j < 2; j++) acc[i][j] = f4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int i = 0; i < 8; i++)
 #pragma unroll
-    for (int j = 0; j < 2; j++) {
-      acc[i][j] = f4_t{0.f, 0.f, 0.f, 0.f};
-      accg[i][j] = f4_t{0.f, 0.f, 0.f, 0.f};
-    }
+    for (int j = 0; j < 2; j++) accg[i][j] = f4_t{0.f, 0.f, 0.f, 0.f};
 
   // prologue: batches -3, -2, -1 (A0 + tile 0, A1, A2; the tile of half 2 goes with A2 when HPT == 2)
   issue(std::integral_constant<int, 0>{}, -3);
@@ -322,6 +334,8 @@ __global__ __launch_bounds__(512, 1) void woq_gemm4_kernel(GemmArgs a, const _Fl
   uint32_t roff[2];
 #pragma unroll
   for (int dd = 0; dd < 2; dd++) roff[dd] = uint32_t((wm * 128 + nl) * ROWB + (((dd * 4 + kq) ^ ((nl >> 1) & 7)) * 16));
+  // KSW: rows 0..255 (f(row) = (nl >> 1) & 7 for every 16-row block), chunk of step wk
+  const uint32_t roffk = uint32_t(nl * ROWB + (((wk * 4 + kq) ^ ((nl >> 1) & 7)) * 16));
   const int boff = (wn * 2) * 1024 + lane * 16;
   const int soff = BTILES + ((wn * 2) * 16 + nl) * 4;
   const int zoff = BTILES + BSC + (wn * 2) * 16 + (nl & ~3);
@@ -378,6 +392,64 @@ __global__ __launch_bounds__(512, 1) void woq_gemm4_kernel(GemmArgs a, const _Fl
     const char* bb = smem + NA * HBUF + (t % NBR) * BBUF;
     issue(std::integral_constant<int, (H + 3) % HPT>{}, u);
     const uint32_t al = lds_addr(ab), bl = lds_addr(bb);
+    if constexpr (KSW) {
+      // this wave's step wk: one B dword per stripe (int8: two), its group's scale (and zero point), 16 A fragments
+      const int slot = G32 ? 2 * H + wk : (gh_log2 >= 30 ? 0 : (H >> gh_log2) % GS);
+      uint32_t b0 = 0u, b1 = 0u;
+      uint2 e0 = {0u, 0u}, e1 = {0u, 0u};
+      if constexpr (BITS == 8) {
+        e0 = lds_b64<0>(bl + boff + wk * 8);
+        e1 = lds_b64<1024>(bl + boff + wk * 8);
+      } else if constexpr (BITS == 4) {
+        b0 = lds_b32<H * 8>(bl + boff + wk * 4);
+        b1 = lds_b32<1024 + H * 8>(bl + boff + wk * 4);
+      } else {
+        b0 = lds_b32<H * 4>(bl + boff);
+        b1 = lds_b32<1024 + H * 4>(bl + boff);
+      }
+      uint32_t z0 = 0u, z1 = 0u;
+      if constexpr (ASYM) {
+        const uint32_t za = bl + zoff + slot * 128;
+        z0 = lds_b32v(za);
+        z1 = lds_b32v(za + 16);
+      }
+      const uint32_t sa = bl + soff + slot * 512;
+      uint32_t s0 = lds_b32v(sa), s1 = lds_b32v(sa + 64);
+      h8_t af[16];
+      lds_frags16(af, al + roffk, std::make_index_sequence<16>{});
+      wait_lgk<8>(b0, b1, e0, e1, z0, z1, s0, s1, af[0], af[1], af[2], af[3], af[4], af[5], af[6], af[7]);
+      if constexpr (L) {
+        wait_lgk<0>(af[8], af[9], af[10], af[11], af[12], af[13], af[14], af[15]);
+        hand_over(Hc, u);
+      }
+      h8_t bf[2];
+      const uint32_t bw1[2] = {b0, b1};
+      const uint2 bw8[2] = {e0, e1};
+      const uint32_t zw1[2] = {z0, z1};
+      const uint32_t sw1[2] = {s0, s1};
+#pragma unroll
+      for (int j = 0; j < 2; j++) {
+        const float zf = ASYM ? float(int(int8_t((zw1[j] >> zsh) & 0xFFu))) : 0.f;
+        if constexpr (BITS == 8)
+          bf[j] = dq8(bw8[j].x, bw8[j].y, zc0 - splat(zf));
+        else if constexpr (BITS == 4)
+          bf[j] = dq4(bw1[j], s16, zc0 - splat(zf), zc1 - splat(zf));
+        else
+          bf[j] = dq2(bw1[j], wk * 8, zc0 - splat(zf));
+        bf[j] = bf[j] * scale_h8(sw1[j]);
+      }
+#pragma unroll
+      for (int i = 0; i < 8; i++)
+#pragma unroll
+        for (int j = 0; j < 2; j++) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
+      if constexpr (!L) wait_lgk<0>(af[8], af[9], af[10], af[11], af[12], af[13], af[14], af[15]);
+#pragma unroll
+      for (int i = 8; i < RB; i++)
+#pragma unroll
+        for (int j = 0; j < 2; j++) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
+      if constexpr (!L) hand_over(Hc, u);
+      return;
+    } else {
     // B words of this half step for the wave's two stripes: int4 two dwords (one per 32-deep step), int2 one dword
     uint32_t bw[2][2];
     u4_t b8[2];
@@ -522,6 +594,7 @@ __global__ __launch_bounds__(512, 1) void woq_gemm4_kernel(GemmArgs a, const _Fl
       }
     }
     if constexpr (!L) hand_over(Hc, u);
+    }
   };
 
   auto loop = [&](auto Lc) {
@@ -539,21 +612,42 @@ __global__ __launch_bounds__(512, 1) void woq_gemm4_kernel(GemmArgs a, const _Fl
   else
     loop(std::false_type{});
 
-  // epilogue through LDS (as gemm3)
+  // epilogue through LDS (as gemm3); KSW: the two K-halves of each 256 x 32 tile meet first (as gemm5): wave (wn, wk)
+  // finishes rows wk * 128 .. + 127, its partial of the other rows goes to its partner's region
   float* tw = reinterpret_cast<float*>(smem) + wave * (128 * 36);
+  if constexpr (KSW) {
+    __syncthreads();
+    float* const tp = reinterpret_cast<float*>(smem) + (wave ^ 4) * (128 * 36);
+    const int io = (wk ^ 1) * 8;
 #pragma unroll
-  for (int i = 0; i < 8; i++)
+    for (int i = 0; i < 8; i++)
 #pragma unroll
-    for (int j = 0; j < 2; j++)
+      for (int j = 0; j < 2; j++)
 #pragma unroll
-      for (int rr = 0; rr < 4; rr++) tw[(i * 16 + kq * 4 + rr) * 36 + j * 16 + nl] = acc[i][j][rr];
+        for (int rr = 0; rr < 4; rr++) tp[(i * 16 + kq * 4 + rr) * 36 + j * 16 + nl] = acc[(io + i) % RB][j][rr];
+    __syncthreads();
+    const int im = wk * 8;
+#pragma unroll
+    for (int i = 0; i < 8; i++)
+#pragma unroll
+      for (int j = 0; j < 2; j++)
+#pragma unroll
+        for (int rr = 0; rr < 4; rr++) tw[(i * 16 + kq * 4 + rr) * 36 + j * 16 + nl] += acc[(im + i) % RB][j][rr];
+  } else {
+#pragma unroll
+    for (int i = 0; i < 8; i++)
+#pragma unroll
+      for (int j = 0; j < 2; j++)
+#pragma unroll
+        for (int rr = 0; rr < 4; rr++) tw[(i * 16 + kq * 4 + rr) * 36 + j * 16 + nl] = acc[i][j][rr];
+  }
   const int s0 = bn * 8 + wn * 2;
   const int col0 = s0 * 16;
 #pragma unroll 4
   for (int q = 0; q < 16; q++) {
     const int c = q * 64 + lane;
     const int rl = c >> 3, c4 = c & 7;
-    const int row = m0 + wm * 128 + rl;
+    const int row = m0 + (KSW ? wk : wm) * 128 + rl;
     const int n0 = col0 + c4 * 4;
     const float4 tv = *reinterpret_cast<const float4*>(tw + rl * 36 + c4 * 4);
     if (row >= M || n0 >= W.n) continue;
@@ -602,7 +696,9 @@ hipError_t launch_gemm4(const GemmArgs& a, int bits, const _Float16* A16, int ld
     return hipGetLastError();
   };
 #define NAD_G4(B, G, A) go(g4::woq_gemm4_kernel<B, G, A>, g4::lds_bytes<B, G, A>())
-#define NAD_G4F(B, G, A) go(g4::woq_gemm4_kernel<B, G, A, true>, g4::lds_bytes<B, G, A>())
+#define NAD_G4F(B, G, A)                                                                              \
+  (a.ksw ? go(g4::woq_gemm4_kernel<B, G, A, true, true>, g4::lds_bytes<B, G, A>())                    \
+         : go(g4::woq_gemm4_kernel<B, G, A, true, false>, g4::lds_bytes<B, G, A>()))
   if (bits == 4) {
     if (g32 && a.fold) return asym ? NAD_G4F(4, true, true) : NAD_G4F(4, true, false);
     if (g32) return asym ? NAD_G4(4, true, true) : NAD_G4(4, true, false);

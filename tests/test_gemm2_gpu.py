@@ -38,11 +38,14 @@ GEMM2_CASES = [
 ]
 
 
-@pytest.mark.parametrize("kernel", ["3", "2"])
+@pytest.mark.parametrize("kernel", ["3", "2", "5"])
 @pytest.mark.parametrize("cfg", GEMM2_CASES)
 @pytest.mark.parametrize("act", ["fp32", "fp16", "bf16"])
 def test_gemm_parity(oracle, knob, kernel, cfg, act):
-    knob("NAD_GEMM_KERNEL", kernel)
+    """gemm3 / gemm2 / gemm5 (NAD_GEMM5=1: waves split over K, the group scale folded into the fp16 weights -- held to
+    FOLD_TOL when it folds, which nad_plan_weight reports)."""
+    knob("NAD_GEMM_KERNEL", "3" if kernel == "5" else kernel)
+    knob("NAD_GEMM5", "1" if kernel == "5" else "0")
     m, n, k, bs, qt, st, asym, comp, shuf = cfg
     blob = _blob(oracle, n, k, bs, qt, st, asym, comp, seed=m + 3 * n + k, gidx=shuf)
     w = bestla.DeviceWeight(blob)
@@ -52,8 +55,12 @@ def test_gemm_parity(oracle, knob, kernel, cfg, act):
     if act != "fp32":
         x = x.to(torch.float16 if act == "fp16" else torch.bfloat16)
     ref = oracle.forward(x.float().cpu().numpy(), blob, n, k)
+    plan = w.plan(m, act)
+    if kernel == "5":
+        assert plan["kernel"] == "woq_gemm5_kernel" and plan["fold"], plan
     y = w.forward(x).cpu().numpy()
-    assert _rel_err(y, ref) <= TOL[act], (_rel_err(y, ref), act)
+    tol = max(TOL[act], FOLD_TOL) if plan["fold"] else TOL[act]
+    assert _rel_err(y, ref) <= tol, (_rel_err(y, ref), act)
 
 
 def test_gemm_kernels_agree(oracle, knob):
@@ -152,10 +159,12 @@ GEMM4_CASES = [
 ]
 
 
+@pytest.mark.parametrize("ksw", ["0", "1"])
 @pytest.mark.parametrize("cfg", GEMM4_CASES)
 @pytest.mark.parametrize("act", ["fp32", "fp16", "bf16"])
-def test_gemm4_parity(oracle, cfg, act):
-    """gemm4 against the oracle, and against the register-staged fallback (NAD_GEMM4_DISABLE=1) on the same inputs."""
+def test_gemm4_parity(oracle, knob, cfg, act, ksw):
+    """gemm4 against the oracle (NAD_GEMM4_KSW=1: folded launches with the waves split over K)."""
+    knob("NAD_GEMM4_KSW", ksw)
     m, n, k, bs, qt, st, asym, comp = cfg
     blob = _blob(oracle, n, k, bs, qt, st, asym, comp, seed=m + 7 * n + k)
     w = bestla.DeviceWeight(blob)

@@ -33,8 +33,8 @@ __device__ __host__ inline int wkb_of(int wkb, int k) {
   return t[k & 3];
 }
 
-// waves 0..6 hold the weights (issued at dispatch, each wave's vmcnt queue holds only its own weight loads); wave 7
-// gathers the input (its queue holds only gather loads), so the gather's first pass is not queued behind the weights
+// every wave holds a share of the weights (issued at dispatch) and then gathers 8 granules per lane -- all 8 loads in
+// flight per pass, tags checked after the pass (a load -> check -> load loop would make 8 serial round trips per pass)
 __global__ __launch_bounds__(512, 4) void op_kernel(unsigned* ctl, unsigned long long* gran, const uint4* weights,
                                                    int wkb_arg, int k, int last, unsigned long long* st) {
   extern __shared__ unsigned lds[];
@@ -42,58 +42,49 @@ __global__ __launch_bounds__(512, 4) void op_kernel(unsigned* ctl, unsigned long
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
   const unsigned gen = __builtin_amdgcn_readfirstlane(__hip_atomic_load(ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
   const int wkb = wkb_of(wkb_arg, k);
-  unsigned long long tw = 0, tg = 0;
+  const uint4* wp = weights + (size_t(k) * kWg + blockIdx.x) * size_t(176 * 64);
+  const int nld = wkb * 64;  // 16-B loads of the workgroup
+  u4v w[22];
+#pragma unroll
+  for (int i = 0; i < 22; i++) {
+    const int idx = i * 512 + threadIdx.x;
+    if (idx < nld) w[i] = __builtin_nontemporal_load(reinterpret_cast<const u4v*>(wp + idx));
+    else w[i] = u4v{0u, 0u, 0u, 0u};
+  }
   float part = 0.f;
-  if (wave < 7) {
-    // (A) this workgroup's weights: wkb KiB over 448 lanes, 16 B per load, all in flight
-    const uint4* wp = weights + (size_t(k) * kWg + blockIdx.x) * size_t(176 * 64);
-    const int nld = wkb * 64;  // 16-B loads of the workgroup
-    u4v w[24];
-#pragma unroll
-    for (int i = 0; i < 24; i++) {
-      const int idx = i * 448 + threadIdx.x;
-      if (idx < nld) w[i] = __builtin_nontemporal_load(reinterpret_cast<const u4v*>(wp + idx));
-      else w[i] = u4v{0u, 0u, 0u, 0u};
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    tw = __builtin_amdgcn_s_memrealtime();
-#pragma unroll
-    for (int i = 0; i < 24; i++) part += __uint_as_float(w[i][0] & 0x3f7fffffu) + __uint_as_float(w[i][3] & 0x3f7fffffu);
-  } else if (k > 0) {
-    // (B) the previous op's vector: 4096 granules, 64 per lane, sc1 (L2) loads, passes of 16 until every tag matches
+  unsigned long long tg = t0;
+  if (k > 0) {
     const unsigned want = gen * 256u + unsigned(k);
     const unsigned long long* src = gran + size_t(k - 1) * kVec;
+    unsigned pend = 0xFFu;
     unsigned spins = 0;
-    for (int p0 = 0; p0 < 64; p0 += 16) {
-      unsigned pend = 0xFFFFu;
-      while (pend) {
-        unsigned long long g[16];
+    while (true) {
+      unsigned long long g[8];
 #pragma unroll
-        for (int j = 0; j < 16; j++)
-          g[j] = (pend & (1u << j)) ? __hip_atomic_load(src + (p0 + j) * 64 + lane, __ATOMIC_RELAXED,
-                                                        __HIP_MEMORY_SCOPE_AGENT)
-                                    : 0ull;
+      for (int j = 0; j < 8; j++)
+        g[j] = __hip_atomic_load(src + j * 512 + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int j = 0; j < 16; j++)
-          if ((pend & (1u << j)) && unsigned(g[j] >> 32) == want) {
-            part += __uint_as_float(unsigned(g[j]));
-            pend &= ~(1u << j);
-          }
-        if (__all(pend == 0u)) break;
-        __builtin_amdgcn_s_sleep(1);
-        if (((++spins) & 63) == 0 && (__builtin_amdgcn_s_memrealtime() - t0) > 5000000ull) {  // 50 ms
-          if (lane == 0) __hip_atomic_fetch_add(ctl + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          break;
+      for (int j = 0; j < 8; j++)
+        if ((pend & (1u << j)) && unsigned(g[j] >> 32) == want) {
+          part += __uint_as_float(unsigned(g[j]));
+          pend &= ~(1u << j);
         }
+      if (__all(pend == 0u)) break;
+      __builtin_amdgcn_s_sleep(1);
+      if (((++spins) & 63) == 0 && (__builtin_amdgcn_s_memrealtime() - t0) > 5000000ull) {  // 50 ms
+        if (lane == 0) __hip_atomic_fetch_add(ctl + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
       }
     }
-    tg = __builtin_amdgcn_s_memrealtime();
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  tg = __builtin_amdgcn_s_memrealtime();
+#pragma unroll
+  for (int i = 0; i < 22; i++) part += __uint_as_float(w[i][0] & 0x3f7fffffu) + __uint_as_float(w[i][3] & 0x3f7fffffu);
   lds[threadIdx.x] = __float_as_uint(part);
-  if (threadIdx.x == 0) lds[600] = unsigned(tw), lds[601] = unsigned(tw >> 32);
-  if (threadIdx.x == 448) lds[602] = unsigned(tg), lds[603] = unsigned(tg >> 32);
+  if (threadIdx.x == 0) lds[600] = unsigned(tg), lds[601] = unsigned(tg >> 32);
   __syncthreads();
-  // (C) 16 outputs per workgroup: a 32-way tree per output
   if (threadIdx.x < 64) {
     const int o = threadIdx.x & 15, q = threadIdx.x >> 4;
     float v = 0.f;
@@ -111,10 +102,10 @@ __global__ __launch_bounds__(512, 4) void op_kernel(unsigned* ctl, unsigned long
   if (threadIdx.x == 0) {
     unsigned long long* s = st + (size_t(k) * kWg + blockIdx.x) * 4;
     s[0] = t0;
-    s[1] = (static_cast<unsigned long long>(lds[601]) << 32) | lds[600];
-    s[2] = (static_cast<unsigned long long>(lds[603]) << 32) | lds[602];
+    s[1] = (static_cast<unsigned long long>(lds[601]) << 32) | lds[600];  // weights landed and input gathered
+    s[2] = s[1];
     s[3] = __builtin_amdgcn_s_memrealtime();
-    if (last) {  // the generation moves on after every workgroup of the last op arrived
+    if (last) {
       const unsigned old = __hip_atomic_fetch_add(ctl + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (old == gridDim.x * (gen + 1u) - 1u) __hip_atomic_fetch_add(ctl, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
@@ -234,7 +225,7 @@ int main() {
   hipEvent_t fork, join;
   CK(hipEventCreateWithFlags(&fork, hipEventDisableTiming));
   CK(hipEventCreateWithFlags(&join, hipEventDisableTiming));
-  for (int wkb : {0, 32, 96, -1}) {
+  for (int wkb : {0, 32, 96, 176, -1}) {
     b.wkb = wkb;
     if (wkb >= 0)
       printf("-- %d KiB of weights per workgroup per op (%.1f MB per op)\n", wkb, wkb * 1024.0 * kWg / 1e6);
