@@ -555,14 +555,16 @@ def main(argv=None):
     def timed(runner, steps, warmup, use_graph):
         fn = runner.step
         if use_graph:
+            # warm-up and capture on the SAME stream: the library's prefill scratch workspace is per stream (it grows
+            # outside capture only), so a capture stream that never ran the shape would have none
             s = torch.cuda.Stream()
             s.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(s):
                 runner.step()
-            torch.cuda.current_stream().wait_stream(s)
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                runner.step(stream=torch.cuda.current_stream())
+            with torch.cuda.graph(g, stream=s):
+                runner.step(stream=s)
+            torch.cuda.current_stream().wait_stream(s)
             fn = g.replay
         for _ in range(warmup):
             fn()

@@ -158,6 +158,29 @@ def test_host_cache_sees_repack_into_same_buffer(oracle):
     L.nad_host_cache_clear()
 
 
+def test_host_cache_evict_contract_for_partial_rewrites(oracle):
+    """the per-call key samples the blob, so a partial in-place rewrite outside the pack API (a few groups
+    re-scaled) need not change it -- the documented contract (include/neural_amd.h) is nad_host_cache_evict before such
+    a rewrite is used.  Checked: after the rewrite + evict the forward follows the new bytes."""
+    L = _lib.lib()
+    n, k, m = 96, 1024, 3
+    blob = _wb(oracle, n, k, 41)
+    A = np.random.default_rng(2).uniform(-1, 1, size=(m, k)).astype(np.float32)
+    out = np.zeros((m, n), np.float32)
+    L.bestla_f32f32_forward(vp(A), vp(blob), vp(out), m, n, k, k, n, None)
+    assert _rel_err(out, oracle.forward(A, blob, n, k)) <= 2e-5
+    # rewrite the scales of a handful of (group, column) entries in place: fp16 scales, halve them
+    info = bestla.blob_info(blob)
+    s_off = int(info["s_off"]) if "s_off" in info else None
+    assert s_off is not None, info
+    sc = blob[s_off:s_off + 2 * 16].view(np.float16).copy()
+    blob[s_off:s_off + 2 * 16] = (sc * np.float16(0.5)).view(np.uint8)
+    L.nad_host_cache_evict(vp(blob))
+    L.bestla_f32f32_forward(vp(A), vp(blob), vp(out), m, n, k, k, n, None)
+    assert _rel_err(out, oracle.forward(A, blob, n, k)) <= 2e-5
+    L.nad_host_cache_clear()
+
+
 def test_device_forward_uses_caller_workspace_and_capture_contract(oracle):
     """bestla_device_f32f32_forward runs the prefill GEMM with the caller's workspace (sized by bestla_support ->
     nad_device_workspace_size); nad_device_forward under graph capture uses a bound workspace, and without one on a
