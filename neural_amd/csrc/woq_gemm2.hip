@@ -868,24 +868,34 @@ __global__ __launch_bounds__(512, 1) void woq_gemm5_kernel(GemmArgs a, const _Fl
   __syncthreads();
   float* const tw = reinterpret_cast<float*>(smem) + wave * (128 * 36);
   float* const tp = reinterpret_cast<float*>(smem) + (wave ^ 4) * (128 * 36);
-  const int io = (wk ^ 1) * 8, im = wk * 8;
+  // (static indices only: a wave-dependent index into acc would move the whole array to scratch memory)
+  auto put = [&](auto Oc) {
+    constexpr int O = decltype(Oc)::value;
 #pragma unroll
-  for (int i = 0; i < 8; i++)
+    for (int i = 0; i < 8; i++)
 #pragma unroll
-    for (int j = 0; j < 2; j++)
+      for (int j = 0; j < 2; j++)
 #pragma unroll
-      for (int rr = 0; rr < 4; rr++) tp[(i * 16 + kq * 4 + rr) * 36 + j * 16 + nl] = acc[io + i][j][rr];
+        for (int rr = 0; rr < 4; rr++) tp[(i * 16 + kq * 4 + rr) * 36 + j * 16 + nl] = acc[O + i][j][rr];
+  };
+  auto add = [&](auto Oc) {
+    constexpr int O = decltype(Oc)::value;
+#pragma unroll
+    for (int i = 0; i < 8; i++)
+#pragma unroll
+      for (int j = 0; j < 2; j++)
+#pragma unroll
+        for (int rr = 0; rr < 4; rr++) tw[(i * 16 + kq * 4 + rr) * 36 + j * 16 + nl] += acc[O + i][j][rr];
+  };
+  if (wk == 0)
+    put(std::integral_constant<int, 8>{});
+  else
+    put(std::integral_constant<int, 0>{});
   __syncthreads();
-#pragma unroll
-  for (int i = 0; i < 8; i++)
-#pragma unroll
-    for (int j = 0; j < 2; j++)
-#pragma unroll
-      for (int rr = 0; rr < 4; rr++) {
-        float* p = tw + (i * 16 + kq * 4 + rr) * 36 + j * 16 + nl;
-        // the same order for both halves of every output: (k-half 0) + (k-half 1)
-        *p = wk == 0 ? acc[im + i][j][rr] + *p : *p + acc[im + i][j][rr];
-      }
+  if (wk == 0)
+    add(std::integral_constant<int, 0>{});
+  else
+    add(std::integral_constant<int, 8>{});
   const int s0 = bn * 8 + wn * 2;
   const int col0 = s0 * 16;
 #pragma unroll 4

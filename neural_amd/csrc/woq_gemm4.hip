@@ -618,21 +618,34 @@ __global__ __launch_bounds__(512, 1) void woq_gemm4_kernel(GemmArgs a, const _Fl
   if constexpr (KSW) {
     __syncthreads();
     float* const tp = reinterpret_cast<float*>(smem) + (wave ^ 4) * (128 * 36);
-    const int io = (wk ^ 1) * 8;
+    // (static indices only: a wave-dependent index into acc would move the whole array to scratch memory)
+    auto put = [&](auto Oc) {
+      constexpr int O = decltype(Oc)::value;
 #pragma unroll
-    for (int i = 0; i < 8; i++)
+      for (int i = 0; i < 8; i++)
 #pragma unroll
-      for (int j = 0; j < 2; j++)
+        for (int j = 0; j < 2; j++)
 #pragma unroll
-        for (int rr = 0; rr < 4; rr++) tp[(i * 16 + kq * 4 + rr) * 36 + j * 16 + nl] = acc[(io + i) % RB][j][rr];
+          for (int rr = 0; rr < 4; rr++) tp[(i * 16 + kq * 4 + rr) * 36 + j * 16 + nl] = acc[(O + i) % RB][j][rr];
+    };
+    auto add = [&](auto Oc) {
+      constexpr int O = decltype(Oc)::value;
+#pragma unroll
+      for (int i = 0; i < 8; i++)
+#pragma unroll
+        for (int j = 0; j < 2; j++)
+#pragma unroll
+          for (int rr = 0; rr < 4; rr++) tw[(i * 16 + kq * 4 + rr) * 36 + j * 16 + nl] += acc[(O + i) % RB][j][rr];
+    };
+    if (wk == 0)
+      put(std::integral_constant<int, 8>{});
+    else
+      put(std::integral_constant<int, 0>{});
     __syncthreads();
-    const int im = wk * 8;
-#pragma unroll
-    for (int i = 0; i < 8; i++)
-#pragma unroll
-      for (int j = 0; j < 2; j++)
-#pragma unroll
-        for (int rr = 0; rr < 4; rr++) tw[(i * 16 + kq * 4 + rr) * 36 + j * 16 + nl] += acc[(im + i) % RB][j][rr];
+    if (wk == 0)
+      add(std::integral_constant<int, 0>{});
+    else
+      add(std::integral_constant<int, 8>{});
   } else {
 #pragma unroll
     for (int i = 0; i < 8; i++)
