@@ -56,8 +56,8 @@ struct Knobs {
   int gemv_wpc, gemv_grid, gemv_waves, gemv_pre, gemv_lean, gemv_ks, gemv_spw, gemv_disable;
   int compute_int8;
   int gemm2_disable, gemm4_all, gemm4_disable, ffn_f32, gemm_kernel, splitk_disable;
-  int gemm3_prio, gemm3_stagger, gemm4_stagger2, gemm_fold, gemm4_fold_all, gemm4_fold, gemm5, gemm4_ksw;
-  int engine_thin, engine_start_sync, engine_loaders, engine_depth, engine_slots;
+  int gemm3_stagger, gemm4_stagger2, gemm_fold, gemm4_fold_all, gemm4_fold, gemm5, gemm4_ksw;
+  int engine_loaders, engine_slots;
   int host_cache_mb, tile_kmajor;
 };
 static Knobs read_knobs() {
@@ -77,7 +77,6 @@ static Knobs read_knobs() {
   k.ffn_f32 = env_int("NAD_FFN_F32", 0);
   k.gemm_kernel = env_int("NAD_GEMM_KERNEL", 3);
   k.splitk_disable = env_int("NAD_SPLITK_DISABLE", 0);
-  k.gemm3_prio = env_int("NAD_GEMM3_PRIO", 0);
   k.gemm3_stagger = env_int("NAD_GEMM3_STAGGER", 1);  // measured +3-7 % (profiles/r02_gemm3_stagger.txt)
   k.gemm4_stagger2 = env_int("NAD_GEMM4_STAGGER2", 0);
   k.gemm_fold = env_int("NAD_GEMM_FOLD", 0);
@@ -85,10 +84,7 @@ static Knobs read_knobs() {
   k.gemm4_fold = env_int("NAD_GEMM4_FOLD", 1);
   k.gemm5 = env_int("NAD_GEMM5", 0);
   k.gemm4_ksw = env_int("NAD_GEMM4_KSW", 0);  // folded gemm4 launches with the waves split over K  // int4 g128 * 2^j prefill on gemm5 (waves split over K, scale folded)
-  k.engine_thin = env_int("NAD_ENGINE_THIN", 0);
-  k.engine_start_sync = env_int("NAD_ENGINE_START_SYNC", 0);
   k.engine_loaders = env_int("NAD_ENGINE_LOADERS", 2);
-  k.engine_depth = env_int("NAD_ENGINE_DEPTH", 1);
   k.engine_slots = env_int("NAD_ENGINE_SLOTS", 16);
   k.host_cache_mb = env_int("NAD_HOST_CACHE_MB", 64 * 1024);
   k.tile_kmajor = env_int("NAD_TILE_KMAJOR", 0);
@@ -1049,7 +1045,6 @@ static int run_gemm(const void* act, int act_t, int lda, int m, int k, const Dev
   a.aux = aux;
   a.ld_aux = ld_aux;
   const Knobs& kn = knobs();
-  a.prio = kn.gemm3_prio;
   a.stagger = kn.gemm3_stagger;  // measured +3-7 % (profiles/r02_gemm3_stagger.txt)
   a.stagger2 = kn.gemm4_stagger2;
   // scale folding measured 1-5 % SLOWER on gemm3 (profiles/r03_gemm3_fold.txt) and it rounds q * s to fp16: opt-in
@@ -1587,11 +1582,7 @@ extern "C" void* nad_chain_create(const nad_chain_op* ops, int n_ops, int m) {
     for (EngOp& e : host) e.fmt ^= 1;
   }
   const Knobs& kn = knobs();
-  g.thin = kn.engine_thin ? 1 : 0;  // bit 0: loader thinned during gathers (measured slower: off)
-  // bit 1: the loaders start after every consumer issued the first op's input loads (woq_chain.hip start sync)
-  if (kn.engine_start_sync) g.thin |= 2;  // measured 2 % slower (profiles/r03_engine_start_sync.txt)
-  g.loaders = kn.engine_loaders;  // loader waves (tools/dma_probe.hip: 2 x 2 fills in flight best)
-  g.depth = kn.engine_depth;      // fills in flight per loader wave (1 measured faster than 2)
+  g.loaders = kn.engine_loaders;  // loader waves (tools/dma_probe.hip: 2 loaders with one fill in flight each best)
   g.sd = int((sd_bytes + 1023) / 1024);
   if (g.sd < 1) g.sd = 1;
   g.max_slots = kn.engine_slots;  // ring slots at most (A/B of the ring's size)

@@ -62,9 +62,7 @@ struct EngGeometry {
   int kp;                       // activation row length (max over ops of nt * KT)
   size_t lds;                   // dynamic LDS bytes
   size_t slot_bytes;
-  int thin;                     // bit 0: no fill in flight while the consumers gather (NAD_ENGINE_THIN); bit 1: the
-                                // loaders wait for the consumers' first input loads (NAD_ENGINE_START_SYNC)
-  int loaders, depth;           // loader waves, fills in flight per loader wave
+  int loaders;                  // loader waves (one fill in flight each)
   int max_slots;                // cap on the ring's slots (A/B; 16 = as many as fit)
 };
 

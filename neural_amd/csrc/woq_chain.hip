@@ -78,7 +78,7 @@ constexpr int kNT = 2;                      // buffer-load aux: non-temporal (we
 constexpr unsigned kSpinMax = 1u << 24;     // ~1 s of s_sleep(1) polls
 // LDS control words (u32 index): FULL[16], FREE[16], consumer barrier, RMS partial sums[2][8], gather phase,
 // consumers that issued the launch's first gather (start sync)
-constexpr int kFull = 0, kFree = 16, kBar = 32, kNsum = 36, kPhase = 52, kStart = 53, kCtlBytes = 256;
+constexpr int kFull = 0, kFree = 16, kBar = 32, kNsum = 36, kCtlBytes = 256;
 constexpr int kPartBytes = kEngMaxStripes * NC * 16 * 4;
 
 typedef __attribute__((address_space(3))) void lds_void_t;
@@ -177,7 +177,7 @@ __device__ __forceinline__ void fill_groups_rt(const OpGeom& o, int gpt, int t0,
 // slot stay ordered whichever loader issues them.
 template <bool ASYM, int SD, int D>
 __device__ void loader(const EngOp* ops, int n_ops, char* ring, int S, int slot_bytes, uint32_t ctl_a, unsigned* ctl,
-                       int lane, int thin, int lw, int NL) {
+                       int lane, int lw, int NL) {
   constexpr int IPF = FT + SD + (ASYM ? 1 : 0);  // DMA instructions per fill: constant, so vmcnt counts are exact
   static_assert(D * IPF <= 63, "in-flight DMAs beyond what vmcnt counts");
   const uint32_t full_a = ctl_a + kFull * 4, free_a = ctl_a + kFree * 4;
@@ -187,18 +187,6 @@ __device__ void loader(const EngOp* ops, int n_ops, char* ring, int S, int slot_
   int pub_f = lw, pub_slot = lw;  // the next own fill to publish and its slot
   while (pub_slot >= S) pub_slot -= S;
   bool failed = false;
-  // start sync (thin bit 1): the first op's input loads go out before this launch's first DMA burst, which they would
-  // otherwise queue behind (the first op's gather is on the launch's critical path; its weights are not yet)
-  if (thin & 2) {
-    unsigned spins = 0;
-    while (!failed && lds_ld(ctl_a + kStart * 4) < unsigned(NC)) {
-      __builtin_amdgcn_s_sleep(1);
-      if (++spins > kSpinMax) {
-        give_up(ctl, 6);
-        failed = true;
-      }
-    }
-  }
   auto publish_one = [&]() {
     lds_st(full_a + pub_slot * 4, unsigned(pub_f + 1));
     mpub++;
@@ -260,12 +248,6 @@ __device__ void loader(const EngOp* ops, int n_ops, char* ring, int S, int slot_
           if (tr_first && lw == 0) ETRACE(6, op, wall_clock64());
           tr_first = false;
 #endif
-          // while the consumers gather an input, keep no fill in flight: their loads queue behind this wave's DMAs
-          // (MI355X_MICROARCH.md gather-pass: 0.3-0.65 us with the own DMA quiet vs 1.0-1.7 behind a refill burst)
-          if ((thin & 1) && lds_ld(ctl_a + kPhase * 4) != 0u) {
-            wait_vm<0>();
-            while (mpub < mine) publish_one();
-          }
           char* sb = ring + slot * slot_bytes;
           const int t0 = c * FT;
 #pragma unroll
@@ -363,7 +345,7 @@ using IC = std::integral_constant<int, V>;
 template <int B0, int G0, int B1, int G1, bool ASYM, int SD>
 __global__ __launch_bounds__(kEngMaxThreads, 1) void woq_engine_kernel(const EngOp* __restrict__ ops, int n_ops,
                                                                        unsigned* ctl, int S, int slot_bytes, int Kp,
-                                                                       int bump, int thin, int nl, int depth) {
+                                                                       int bump, int nl) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr bool MIXED = B0 != B1 || G0 != G1;
   const int lane = threadIdx.x & 63;
@@ -378,10 +360,7 @@ __global__ __launch_bounds__(kEngMaxThreads, 1) void woq_engine_kernel(const Eng
   __syncthreads();
   if (wave >= NC) {
     const int lw = wave - NC;
-    if (depth == 1)
-      loader<ASYM, SD, 1>(ops, n_ops, ring, S, slot_bytes, ctl_a, ctl, lane, thin, lw, nl);
-    else
-      loader<ASYM, SD, 2>(ops, n_ops, ring, S, slot_bytes, ctl_a, ctl, lane, thin, lw, nl);
+    loader<ASYM, SD, 1>(ops, n_ops, ring, S, slot_bytes, ctl_a, ctl, lane, lw, nl);
     return;
   }
 
@@ -429,7 +408,6 @@ __global__ __launch_bounds__(kEngMaxThreads, 1) void woq_engine_kernel(const Eng
     const int vpu = o.dual ? 2 : 1;
     const int nout = nv / vpu * 16;
 
-    if ((thin & 1) && cw == 0 && lane == 0) lds_st(ctl_a + kPhase * 4, 1u);  // gathering: loader thinned
     // 0) this lane's residual (one output per lane at most: nout <= 256), issued now, used in the epilogue
     float res_v = 0.f;
     unsigned long long res_g = 0;
@@ -523,7 +501,6 @@ __global__ __launch_bounds__(kEngMaxThreads, 1) void woq_engine_kernel(const Eng
             g[j] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(ra, q < npair ? q * 8 : kOOB, 0, 0));
           }
           __builtin_amdgcn_sched_barrier(0);
-          if ((thin & 2) && op == 0 && q0 == 0 && lane == 0) lds_add(ctl_a + kStart * 4, 1u);  // start sync
           if (cw == 0 && q0 == 0) ETRACE(11, op, wall_clock64());
 #pragma unroll
           for (int j = 0; j < PJ; j++) {
@@ -554,7 +531,6 @@ __global__ __launch_bounds__(kEngMaxThreads, 1) void woq_engine_kernel(const Eng
     // every consumer staged a share of the whole vector, so all meet before the stream.  (Staging only the consumer's
     // own tiles with no barrier measured 2-3 % slower per whole-token launch.)
     cbar(bar_a, bar_epoch, ctl, lane, failed);
-    if ((thin & 1) && cw == 0 && lane == 0) lds_st(ctl_a + kPhase * 4, 0u);
     if (cw == 0) ETRACE(2, op, wall_clock64());
 
     // 2) the weight stream: consumer cw takes tiles cw and cw + 8 of every fill.  One LDS round trip per fill: the FULL
@@ -792,8 +768,8 @@ bool engine_geometry(EngGeometry& g, int kp) {
   int s = int((budget - fixed) / g.slot_bytes);
   if (s > 16) s = 16;
   if (g.max_slots > 0 && s > g.max_slots) s = g.max_slots;
-  if (g.loaders < 1 || g.loaders > kEngMaxLoaders || g.depth < 1 || g.depth > 2) return false;
-  if (s < g.loaders * g.depth + 2) return false;  // fills in flight + at least two published ones for the consumers
+  if (g.loaders < 1 || g.loaders > kEngMaxLoaders) return false;
+  if (s < g.loaders + 2) return false;  // fills in flight + at least two published ones for the consumers
   g.slots = s;
   g.lds = fixed + size_t(s) * g.slot_bytes;
   return true;
@@ -811,7 +787,7 @@ static hipError_t engine_launch5(const EngOp* ops, int n_ops, const EngGeometry&
     attr = true;
   }
   hipLaunchKernelGGL(k, dim3(grid), dim3((kEngConsumers + g.loaders) * 64), g.lds, st, ops, n_ops, ctl, g.slots,
-                     int(g.slot_bytes), g.kp, bump, g.thin, g.loaders, g.depth);
+                     int(g.slot_bytes), g.kp, bump, g.loaders);
   return hipGetLastError();
 }
 

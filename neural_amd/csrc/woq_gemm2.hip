@@ -609,7 +609,6 @@ __global__ __launch_bounds__(512, 1) void woq_gemm3_kernel(GemmArgs a, const _Fl
     if constexpr (!L) hand_over(Hc, u);
   };
 
-  if (a.prio && wave >= 4) __builtin_amdgcn_s_setprio(1);  // static priority for the younger half (wave-uniform)
   if (a.stagger && wave >= 4) {
     for (int u = 0; u < nh; u += 2) {
       half(std::integral_constant<int, 0>{}, std::true_type{}, u);

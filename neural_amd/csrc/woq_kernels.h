@@ -71,7 +71,6 @@ struct GemmArgs {
   int ld_res;
   const float* aux;
   int ld_aux;
-  int prio;             // gemm3: waves 4-7 at s_setprio 1 for the whole loop (NAD_GEMM3_PRIO)
   int stagger;          // gemm3: waves 4-7 half a step behind waves 0-3 (NAD_GEMM3_STAGGER)
   int stagger2;         // gemm4: the stagger for int2 too (NAD_GEMM4_STAGGER2, A/B)
   int fold;             // gemm3 / gemm4: group scale folded into the fp16 B fragment (DeviceWeight::fold_ok)

@@ -255,6 +255,39 @@ def test_chain_rejects_ineligible():
                            out=[torch.empty((2, 128), device="cuda")])], 2)
 
 
+def test_chain_rejects_write_after_read_hazards():
+    """the engine orders only the hand-offs that go through granules, so nad_chain_create refuses
+    an op whose result or aux overwrites a vector an op of the chain reads from outside it (its own input included),
+    and any read of an earlier op's aux (aux has no in-launch hand-off)."""
+    w = _w(256, 256, 3)
+    wd = _w(256, 256, 4)
+    x = torch.rand((1, 256), device="cuda")
+    y = torch.empty((1, 256), device="cuda")
+    z = torch.empty((1, 256), device="cuda")
+    # op 1 writes op 0's external input
+    with pytest.raises(RuntimeError, match="write-after-read"):
+        bestla.Chain([dict(kind=CHAIN_LINEAR, w=[w], act=x, out=[y]),
+                      dict(kind=CHAIN_LINEAR, w=[wd], act=y, out=[x])], 1)
+    # an op writes its own input
+    with pytest.raises(RuntimeError, match="write-after-read"):
+        bestla.Chain([dict(kind=CHAIN_LINEAR, w=[w], act=x, out=[x])], 1)
+    # op 1's external residual overwritten by op 2
+    with pytest.raises(RuntimeError, match="write-after-read"):
+        bestla.Chain([dict(kind=CHAIN_LINEAR, w=[w], act=x, out=[y]),
+                      dict(kind=CHAIN_LINEAR, w=[wd], act=y, out=[z], epi=EPI_RES_ADD, res=x),
+                      dict(kind=CHAIN_LINEAR, w=[w], act=z, out=[x])], 1)
+    # reading an earlier op's aux
+    g1, g3 = _w(256, 256, 5), _w(256, 256, 6)
+    aux = torch.empty((1, 256), device="cuda")
+    t = torch.empty((1, 256), device="cuda")
+    with pytest.raises(RuntimeError, match="aux"):
+        bestla.Chain([dict(kind=CHAIN_GATE_UP, w=[g1, g3], act=x, out=[t], aux=aux),
+                      dict(kind=CHAIN_LINEAR, w=[wd], act=aux, out=[y])], 1)
+    # the legal form of the same chain still builds
+    bestla.Chain([dict(kind=CHAIN_LINEAR, w=[w], act=x, out=[y]),
+                  dict(kind=CHAIN_LINEAR, w=[wd], act=y, out=[z], epi=EPI_RES_ADD, res=x)], 1)
+
+
 def test_chain_mixed_formats_mistral_policy():
     """Two weight formats in one launch (Mistral-7B's int2 policy: q, k, o, gate, up, lm_head int2 g64; wv, w2 int4 g64;
     GQA so {Q, K} is one op and V its own): bit-identical across launch forms (whole token, cut at attention, one op

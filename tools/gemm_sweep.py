@@ -45,7 +45,6 @@ def main():
                     os.environ["NAD_GEMM5"] = "1" if kern[0] == "5" else "0"
                     os.environ["NAD_GEMM2_DISABLE"] = "1" if kern[0] == "0" else "0"
                     os.environ["NAD_GEMM4_DISABLE"] = "1" if kern[0] != "4" else "0"
-                    os.environ["NAD_GEMM3_PRIO"] = "1" if "p" in kern[1:] else "0"
                     os.environ["NAD_GEMM3_STAGGER"] = "1" if "s" in kern[1:] else "0"
                     os.environ["NAD_GEMM4_KSW"] = "1" if "k" in kern[1:] else "0"
                     os.environ["NAD_GEMM4_FOLD_ALL"] = "1" if "f" in kern[1:] else "0"
