@@ -1354,7 +1354,7 @@ extern "C" int nad_device_ffn_forward(const void* act, int act_dtype, const void
 // GELU_MUL.  The reference graph cuts such a segment at every attention node (ne_layers.c:11915-12028).
 struct NadChain {
   EngOp* dev_ops = nullptr;
-  unsigned* ctl = nullptr;              // [0] generation, [1] status, [2] workgroup arrivals (monotonic)
+  unsigned* ctl = nullptr;              // [1] status, [2] workgroup arrivals (monotonic; the launch generation is arrivals / grid)
   unsigned long long* gran = nullptr;   // granule arrays of the results read inside the launch
   int n_ops = 0, grid = 0, bump = 0;
   EngGeometry g{};

@@ -33,8 +33,9 @@
 //     each result element is published as ONE 8-byte {fp32 value, tag} granule by an agent-scope relaxed 64-bit store
 //     (write-through sc1), tag = launch generation * 256 + op index + 1; a consumer reads the whole input vector with
 //     sc1 buffer loads and re-reads every granule whose tag is not yet the expected one -- the data is the flag, no
-//     fence, no counter.  The generation is a per-chain device word bumped by workgroup 0 at its end, so stale
-//     granules of the previous run never match (graph replay safe, nothing to reset per call);
+//     fence, no counter.  The generation is the launch's index on its chain, taken by every workgroup at its start
+//     as a ticket of a monotonic arrival counter (ticket / grid), so stale granules of the previous run never match
+//     (graph replay safe, nothing to reset per call, nothing to publish at the end);
 //   * every spin is bounded (~1 s); a give-up records a code in ctl[1] and the launch still terminates;
 //   * one launch may hold two weight formats (the op body is a generic lambda over (bits, groups per tile)): Mistral's
 //     int2 policy keeps wv / w2 at int4 (llama_utils.cpp:269-287);
@@ -78,7 +79,7 @@ constexpr int kNT = 2;                      // buffer-load aux: non-temporal (we
 constexpr unsigned kSpinMax = 1u << 24;     // ~1 s of s_sleep(1) polls
 // LDS control words (u32 index): FULL[16], FREE[16], consumer barrier, RMS partial sums[2][8], gather phase,
 // consumers that issued the launch's first gather (start sync)
-constexpr int kFull = 0, kFree = 16, kBar = 32, kNsum = 36, kCtlBytes = 256;
+constexpr int kFull = 0, kFree = 16, kBar = 32, kNsum = 36, kGen = 60, kCtlBytes = 256;
 constexpr int kPartBytes = kEngMaxStripes * NC * 16 * 4;
 
 typedef __attribute__((address_space(3))) void lds_void_t;
@@ -367,7 +368,14 @@ __global__ __launch_bounds__(kEngMaxThreads, 1) void woq_engine_kernel(const Eng
   const int cw = wave, cl = wave * 64 + lane;  // consumer wave, consumer lane
   const uint32_t full_a = ctl_a + kFull * 4, free_a = ctl_a + kFree * 4, bar_a = ctl_a + kBar * 4;
   float* nsum = reinterpret_cast<float*>(smem) + kNsum;
-  const unsigned gen = __builtin_amdgcn_readfirstlane(__hip_atomic_load(ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  // The launch generation (granule tags): every workgroup takes a ticket from a monotonic arrival counter at its start;
+  // launches of one chain are stream-ordered, so tickets of launch L are L * grid ... L * grid + grid - 1 and
+  // gen = ticket / grid.  Nothing is bumped at the end (a workgroup that starts late, or owns no stripes, still reads
+  // its own launch's generation); the ticket's round trip overlaps the first op's gather and is read after its barrier.
+  unsigned gticket = 0;
+  if (cw == 0 && lane == 0)
+    gticket = __hip_atomic_fetch_add(ctl + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  unsigned gen = 0;  // defined after the first op's staging barrier (no op of a launch reads a granule before that)
   unsigned bar_epoch = 0;
   bool failed = false;
   const int m = lane & 15, kq = lane >> 4;
@@ -530,7 +538,9 @@ __global__ __launch_bounds__(kEngMaxThreads, 1) void woq_engine_kernel(const Eng
     }
     // every consumer staged a share of the whole vector, so all meet before the stream.  (Staging only the consumer's
     // own tiles with no barrier measured 2-3 % slower per whole-token launch.)
+    if (op == 0 && cw == 0 && lane == 0) lds_st(ctl_a + kGen * 4, gticket / gridDim.x);
     cbar(bar_a, bar_epoch, ctl, lane, failed);
+    if (op == 0) gen = lds_ld(ctl_a + kGen * 4);
     if (cw == 0) ETRACE(2, op, wall_clock64());
 
     // 2) the weight stream: consumer cw takes tiles cw and cw + 8 of every fill.  One LDS round trip per fill: the FULL
@@ -742,17 +752,7 @@ __global__ __launch_bounds__(kEngMaxThreads, 1) void woq_engine_kernel(const Eng
     else
       op_body(IC<B0>(), IC<G0>(), op);
   }
-  // the launch generation moves on once EVERY workgroup is past its last granule read (bump is set only when an op
-  // reads a result of this launch): the consumers of a workgroup meet, one lane arrives on a monotonic counter
-  // (ctl[2]), and the last arrival of this launch bumps the generation -- a workgroup that owns no stripes, or is
-  // scheduled late, can never read the next generation at its start
-  if (bump) {
-    cbar(bar_a, bar_epoch, ctl, lane, failed);
-    if (cw == 0 && lane == 0) {
-      const unsigned old = __hip_atomic_fetch_add(ctl + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (old == gridDim.x * (gen + 1u) - 1u) __hip_atomic_fetch_add(ctl, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
+  (void)bump;
 }
 
 }  // namespace eng

@@ -50,6 +50,7 @@ def set_env(cfg):
         for kv in cfg.split(","):
             k, v = kv.split("=")
             os.environ[k] = v
+    _lib.reload_knobs()  # the library reads its switches once
 
 
 def main():
