@@ -68,9 +68,8 @@ struct EngGeometry {
 
 // fills g.kp/slots/lds from g.bits/gpt/asym/sd and the ops' largest padded K; false if the ring does not fit
 bool engine_geometry(EngGeometry& g, int kp);
-// ops: device array; ctl: [0] launch generation (tags), [1] status (0 ok, else the first give-up code), [2] workgroup
-// arrivals (the last one of a launch bumps [0]); bump: some op
-// reads a result of this launch (the generation then moves on after the launch)
+// ops: device array; ctl: [1] status (0 ok, else the first give-up code), [2] workgroup arrivals (monotonic: the launch
+// generation that tags granules is arrivals / grid); bump: some op reads a result of this launch
 // the (bits, groups per tile) formats one launch may hold: one of int4 g >= 128 / g64, int2 g >= 256 / g128 / g64, or the
 // mixed pairs (int2 g64, int4 g64) and (int2 g128, int4 g128)
 bool engine_format_pair_ok(int bits0, int gpt0, int bits1, int gpt1);

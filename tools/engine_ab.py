@@ -12,6 +12,7 @@ sys.path.insert(0, REPO)
 import torch  # noqa: E402
 
 import bench  # noqa: E402
+from neural_amd import _lib  # noqa: E402
 
 specs = []
 for a in sys.argv[1:]:
@@ -50,6 +51,7 @@ for rep in range(2):
     for combo in combos:
         for (k, _), v in zip(specs, combo):
             os.environ[k] = v
+        _lib.reload_knobs()  # the library reads its switches once
         res = {}
         for cut in (True, False):
             cr = bench.ChainRunner(stack, "cuda", cut=cut)
