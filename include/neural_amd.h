@@ -173,8 +173,9 @@ int nad_device_forward(const void* act, int act_dtype, const void* devstor, floa
 /* Dry run of nad_device_forward for a weight geometry (bits 2 / 4 / 8, blocksize <= 0 = per-channel, scale_t
  * NAD_SCALE_*, m rows of act_dtype): the whole host side of the call -- validation, kernel choice, geometry,
  * workspace sizing -- with every launch recorded instead of issued; no device memory is touched and no GPU is needed.
- * out (versioned by nout): [kernel NAD_KERNEL_*, grid, threads per workgroup, split-K runs, scale folded into the fp16
- * weights (0/1), launches including pre-passes].  Returns the number of values written or -1. */
+ * out (versioned by nout): [kernel NAD_KERNEL_*, grid, threads per workgroup, split-K runs, flags (bit 0: scale folded
+ * into the fp16 weights; bit 1: gemm4 waves split over K), launches including pre-passes].  Returns the number of values
+ * written or -1. */
 #define NAD_KERNEL_GEMV_M1 1   /* woq_gemv_m1_kernel: M = 1 decode */
 #define NAD_KERNEL_GEMV 2      /* woq_gemv_kernel: the stripe-stream GEMV, M <= 16 */
 #define NAD_KERNEL_SKINNY 3    /* woq_skinny_kernel: decode geometries the stream does not take */
@@ -183,7 +184,6 @@ int nad_device_forward(const void* act, int act_dtype, const void* devstor, floa
 #define NAD_KERNEL_GEMM4 6     /* woq_gemm4_kernel: prefill, int4 g32 / g64, int2, int8 */
 #define NAD_KERNEL_GEMM2 7     /* woq_gemm2_kernel (NAD_GEMM_KERNEL=2) */
 #define NAD_KERNEL_GEMM 8      /* woq_gemm_kernel: register-staged prefill fallback */
-#define NAD_KERNEL_GEMM5 9     /* woq_gemm5_kernel: prefill, int4 groups of 128 * 2^j, waves split over K, scale folded */
 int nad_plan_forward(int bits, int n, int k, int blocksize, int scale_t, int asym, int m, int act_dtype, int64_t* out,
                      int nout);
 /* the same dry run for a loaded device weight (its format, act-order, fold range and compute mode included) */

@@ -166,8 +166,7 @@ def split_range(blob, axis, rank, world, unit=1):
 
 # ---------------------------------------------------------------------------------------------------- device
 KERNELS = {1: "woq_gemv_m1_kernel", 2: "woq_gemv_kernel", 3: "woq_skinny_kernel", 4: "woq_i8_kernel",
-           5: "woq_gemm3_kernel", 6: "woq_gemm4_kernel", 7: "woq_gemm2_kernel", 8: "woq_gemm_kernel",
-           9: "woq_gemm5_kernel"}
+           5: "woq_gemm3_kernel", 6: "woq_gemm4_kernel", 7: "woq_gemm2_kernel", 8: "woq_gemm_kernel"}
 
 
 def plan_forward(bits, n, k, group_size=128, scale_dtype="fp16", asym=False, m=1, act="fp32"):
@@ -180,7 +179,7 @@ def plan_forward(bits, n, k, group_size=128, scale_dtype="fp16", asym=False, m=1
     if r != 6:
         raise RuntimeError(f"nad_plan_forward failed: {last_error()}")
     return dict(kernel=KERNELS.get(int(o[0]), str(int(o[0]))), grid=int(o[1]), threads=int(o[2]), ksplit=int(o[3]),
-                fold=bool(o[4]), launches=int(o[5]))
+                fold=bool(o[4] & 1), ksw=bool(o[4] & 2), launches=int(o[5]))
 
 
 def _torch():
@@ -284,7 +283,7 @@ class DeviceWeight:
         if lib().nad_plan_weight(self.desc, m, at, _ptr(o), 6) != 6:
             raise RuntimeError(f"nad_plan_weight failed: {last_error()}")
         return dict(kernel=KERNELS.get(int(o[0]), str(int(o[0]))), grid=int(o[1]), threads=int(o[2]),
-                    ksplit=int(o[3]), fold=bool(o[4]), launches=int(o[5]))
+                    ksplit=int(o[3]), fold=bool(o[4] & 1), ksw=bool(o[4] & 2), launches=int(o[5]))
 
     def set_compute(self, mode):
         """Per-weight arithmetic (nad_device_set_compute): None / -1 follow the thread / process mode, COMPUTE_FP or

@@ -56,7 +56,7 @@ struct Knobs {
   int gemv_wpc, gemv_grid, gemv_waves, gemv_pre, gemv_lean, gemv_ks, gemv_spw, gemv_disable;
   int compute_int8;
   int gemm2_disable, gemm4_all, gemm4_disable, ffn_f32, gemm_kernel, splitk_disable;
-  int gemm3_stagger, gemm4_stagger2, gemm_fold, gemm4_fold_all, gemm4_fold, gemm5, gemm4_ksw;
+  int gemm3_stagger, gemm4_stagger2, gemm_fold, gemm4_fold_all, gemm4_fold, gemm4_ksw;
   int engine_loaders, engine_slots;
   int host_cache_mb, tile_kmajor;
 };
@@ -80,10 +80,9 @@ static Knobs read_knobs() {
   k.gemm3_stagger = env_int("NAD_GEMM3_STAGGER", 1);  // measured +3-7 % (profiles/r02_gemm3_stagger.txt)
   k.gemm4_stagger2 = env_int("NAD_GEMM4_STAGGER2", 0);
   k.gemm_fold = env_int("NAD_GEMM_FOLD", 0);
-  k.gemm4_fold_all = env_int("NAD_GEMM4_FOLD_ALL", 0);
+  k.gemm4_fold_all = env_int("NAD_GEMM4_FOLD_ALL", 1);
   k.gemm4_fold = env_int("NAD_GEMM4_FOLD", 1);
-  k.gemm5 = env_int("NAD_GEMM5", 0);
-  k.gemm4_ksw = env_int("NAD_GEMM4_KSW", 0);  // folded gemm4 launches with the waves split over K  // int4 g128 * 2^j prefill on gemm5 (waves split over K, scale folded)
+  k.gemm4_ksw = env_int("NAD_GEMM4_KSW", 2);  // folded gemm4 launches with the waves split over K: 0 off, 1 on, 2 auto
   k.engine_loaders = env_int("NAD_ENGINE_LOADERS", 2);
   k.engine_slots = env_int("NAD_ENGINE_SLOTS", 16);
   k.host_cache_mb = env_int("NAD_HOST_CACHE_MB", 64 * 1024);
@@ -1053,11 +1052,19 @@ static int run_gemm(const void* act, int act_t, int lda, int m, int k, const Dev
   const int pg = pipelined_gemm(w, m);
   // gemm4 at groups of 32 / 64 scales the products into the result every 32 / 64 k (4 / 2 FMAs per MFMA): there the
   // fold pays, +14-23 %; at groups of 128 (int2 / int8: int4 g128 runs gemm3) it measured +6-21 % with the int2 stagger
-  // it enables (profiles/r03_gemm4_g128_fold.txt) but is opt-in (NAD_GEMM4_FOLD_ALL=1) until the full GPU suite has run
-  // with it; NAD_GEMM4_FOLD=0 restores the exact fp32 per-group path (gemm4 scale folding)
+  // it enables (profiles/r03_gemm4_g128_fold.txt), the default since the full GPU suite ran green with it
+  // (profiles/r04_pytest_gpu_foldall.log; NAD_GEMM4_FOLD_ALL=0 keeps g128 unfolded); NAD_GEMM4_FOLD=0 restores the exact
+  // fp32 per-group path everywhere (gemm4 scale folding)
   if (pg == 4 && (w.blocksize == 32 || w.blocksize == 64 || kn.gemm4_fold_all))
     a.fold = w.fold_ok && kn.gemm4_fold ? 1 : 0;
-  if (pg == 4 && a.fold && kn.gemm4_ksw) a.ksw = 1;
+  // KSW (waves split over K, each B fragment dequantized once per workgroup): measured +8-18 % on launches of more than
+  // one round of output tiles or long K (gate 11008 x 4096, down 4096 x 11008 at M = 2048) and 0-7 % slower on a single
+  // round at K = 4096 (4096 x 4096, 256 tiles; profiles/r04_gemm4_ksw_ab.txt): auto picks it for the former
+  if (pg == 4 && a.fold) {
+    const int tiles = ((m + 255) / 256) * ((w.n + 127) / 128);
+    const bool win = tiles > device_cus() || w.nt * k_tile(w) >= 8192;
+    a.ksw = kn.gemm4_ksw == 1 || (kn.gemm4_ksw == 2 && win) ? 1 : 0;
+  }
   if (h16) {
     if (!pg) {
       set_err("fp16 GEMM output needs the pipelined GEMM");
@@ -1074,11 +1081,9 @@ static int run_gemm(const void* act, int act_t, int lda, int m, int k, const Dev
       pre = &own;
     }
     const bool g2 = pg == 3 && kn.gemm_kernel == 2;
-    // gemm5 (waves split over K: each B fragment dequantized once per workgroup) needs the fold
-    const bool g5 = pg == 3 && !g2 && kn.gemm5 && w.fold_ok;
-    if (g5) a.fold = 1;
     int ktiles = w.nt;
     const int ks = !g2 ? splitk_plan(w, m, &ktiles) : 1;
+    if (ks > 1 && kn.gemm4_ksw == 2) a.ksw = 0;  // auto KSW was measured on whole-K launches only
     if (ks > 1) {  // partials after the fp16 activations in the same workspace (stream-ordered reuse)
       a.ksplit = ks;
       a.ktiles = ktiles;
@@ -1089,14 +1094,13 @@ static int run_gemm(const void* act, int act_t, int lda, int m, int k, const Dev
       a.part = reinterpret_cast<float*>(base + a16);
     }
     const int tiles = ((m + 255) / 256) * ((w.n + 127) / 128);
-    if (planned(pg == 4 ? NAD_KERNEL_GEMM4 : (g2 ? NAD_KERNEL_GEMM2 : (g5 ? NAD_KERNEL_GEMM5 : NAD_KERNEL_GEMM3)),
-                tiles * ks, 512, ks, a.fold)) {
+    if (planned(pg == 4 ? NAD_KERNEL_GEMM4 : (g2 ? NAD_KERNEL_GEMM2 : NAD_KERNEL_GEMM3),
+                tiles * ks, 512, ks, a.fold | (a.ksw << 1))) {
       if (ks > 1) planned(0, 0, 0, 1, 0, false);  // the split-K reduce
       return 0;
     }
     hipError_t e = pg == 4 ? launch_gemm4(a, w.bits, pre->p, pre->ld, st)
                    : g2    ? launch_gemm2(a, pre->p, pre->ld, st)
-                   : g5    ? launch_gemm5(a, pre->p, pre->ld, st)
                            : launch_gemm3(a, pre->p, pre->ld, st);
     if (e == hipSuccess && ks > 1) e = launch_splitk_reduce(a, st);
     if (e != hipSuccess) {

@@ -654,269 +654,6 @@ __global__ __launch_bounds__(512, 1) void woq_gemm3_kernel(GemmArgs a, const _Fl
 }  // namespace g3
 
 // ------------------------------------------------------------------------------------------------------------------
-// gemm5: gemm3's pipeline (same DMA plan, rings, counted waits and barriers) with the waves split over K instead of M.
-// In gemm3 the 8 waves are 2 (M) x 4 (N), 128 x 32 per wave over the whole 64-deep half step, so each B stripe is
-// dequantized by BOTH M-waves (3.55 VALU per MFMA).  Here the waves are 1 (M) x 4 (N) x 2 (K): wave
-// (wn, wk) owns a 256 x 32 partial over the 32-deep step wk of every half step, so every B fragment is dequantized
-// once per workgroup (2 dequantizations + 32 MFMAs per wave and half step, against 4 + 32) and the A traffic per MFMA is
-// unchanged (16 fragments of one 32-deep step instead of 8 of two).  The two K-halves meet once in the epilogue.  The
-// group scale is folded into the fp16 B fragment (q * s rounded once, the host checked every q * s is an fp16 normal,
-// DeviceWeight::fold_ok) -- 256 x 32 fp32 accumulators per wave leave no room for per-group partials.
-namespace g5 {
-using namespace g3;
-
-template <size_t... I>
-__device__ __forceinline__ void lds_frags16(h8_t (&f)[16], uint32_t addr, std::index_sequence<I...>) {
-  ((f[I] = lds_b128<int(I) * 16 * ROWB>(addr)), ...);
-}
-
-template <bool ASYM>
-__global__ __launch_bounds__(512, 1) void woq_gemm5_kernel(GemmArgs a, const _Float16* __restrict__ A16, int lda16) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));
-  const int wk = wave >> 2, wn = wave & 3;
-  const SkinnyWeight& W = a.w;
-  const int M = a.M, nt = W.nt, ng = W.ng, ns = W.ns;
-  const int tpg = W.bs / KT;
-  const int tsh = __builtin_ctz(unsigned(tpg));
-
-  // XCD-aware remap and split-K runs exactly as gemm3
-  const int nbm = (M + BM - 1) / BM;
-  const int nbn = (ns + 7) / 8;
-  const int ntile = nbm * nbn;
-  const int nsplit = a.ksplit > 1 ? a.ksplit : 1;
-  const int nwg = ntile * nsplit;
-  int bid = blockIdx.x;
-  {
-    const int q = nwg / 8, r = nwg % 8, x = bid % 8, o = bid / 8;
-    bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + o;
-  }
-  const int ks = bid / ntile;
-  bid -= ks * ntile;
-  const int kt0 = nsplit > 1 ? ks * a.ktiles : 0;
-  const int ntl = nsplit > 1 ? min(a.ktiles, nt - kt0) : nt;
-  const int nh = 2 * ntl;
-  const int bm = bid / nbn, bn = bid % nbn;
-  const int m0 = bm * BM;
-  const int nl = lane & 15, kq = lane >> 4;
-
-  uint32_t aoff[4];
-#pragma unroll
-  for (int i = 0; i < 4; i++) {
-    const int row = (wave * 4 + i) * 8 + (lane >> 3);
-    const int grow = min(m0 + row, M - 1);
-    aoff[i] = uint32_t(grow) * uint32_t(lda16) * 2u + uint32_t(((lane & 7) ^ ((row >> 1) & 7)) * 16);
-  }
-  const char* abase = reinterpret_cast<const char*>(A16) + size_t(kt0) * KT * 2;
-  const char* btile =
-      static_cast<const char*>(W.tiles) + (size_t(min(bn * 8 + wave, ns - 1)) * nt * 64 + lane) * 16 + size_t(kt0) * 1024;
-  const int sstripe = min(bn * 8 + (wave & 1) * 4 + (lane >> 4), ns - 1);
-  const size_t srow0 = size_t(sstripe) * ng * 16 + nl + size_t(kt0 >> tsh) * 16;
-  const int st = a.scale_t;
-  const uint32_t* sbase = static_cast<const uint32_t*>(W.scales);
-  const uint32_t* zbase = reinterpret_cast<const uint32_t*>(W.zps);
-
-  auto issue = [&](auto Hc, int u) {
-    constexpr int H = decltype(Hc)::value;
-    if (u + 3 >= nh) return;
-    const int ua = u + 3;
-    char* ab = smem + (ua & 3) * HBUF;
-    const char* src = abase + size_t(ua) * ROWB;
-#pragma unroll
-    for (int i = 0; i < 4; i++) glds16(src + aoff[i], ab + (wave * 4 + i) * 1024);
-    if constexpr (H == 1) {
-      const int t = ua >> 1;
-      char* bb = smem + NA * HBUF + (t % NBR) * BBUF;
-      glds16(btile + size_t(t) * 1024, bb + wave * 1024);
-      const size_t si = srow0 + size_t(t >> tsh) * 16;
-      glds4(sbase + (st == kScaleF32 ? si : (si >> 1)), bb + BTILES + (wave & 1) * 256);
-      if constexpr (ASYM) glds4(zbase + (si >> 2), bb + BTILES + BSC + (wave & 1) * 256);
-    }
-  };
-  constexpr int NBW = ASYM ? 3 : 2;
-
-  f4_t acc[16][2];
-#pragma unroll
-  for (int i = 0; i < 16; i++)
-#pragma unroll
-    for (int j = 0; j < 2; j++) acc[i][j] = f4_t{0.f, 0.f, 0.f, 0.f};
-
-  issue(std::integral_constant<int, 1>{}, -3);
-  issue(std::integral_constant<int, 0>{}, -2);
-  issue(std::integral_constant<int, 1>{}, -1);
-  if (nh > 2)
-    wait_vm<8 + NBW>();
-  else
-    wait_vm<4>();
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-
-  const uint32_t m0k = 0x000F000Fu, m1k = 0x00F000F0u, mag = 0x64006400u;
-  const h2_t s16 = g2::splat(1.f / 16.f);
-  const h2_t zc0 = g2::splat(-(1024.f + 8.f)), zc1 = g2::splat(-(64.f + 8.f));
-  // A fragment i: rows i * 16 + nl, chunk (wk * 4 + kq) ^ f(row), f(row) = (row >> 1) & 7 = (nl >> 1) & 7
-  const uint32_t roff = uint32_t(nl * ROWB + (((wk * 4 + kq) ^ ((nl >> 1) & 7)) * 16));
-  // B dword of step 2 H + wk of stripe wn * 2 + j: byte (wn * 2 + j) * 1024 + lane * 16 + (2 H + wk) * 4
-  const int boff = (wn * 2) * 1024 + lane * 16 + wk * 4;
-  const int soff = BTILES + ((wn * 2) * 16 + nl) * 4;
-  const int zoff = BTILES + BSC + ((wn * 2) * 16 + nl) * 4;
-  const int ssh = st == kScaleF32 ? 0 : (nl & 1) * 16;
-  const int zsh = (nl & 3) * 8;
-  auto scale_h2 = [&](uint32_t x) {
-    const uint32_t h = (x >> ssh) & 0xFFFFu;
-    if (st == kScaleF16) return as_h2(h | (h << 16));
-    const float f = st == kScaleF32 ? __uint_as_float(x) : (st == kScaleBF16 ? __uint_as_float(h << 16)
-                                                                              : f16_bits_to_f32(uint16_t(h)));
-    return g2::splat(f);
-  };
-  h2_t fsc[2] = {g2::splat(1.f), g2::splat(1.f)};
-
-  auto hand_over = [&](auto Hc, int u) {
-    constexpr int H = decltype(Hc)::value;
-    if constexpr (H == 0) {
-      if (u + 3 < nh)
-        wait_vm<8 + NBW>();
-      else
-        wait_vm<0>();
-    } else {
-      if (u + 3 < nh)
-        wait_vm<8 + NBW>();
-      else if (u + 3 == nh)
-        wait_vm<4>();
-      else
-        wait_vm<0>();
-    }
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-  };
-
-  // L (staggered, waves 4-7): every LDS operand of half step u is in registers before the barrier, and the MFMAs run
-  // after it -- beside the other half's reads and dequantisation of half step u + 1 (MI355X_MICROARCH item 9)
-  auto half = [&](auto Hc, auto Lc, int u) {
-    constexpr int H = decltype(Hc)::value;
-    constexpr bool L = decltype(Lc)::value;
-    const int t = u >> 1;
-    const char* ab = smem + (u & 3) * HBUF;
-    const char* bb = smem + NA * HBUF + (t % NBR) * BBUF;
-    issue(Hc, u);
-    const uint32_t al = lds_addr(ab), bl = lds_addr(bb);
-    uint32_t bw0 = lds_b32<H * 8>(bl + boff), bw1 = lds_b32<1024 + H * 8>(bl + boff);
-    uint32_t zw0 = 0, zw1 = 0;
-    if constexpr (ASYM) {
-      zw0 = lds_b32<0>(bl + zoff);
-      zw1 = lds_b32<64>(bl + zoff);
-    }
-    uint32_t fw0 = 0, fw1 = 0;
-    if constexpr (H == 0) {  // every tile carries its group's scale piece
-      fw0 = lds_b32<0>(bl + soff);
-      fw1 = lds_b32<64>(bl + soff);
-    }
-    h8_t af[16];
-    lds_frags16(af, al + roff, std::make_index_sequence<16>{});
-    wait_lgk<8>(bw0, bw1, zw0, zw1, fw0, fw1, af[0], af[1], af[2], af[3], af[4], af[5], af[6], af[7]);
-    if constexpr (H == 0) {
-      fsc[0] = scale_h2(fw0);
-      fsc[1] = scale_h2(fw1);
-    }
-    if constexpr (L) {
-      wait_lgk<0>(af[8], af[9], af[10], af[11], af[12], af[13], af[14], af[15]);
-      hand_over(Hc, u);
-    }
-    const uint32_t bw[2] = {bw0, bw1};
-    h8_t bf[2];
-#pragma unroll
-    for (int j = 0; j < 2; j++) {
-      if constexpr (ASYM) {
-        const float zf = float(int(int8_t(((j ? zw1 : zw0) >> zsh) & 0xFFu)));
-        bf[j] = g2::dequant4(bw[j], m0k, m1k, mag, s16, zc0 - g2::splat(zf), zc1 - g2::splat(zf));
-      } else {
-        bf[j] = g2::dequant4(bw[j], m0k, m1k, mag, s16, zc0, zc1);
-      }
-      const h8_t s8 = {fsc[j][0], fsc[j][0], fsc[j][0], fsc[j][0], fsc[j][0], fsc[j][0], fsc[j][0], fsc[j][0]};
-      bf[j] = bf[j] * s8;
-    }
-#pragma unroll
-    for (int i = 0; i < 8; i++)
-#pragma unroll
-      for (int j = 0; j < 2; j++) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
-    if constexpr (!L) wait_lgk<0>(af[8], af[9], af[10], af[11], af[12], af[13], af[14], af[15]);
-#pragma unroll
-    for (int i = 8; i < 16; i++)
-#pragma unroll
-      for (int j = 0; j < 2; j++) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
-    if constexpr (!L) hand_over(Hc, u);
-  };
-
-  if (a.stagger && wave >= 4) {
-    for (int u = 0; u < nh; u += 2) {
-      half(std::integral_constant<int, 0>{}, std::true_type{}, u);
-      half(std::integral_constant<int, 1>{}, std::true_type{}, u + 1);
-    }
-  } else {
-    for (int u = 0; u < nh; u += 2) {
-      half(std::integral_constant<int, 0>{}, std::false_type{}, u);
-      half(std::integral_constant<int, 1>{}, std::false_type{}, u + 1);
-    }
-  }
-
-  // epilogue: the two K-halves of each 256 x 32 tile meet in LDS (the rings are dead: every wave's last LDS read came
-  // before its last barrier and the last waits drained every DMA).  Wave (wn, wk) finishes rows wk * 128 .. + 127: it
-  // writes its partial of the OTHER half's rows, transposed, into its partner's region, then adds its own partial of its
-  // own rows in place (read-modify-write, lanes of one wave: LDS operations in order) and stores whole 16-B row chunks.
-  __syncthreads();
-  float* const tw = reinterpret_cast<float*>(smem) + wave * (128 * 36);
-  float* const tp = reinterpret_cast<float*>(smem) + (wave ^ 4) * (128 * 36);
-  // (static indices only: a wave-dependent index into acc would move the whole array to scratch memory)
-  auto put = [&](auto Oc) {
-    constexpr int O = decltype(Oc)::value;
-#pragma unroll
-    for (int i = 0; i < 8; i++)
-#pragma unroll
-      for (int j = 0; j < 2; j++)
-#pragma unroll
-        for (int rr = 0; rr < 4; rr++) tp[(i * 16 + kq * 4 + rr) * 36 + j * 16 + nl] = acc[O + i][j][rr];
-  };
-  auto add = [&](auto Oc) {
-    constexpr int O = decltype(Oc)::value;
-#pragma unroll
-    for (int i = 0; i < 8; i++)
-#pragma unroll
-      for (int j = 0; j < 2; j++)
-#pragma unroll
-        for (int rr = 0; rr < 4; rr++) tw[(i * 16 + kq * 4 + rr) * 36 + j * 16 + nl] += acc[O + i][j][rr];
-  };
-  if (wk == 0)
-    put(std::integral_constant<int, 8>{});
-  else
-    put(std::integral_constant<int, 0>{});
-  __syncthreads();
-  if (wk == 0)
-    add(std::integral_constant<int, 0>{});
-  else
-    add(std::integral_constant<int, 8>{});
-  const int s0 = bn * 8 + wn * 2;
-  const int col0 = s0 * 16;
-#pragma unroll 4
-  for (int q = 0; q < 16; q++) {
-    const int c = q * 64 + lane;
-    const int rl = c >> 3, c4 = c & 7;
-    const int row = m0 + wk * 128 + rl;
-    const int n0 = col0 + c4 * 4;
-    const float4 t = *reinterpret_cast<const float4*>(tw + rl * 36 + c4 * 4);
-    if (row >= M || n0 >= W.n) continue;
-    if (nsplit > 1) {
-      *reinterpret_cast<float4*>(a.part + (size_t(ks) * M + row) * a.ldp + n0) = t;
-      continue;
-    }
-    float v[4] = {t.x, t.y, t.z, t.w};
-    gemm_epilogue4(a, row, n0, v);
-  }
-}
-
-}  // namespace g5
-
-// ------------------------------------------------------------------------------------------------------------------
 // split-K reduce: out[row][n] = epi(sum over runs r = 0 .. S-1, in order, of part[r][row][n]); 4 columns per thread
 __global__ __launch_bounds__(256) void nad_splitk_reduce_kernel(GemmArgs a) {
   const SkinnyWeight& W = a.w;
@@ -966,23 +703,6 @@ hipError_t launch_gemm3(const GemmArgs& a, const _Float16* A16, int lda16, hipSt
   }
   if (asym) return tpg1 ? go(g3::woq_gemm3_kernel<true, true, false>) : go(g3::woq_gemm3_kernel<true, false, false>);
   return tpg1 ? go(g3::woq_gemm3_kernel<false, true, false>) : go(g3::woq_gemm3_kernel<false, false, false>);
-}
-
-hipError_t launch_gemm5(const GemmArgs& a, const _Float16* A16, int lda16, hipStream_t st) {
-  const int nbm = (a.M + g3::BM - 1) / g3::BM, nbn = (a.w.ns + 7) / 8;
-  auto go = [&](auto k, bool& done) -> hipError_t {
-    if (!done) {
-      hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                         g3::LDS_BYTES);
-      if (e != hipSuccess) return e;
-      done = true;
-    }
-    hipLaunchKernelGGL(k, dim3(nbm * nbn * (a.ksplit > 1 ? a.ksplit : 1)), dim3(512), g3::LDS_BYTES, st, a, A16, lda16);
-    return hipGetLastError();
-  };
-  static bool attr[2] = {};
-  if (a.w.zps != nullptr) return go(g5::woq_gemm5_kernel<true>, attr[1]);
-  return go(g5::woq_gemm5_kernel<false>, attr[0]);
 }
 
 hipError_t launch_cvt_act(const void* A, int act_t, int lda, int M, int K, int Kp, const int32_t* shuffle,

@@ -136,8 +136,6 @@ hipError_t launch_gemm2(const GemmArgs& a, const _Float16* A16, int lda16, hipSt
 // prefill GEMM v3 (woq_gemm2.hip): same contract as launch_gemm2; every operand staged by LDS-DMA three 64-deep half
 // steps ahead with counted vmcnt (no drain at the barriers)
 hipError_t launch_gemm3(const GemmArgs& a, const _Float16* A16, int lda16, hipStream_t stream);
-// gemm5: the gemm3 pipeline with the waves split over K (each B fragment dequantized once per workgroup), scale folded
-hipError_t launch_gemm5(const GemmArgs& a, const _Float16* A16, int lda16, hipStream_t st);
 // prefill GEMM v4 (woq_gemm4.hip): gemm3's pipeline for int4 groups of 32 / 64 and int2 groups >= 64.
 // gemm4_mode: 0 = not taken, else the group mode; A as for gemm3 with K padded to the weight's K tile (128 / 256)
 int gemm4_mode(int bits, int blocksize, int ng, int kpad, bool asym);

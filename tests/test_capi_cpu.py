@@ -227,6 +227,21 @@ def test_plan_forward_kernel_choice():
         assert (r["kernel"], r["fold"]) == ("woq_gemm4_kernel", True), (bits, g, r)
     r = p(4, 4096, 4096, 128, m=64)
     assert r["kernel"] == "woq_gemm3_kernel" and r["ksplit"] > 1 and r["launches"] == 3   # + the split-K reduce
+    # int8 / int2 at g128 fold too (NAD_GEMM4_FOLD_ALL default since round 4)
+    assert p(8, 4096, 4096, 128, m=2048)["fold"] and p(2, 4096, 4096, 128, m=2048)["fold"]
+
+
+def test_plan_gemm4_waves_split_over_k():
+    """gemm4's K-split wave layout (NAD_GEMM4_KSW=2, auto): on for more than one round of output tiles or K >= 8192
+    (gate, down, lm_head, M = 4096), off for one round at K = 4096 (profiles/r04_gemm4_ksw_ab.txt) and under split-K."""
+    p = bestla.plan_forward
+    assert not p(4, 4096, 4096, 32, m=2048)["ksw"]          # 256 tiles: one round on 256 CUs
+    assert p(4, 4096, 4096, 32, m=4096)["ksw"]              # 512 tiles
+    assert p(4, 11008, 4096, 32, m=2048)["ksw"]             # gate: 688 tiles
+    assert p(4, 4096, 11008, 32, m=2048)["ksw"]             # down: K = 11008
+    r = p(4, 4096, 11008, 32, m=64)
+    assert r["ksplit"] > 1 and not r["ksw"]                 # split-K launches keep the M-split waves
+    assert not p(4, 4096, 4096, 128, m=4096)["ksw"]         # int4 g128: gemm3
 
 
 def test_host_cost_per_forward_under_3us():
