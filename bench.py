@@ -284,7 +284,8 @@ def synthetic_sweep(torch, copies=128, reps=5, batch=64):
     of back-to-back launches replayed `reps` times -- min and median per launch.  Bytes per section 8(d) with 2-byte
     activations (in and out); M <= 64 is priced against HBM, larger M against the dense fp16 MFMA peak.
     Config 2 (M = 1) is also run as BTLAGemmBatchDriver-style batches (bestla_gemm.cpp:508-624): `batch` independent
-    problems in ONE weight-stream engine launch (no hand-off between them; fp32 activations as the engine takes)."""
+    problems in ONE launch -- of the batched M = 1 GEMV (nad_batch_*, the reported form) and of the weight-stream
+    engine (no hand-off between them); fp32 activations."""
     from neural_amd import bestla
     K = N = 4096
     g = 128
@@ -329,14 +330,28 @@ def synthetic_sweep(torch, copies=128, reps=5, batch=64):
                "us_per_problem_median": round(t_med * 1e6, 3), "GBps": round(byts / t_med / 1e9, 1),
                "frac": round(byts / t_med / 1e9 / HBM_PEAK_GBPS, 4), "bytes_per_problem": byts,
                "kernel": "woq_engine_kernel (independent ops: no hand-off)", "act": "fp32"}
+    # config 2 as BTLAGemmBatchDriver batches on the M = 1 GEMV (nad_batch_*): one launch per batch, workgroups dealt
+    # out problem by problem (the batch's problems stream like one large launch)
+    batches = [bestla.Batch([(ws[j * batch + i], xs[i], ys[i]) for i in range(batch)]) for j in range(sets)]
+
+    def fb(st):
+        for bb in batches:
+            bb.run(stream=st)
+    per = sorted(t / (sets * batch) for t in graph_times(fb, reps, torch))
+    t_med = per[len(per) // 2]
+    batched_gemv = {"problems_per_launch": batch, "launches_per_replay": sets,
+                    "us_per_problem_min": round(per[0] * 1e6, 3), "us_per_problem_median": round(t_med * 1e6, 3),
+                    "GBps": round(byts / t_med / 1e9, 1), "frac": round(byts / t_med / 1e9 / HBM_PEAK_GBPS, 4),
+                    "bytes_per_problem": byts, "kernel": "woq_gemv_m1_kernel (batched: nad_batch_run)", "act": "fp32"}
     single = next(r for r in rows if r["m"] == 1)
-    del chains, ws
+    del chains, batches, ws
     torch.cuda.empty_cache()
     return {"config": "K=N=4096 int4 g128 sym, fp16 scales, fp16 activations; 128 weight copies (1.1 GB) rotated "
                       "(cold); graph-replayed back-to-back launches, min / median over replays",
             "bytes_formula": "N*K/2 + N*K/128*2 + (M*K + M*N)*2 (section 8(d), 2-byte activations)",
             "per_m": rows,
             "config2_m1_single_launches": {k: single[k] for k in ("us_min", "us_median", "GBps", "frac", "kernel")},
+            "config2_m1_batched": batched_gemv,
             "config2_m1_batched_engine": batched,
             "m4096_mfma_frac": next(r for r in rows if r["m"] == 4096)["frac"]}
 

@@ -296,6 +296,21 @@ int nad_chain_run(void* chain, void* queue);  /* asynchronous on queue; graph-ca
 int nad_chain_status(void* chain);            /* 0, or the first give-up code of a bounded wait (synchronous) */
 void nad_chain_destroy(void* chain);
 
+/* ===== batched independent decode problems: BTLAGemmBatchDriver (bestla_gemm.cpp:508-624) for device tensors.  n
+ * problems y_i = x_i W_i (M = 1, fp32 x_i [K] 16-B aligned, fp32 y_i [N]) whose weights share N, K and format (int4 /
+ * int2, no act-order, fp arithmetic, a geometry the M = 1 GEMV takes) run as ONE launch: workgroups are dealt out
+ * problem by problem, each streaming its problem's share of the stripes.  The pointers are bound at creation (a device
+ * problem table): keep the tensors alive and reuse them across runs; run is asynchronous on queue and graph-capturable.
+ * create returns NULL with nad_last_error() set when the problems do not qualify. */
+typedef struct nad_batch_problem {
+  const void* weight; /* a loaded device weight (bestla_device_load_storage / nad_device_load) */
+  const float* act;   /* [K] */
+  float* out;         /* [N] */
+} nad_batch_problem;
+void* nad_batch_create(const nad_batch_problem* problems, int n);
+int nad_batch_run(void* batch, void* queue);
+void nad_batch_destroy(void* batch);
+
 #ifdef __cplusplus
 }
 #endif

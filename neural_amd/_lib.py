@@ -96,6 +96,9 @@ SIGNATURES = {
     "nad_chain_run": (_i, [_p, _p]),
     "nad_chain_status": (_i, [_p]),
     "nad_chain_destroy": (None, [_p]),
+    "nad_batch_create": (_p, [_p, _i]),
+    "nad_batch_run": (_i, [_p, _p]),
+    "nad_batch_destroy": (None, [_p]),
     "init_parallel_context": (_p, []),
     "get_tp_size": (_i, [_p]),
     "get_tp_rank": (_i, [_p]),

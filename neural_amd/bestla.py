@@ -410,6 +410,41 @@ def ffn_forward(x, w1, w2, w3, act="silu", tmp1=None, tmp2=None, out=None, strea
 CHAIN_LINEAR, CHAIN_QKV, CHAIN_GATE_UP = 0, 1, 2
 
 
+class Batch:
+    """Independent M = 1 problems y_i = x_i W_i of one weight shape as ONE launch (include/neural_amd.h nad_batch_*:
+    BTLAGemmBatchDriver, bestla_gemm.cpp:508-624, for device tensors).  problems: list of (DeviceWeight, x [K] or [1][K]
+    fp32 cuda tensor, y [N] or [1][N] fp32 cuda tensor); the tensors are bound at creation (keep them alive)."""
+
+    class _P(C.Structure):
+        _fields_ = [("weight", C.c_void_p), ("act", C.c_void_p), ("out", C.c_void_p)]
+
+    def __init__(self, problems):
+        arr = (Batch._P * len(problems))()
+        self._keep = []
+        for i, (w, x, y) in enumerate(problems):
+            arr[i].weight = C.cast(w.desc, C.c_void_p)
+            arr[i].act = x.data_ptr()
+            arr[i].out = y.data_ptr()
+            self._keep.extend((w, x, y))
+        self._arr = arr
+        h = lib().nad_batch_create(C.cast(arr, C.c_void_p), len(problems))
+        if not h:
+            raise RuntimeError(f"nad_batch_create failed: {last_error()}")
+        self.handle = h
+
+    def run(self, stream=None):
+        check(lib().nad_batch_run(self.handle, _stream(stream)), "nad_batch_run")
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h:
+            try:
+                lib().nad_batch_destroy(h)
+            except Exception:
+                pass
+            self.handle = None
+
+
 class Chain:
     """A decode step's WOQ matmuls as ONE persistent launch (include/neural_amd.h nad_chain_*).
 

@@ -1666,6 +1666,103 @@ extern "C" void nad_chain_destroy(void* chain) {
   delete c;
 }
 
+// ------------------------------------------------------------------------------------------------ batched problems
+struct NadBatch {
+  GemvArgs a;
+  int bits = 0, waves = 0, grid = 0;
+  size_t lds = 0;
+  GemvBatchEnt* dev = nullptr;
+};
+
+extern "C" void* nad_batch_create(const nad_batch_problem* p, int n) {
+  if (!p || n <= 0) {
+    set_err("nad_batch_create: need at least one problem");
+    return nullptr;
+  }
+  const DeviceWeight* w0 = as_weight(p[0].weight);
+  if (!w0) return nullptr;
+  for (int i = 0; i < n; i++) {
+    const DeviceWeight* w = as_weight(p[i].weight);
+    if (!w) return nullptr;
+    if (w->n != w0->n || w->k != w0->k || w->bits != w0->bits || w->blocksize != w0->blocksize ||
+        w->asym != w0->asym || w->scale_t != w0->scale_t || w->nt != w0->nt || w->ng != w0->ng ||
+        w->kmajor != w0->kmajor || w->f4kind != w0->f4kind) {
+      set_err("nad_batch_create: problem %d's weight differs in shape or format from problem 0's", i);
+      return nullptr;
+    }
+    if (w->shuffle || int8_compute(*w)) {
+      set_err("nad_batch_create: act-order and int8-compute weights are not batched");
+      return nullptr;
+    }
+    if (!p[i].act || !p[i].out || reinterpret_cast<uintptr_t>(p[i].act) % 16 != 0) {
+      set_err("nad_batch_create: problem %d needs a 16-B aligned activation vector and an output", i);
+      return nullptr;
+    }
+  }
+  auto* b = new NadBatch();
+  int gpt = 0;
+  float* out0 = p[0].out;
+  const int ldo = w0->n;
+  if (!prepare_gemv(b->a, b->waves, b->grid, gpt, p[0].act, kActF32, w0->k, 1, w0->k, 1, &w0, &out0, &ldo, kEpiNone,
+                    nullptr, 0, nullptr, 0, nullptr, 0) ||
+      !gemv_uses_m1(b->a, w0->bits, b->waves)) {
+    set_err("nad_batch_create: this weight geometry does not take the M = 1 GEMV");
+    delete b;
+    return nullptr;
+  }
+  // workgroups per problem: the chip's CUs dealt out evenly, more where one problem's stripes would not fit one
+  // workgroup's partial-sum slots
+  const int ns = w0->ns;
+  int wpp = std::max(1, std::min(ns, device_cus() / n));
+  for (;; wpp++) {
+    b->a.u_q = ns / wpp;
+    b->a.u_r = ns % wpp;
+    b->lds = gemv_lds_layout(b->a, w0->bits, b->waves, wpp);
+    if (b->lds <= 160 * 1024 || wpp >= ns) break;
+  }
+  if (b->lds > 160 * 1024) {
+    set_err("nad_batch_create: LDS layout does not fit");
+    delete b;
+    return nullptr;
+  }
+  b->a.batch_wpp = wpp;
+  b->grid = n * wpp;
+  b->bits = w0->bits;
+  std::vector<GemvBatchEnt> host(static_cast<size_t>(n));
+  for (int i = 0; i < n; i++) {
+    const DeviceWeight* w = as_weight(p[i].weight);
+    host[i] = GemvBatchEnt{p[i].act, w->tiles, w->scales, w->zps, p[i].out, {nullptr, nullptr, nullptr}};
+  }
+  if (hipMalloc(&b->dev, sizeof(GemvBatchEnt) * size_t(n)) != hipSuccess ||
+      hipMemcpy(b->dev, host.data(), sizeof(GemvBatchEnt) * size_t(n), hipMemcpyHostToDevice) != hipSuccess) {
+    set_err("nad_batch_create: device table allocation failed");
+    if (b->dev) (void)hipFree(b->dev);
+    delete b;
+    return nullptr;
+  }
+  b->a.batch = b->dev;
+  return b;
+}
+
+extern "C" int nad_batch_run(void* batch, void* queue) {
+  NadBatch* b = static_cast<NadBatch*>(batch);
+  if (!b) return -1;
+  if (planned(NAD_KERNEL_GEMV_M1, b->grid, b->waves * 64)) return 0;
+  hipError_t e = launch_gemv_batch(b->a, b->bits, b->waves, b->grid, b->lds, static_cast<hipStream_t>(queue));
+  if (e != hipSuccess) {
+    set_err("nad_batch_run: launch failed: %s", hipGetErrorString(e));
+    return -1;
+  }
+  return 0;
+}
+
+extern "C" void nad_batch_destroy(void* batch) {
+  NadBatch* b = static_cast<NadBatch*>(batch);
+  if (!b) return;
+  if (b->dev) (void)hipFree(b->dev);
+  delete b;
+}
+
 // ------------------------------------------------------------------------------------------------ synthetic weights
 __global__ void nad_fill_u32_kernel(uint32_t* p, uint64_t n, uint64_t seed) {
   for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < n; i += uint64_t(gridDim.x) * blockDim.x) {

@@ -577,7 +577,11 @@ static bool lean_ok(const GemvArgs& a, int bits, int waves) {
   return a.lean && a.M == 1 && inst && a.a_fast && nsl <= waves * lean_spw(a);
 }
 
-template <int BITS, int GPT, int AT, bool ASYM, int KSN, int SPW>
+// BATCH: independent problems of one shape in one launch (BTLAGemmBatchDriver, bestla_gemm.cpp:508-624): workgroup
+// b serves problem b / batch_wpp -- its activations, weight and output pointers come from the problem table (one
+// scalar-cache line) -- and that problem's share b % batch_wpp of the stripes, so a batch of decode-size problems
+// streams like one large launch instead of paying each launch's fixed chain.
+template <int BITS, int GPT, int AT, bool ASYM, int KSN, int SPW, bool BATCH>
 __global__ __launch_bounds__((m1_max_threads<GPT, KSN>())) void woq_gemv_m1_kernel(GemvArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int KT = BITS == 4 ? 128 : 256, SPT = KT / 32, SPG = SPT / GPT;
@@ -595,7 +599,17 @@ __global__ __launch_bounds__((m1_max_threads<GPT, KSN>())) void woq_gemv_m1_kern
   const int nsl = (nt + KSN - 1) / KSN;
   const bool ulane = !PART || lane < UNITS;  // this lane holds a staging unit of each slice
   NAD_TRACE(0);
-  const int bid = blockIdx.x;
+  int bid = blockIdx.x;
+  if constexpr (BATCH) {
+    const int p = bid / a.batch_wpp;
+    bid -= p * a.batch_wpp;
+    const GemvBatchEnt e = a.batch[p];
+    a.A = e.act;
+    a.w[0].tiles = e.tiles;
+    a.w[0].scales = e.scales;
+    a.w[0].zps = e.zps;
+    a.w[0].out = e.out;
+  }
   const int u0 = bid * a.u_q + min(bid, a.u_r);
   const int u1 = u0 + a.u_q + (bid < a.u_r ? 1 : 0);
   const int vpu = a.dual ? 2 : 1;
@@ -815,7 +829,19 @@ static hipError_t gemv_launch4(const GemvArgs& a, dim3 g, dim3 b, size_t lds, hi
 
 template <int BITS, int GPT, int AT, bool ASYM, int KSN, int SPW>
 static hipError_t gemv_m1_launch5(const GemvArgs& a, dim3 g, dim3 b, size_t lds, hipStream_t st) {
-  auto k = woq_gemv_m1_kernel<BITS, GPT, AT, ASYM, KSN, SPW>;
+  if (a.batch) {
+    auto kb = woq_gemv_m1_kernel<BITS, GPT, AT, ASYM, KSN, SPW, true>;
+    static bool attr_b = false;
+    if (!attr_b) {
+      hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kb), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                         160 * 1024);
+      if (e != hipSuccess) return e;
+      attr_b = true;
+    }
+    hipLaunchKernelGGL(kb, g, b, lds, st, a);
+    return hipGetLastError();
+  }
+  auto k = woq_gemv_m1_kernel<BITS, GPT, AT, ASYM, KSN, SPW, false>;
   static bool attr_set = false;
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -951,6 +977,13 @@ int gemv_groups_per_tile(int bits, int nt, int ng, int bs, int* tpg) {
 }
 
 bool gemv_uses_m1(const GemvArgs& a, int bits, int waves) { return lean_ok(a, bits, waves); }
+
+hipError_t launch_gemv_batch(const GemvArgs& a, int bits, int waves, int grid, size_t lds, hipStream_t stream) {
+  int tpg = 0;
+  const int gpt = gemv_groups_per_tile(bits, a.nt, a.ng, a.bs, &tpg);
+  if (gpt == 0 || !a.batch || a.batch_wpp <= 0 || !lean_ok(a, bits, waves)) return hipErrorInvalidValue;
+  return gemv_m1_launch(a, bits, gpt, dim3(grid), dim3(waves * 64), lds, stream);
+}
 
 hipError_t launch_gemv(const GemvArgs& a, int bits, int waves, int grid, size_t lds, hipStream_t stream) {
   const int hilo = a.act_t == kActF16 ? 0 : (a.M <= 8 ? 1 : 2);

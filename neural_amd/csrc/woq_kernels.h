@@ -90,6 +90,16 @@ struct GemmArgs {
   SkinnyWeight w;
 };
 
+// One problem of a batched M = 1 launch (nad_batch_*: BTLAGemmBatchDriver's independent problems, bestla_gemm.cpp:508-624)
+struct GemvBatchEnt {
+  const void* act;
+  const void* tiles;
+  const void* scales;
+  const int8_t* zps;
+  float* out;
+  const void* pad[3];  // 64 B per entry (one scalar-cache line)
+};
+
 // Persistent stripe-stream decode GEMV (woq_gemv.hip).  All weights of one launch share K, group size, scale type and
 // symmetry; for the dual epilogues w[0] = gate, w[1] = up.
 struct GemvArgs {
@@ -124,6 +134,8 @@ struct GemvArgs {
   int lean_ks;          // woq_gemv_m1_kernel: K tiles per K-slice (4, or 1 / 2 where that gives each of up to 16 waves one)
   int lean_spw;         // woq_gemv_m1_kernel: K-slices per wave at most (2, or 4 for long K)
   SkinnyWeight w[3];
+  const GemvBatchEnt* batch;  // batched M = 1 launch (woq_gemv_m1_kernel<..., BATCH>): problem p = blockIdx / batch_wpp
+  int batch_wpp;              //   reads its activations / weight / output from batch[p]; u_q / u_r split one problem
 };
 
 hipError_t launch_repack(const RepackArgs& a, hipStream_t stream);
@@ -200,5 +212,7 @@ void gemv_lean_slices(GemvArgs& a, int bits, int* waves, int ks_pref);
 hipError_t launch_gemv(const GemvArgs& a, int bits, int waves, int grid, size_t lds, hipStream_t stream);
 // whether launch_gemv would take woq_gemv_m1_kernel for these arguments
 bool gemv_uses_m1(const GemvArgs& a, int bits, int waves);
+// the batched M = 1 launch (requires gemv_uses_m1; grid = problems * a.batch_wpp)
+hipError_t launch_gemv_batch(const GemvArgs& a, int bits, int waves, int grid, size_t lds, hipStream_t stream);
 
 }  // namespace nad

@@ -2,7 +2,7 @@
 
 Usage: python tools/gemm_sweep.py [--m 2048,4096] [--act fp16,fp32] [--shapes o,gate,down,lm_head] [--reps 20]
        [--kernels 3,2] [--bits 4] [--group 128] [--asym]
-Kernels: 3 / 2 = the int4 pipelined kernels, suffix k = gemm4 waves split over K (j: the library's auto choice), a = int4 g128 on gemm4 too, f = fold at g128 too, 4 = gemm4 (int4 g32/g64, int2), 0 = generic tiled fallback.
+Kernels: 3 / 2 = the int4 pipelined kernels, suffix k = gemm4 waves split over K (j: the library's auto choice), a = int4 g128 on gemm4 too, f / u = fold at g128 on / off (default: the library's), 4 = gemm4 (int4 g32/g64, int2), 0 = generic tiled fallback.
 Each line: shape, M, activation dtype, kernel, average device time per forward (HIP events on the launch stream, back
 to back launches) and TFLOP/s (2*M*N*K / time).  fp32 activations include the one-pass fp16 conversion kernel.
 """
@@ -47,7 +47,10 @@ def main():
                     os.environ["NAD_GEMM3_STAGGER"] = "1" if "s" in kern[1:] else "0"
                     os.environ["NAD_GEMM4_KSW"] = "1" if "k" in kern[1:] else ("2" if "j" in kern[1:] else "0")
                     os.environ["NAD_GEMM4_ALL"] = "1" if "a" in kern[1:] else "0"
-                    os.environ["NAD_GEMM4_FOLD_ALL"] = "1" if "f" in kern[1:] else "0"
+                    if "f" in kern[1:] or "u" in kern[1:]:  # else the library's default
+                        os.environ["NAD_GEMM4_FOLD_ALL"] = "1" if "f" in kern[1:] else "0"
+                    else:
+                        os.environ.pop("NAD_GEMM4_FOLD_ALL", None)
                     _lib.reload_knobs()  # the library reads its switches once
                     for _ in range(3):
                         w.forward(x, out=out)
