@@ -37,8 +37,9 @@ LLAMA = dict(name="Llama-2-7B", hidden=4096, ffn=11008, layers=32, vocab=32000, 
              bits=dict(q=4, k=4, v=4, o=4, gate=4, up=4, down=4, lm=4), asym=False, fuse_qkv=True)
 LLAMA_ASYM = dict(LLAMA, asym=True, scale="bf16")   # GPTQ/AWQ zero points, bf16 scales as qpack stores them
 # Mistral-7B: kv heads 8 (n_head_kv != n_head: the reference's CPU graph runs three matmuls, llama.cpp:212-215); int2
-# policy keeps wv, w2 int4 sym.  Here nad_device_qkv_forward takes Q, K, V of different N and format: decode runs one
-# stream launch for {Q, K} (int2) and one for V (int4), each output bit-identical to its own launch.
+# policy keeps wv, w2 int4 sym.  Here nad_device_qkv_forward takes Q, K, V of different N and format: decode runs ONE
+# launch of two formats ({Q, K} int2 + V int4, woq_gemv_m1_dual_kernel), prefill one GEMM per weight; every output is
+# bit-identical to its own launch.
 MISTRAL = dict(name="Mistral-7B", hidden=4096, ffn=14336, layers=32, vocab=32000, kv=1024, head=128, group=64,
                bits=dict(q=2, k=2, v=4, o=2, gate=2, up=2, down=4, lm=2), asym=False, fuse_qkv=False, group_qkv=True,
                int4_roles_sym=True)
@@ -110,7 +111,9 @@ class Stack:
         wb = lambda role, n, k: weight_bytes(n, k, b[role], g, self.sbytes, self.asym_of(role))  # noqa: E731
         qkv = [("qkv", wb("q", self.nq, H) + wb("k", self.nkv, H) + wb("v", self.nkv, H) +
                 (m * H + m * (self.nq + 2 * self.nkv)) * a, 2 * m * (self.nq + 2 * self.nkv) * H, L)]
-        if c.get("group_qkv"):   # {Q, K} one launch (same format), V its own
+        # {Q, K} one launch (same format), V its own -- except at M = 1, where both formats share ONE launch
+        # (woq_gemv_m1_dual_kernel, NAD_GEMV_DUAL=1)
+        if c.get("group_qkv") and not (m == 1 and os.environ.get("NAD_GEMV_DUAL", "1") != "0"):
             qkv = [("qk", wb("q", self.nq, H) + wb("k", self.nkv, H) + (m * H + m * (self.nq + self.nkv)) * a,
                     2 * m * (self.nq + self.nkv) * H, L),
                    ("v", wb("v", self.nkv, H) + (m * H + m * self.nkv) * a, 2 * m * self.nkv * H, L)]

@@ -53,7 +53,7 @@ static int env_int(const char* name, int def) {
 // Tuning / A-B switches.  Read from the environment ONCE (at the first forward, or by nad_reload_knobs), never per
 // launch: the eager path an NE graph takes (one bestla_device_f32f32_forward per node) must not scan the environment.
 struct Knobs {
-  int gemv_wpc, gemv_grid, gemv_waves, gemv_pre, gemv_lean, gemv_ks, gemv_spw, gemv_disable;
+  int gemv_wpc, gemv_grid, gemv_waves, gemv_pre, gemv_lean, gemv_ks, gemv_spw, gemv_disable, gemv_dual;
   int compute_int8;
   int gemm2_disable, gemm4_all, gemm4_disable, ffn_f32, gemm_kernel, splitk_disable;
   int gemm3_stagger, gemm4_stagger2, gemm_fold, gemm4_fold_all, gemm4_fold, gemm4_ksw;
@@ -67,6 +67,7 @@ static Knobs read_knobs() {
   k.gemv_waves = env_int("NAD_GEMV_WAVES", 0);  // tests / tuning: waves of a stripe-stream launch
   k.gemv_pre = std::min(3, std::max(1, env_int("NAD_GEMV_PRE", 1)));
   k.gemv_lean = env_int("NAD_GEMV_LEAN", 1);
+  k.gemv_dual = env_int("NAD_GEMV_DUAL", 1);  // decode QKV of two formats (int2 Q, K + int4 V) as one launch
   k.gemv_ks = env_int("NAD_GEMV_KS", 2);        // K-slice width (tiles) of the M = 1 kernel's single-op launches
   k.gemv_spw = env_int("NAD_GEMV_SPW", 4);
   k.gemv_disable = env_int("NAD_GEMV_DISABLE", 0);
@@ -1224,6 +1225,36 @@ extern "C" int nad_device_qkv_forward(const void* act, int act_dtype, const void
     // one stream launch over every run of consecutive weights of one kind (Q, K and V may differ in N; a mixed-format
     // model such as the int2 policy's int4 wv gets {Q, K} + {V}), each output computed exactly as on its own
     auto kin = [&](int i, int j) { return same_kind(*ws[i], *ws[j]) && ws[i]->asym == ws[j]->asym; };
+    if (m == 1 && kin(0, 1) && !kin(1, 2) && knobs().gemv_dual && !knobs().gemv_disable) {
+      // {Q, K} int2 + {V} int4 at M = 1: ONE launch whose workgroups are split between the two formats by bytes
+      GemvArgs a1, a2;
+      int w1 = 0, w2 = 0, g1 = 0, g2 = 0, p1 = 0, p2 = 0;
+      if (prepare_gemv(a1, w1, g1, p1, act, act_dtype, lda, 1, k, 2, ws, outs, ldos, kEpiNone, nullptr, 0, nullptr, 0,
+                       nullptr, 0) &&
+          prepare_gemv(a2, w2, g2, p2, act, act_dtype, lda, 1, k, 1, ws + 2, outs + 2, ldos + 2, kEpiNone, nullptr, 0,
+                       nullptr, 0, nullptr, 0) &&
+          w1 == 16 && w2 == 16 && gemv_dual_ok(a1, ws[0]->bits, a2, ws[2]->bits, 16)) {
+        const double b1 = double(a1.units) * a1.nt, b2 = double(a2.units) * a2.nt;  // 1 KiB tiles of each part
+        const int cus = device_cus();
+        int n1 = int(cus * b1 / (b1 + b2) + 0.5);
+        n1 = std::max(1, std::min(std::min(n1, cus - 1), a1.units));
+        const int n2 = std::max(1, std::min(cus - n1, a2.units));
+        a1.u_q = a1.units / n1;
+        a1.u_r = a1.units % n1;
+        a2.u_q = a2.units / n2;
+        a2.u_r = a2.units % n2;
+        const size_t lds = std::max(gemv_lds_layout(a1, ws[0]->bits, 16, n1), gemv_lds_layout(a2, ws[2]->bits, 16, n2));
+        if (lds <= 160 * 1024) {
+          if (planned(NAD_KERNEL_GEMV_M1, n1 + n2, 16 * 64)) return 0;
+          hipError_t e = launch_gemv_dual(a1, a2, n1, n2, 16, lds, st);
+          if (e != hipSuccess) {
+            set_err("gemv dual launch failed: %s", hipGetErrorString(e));
+            return -1;
+          }
+          return 0;
+        }
+      }
+    }
     for (int i = 0; i < 3;) {
       int n = 1;
       while (i + n < 3 && kin(i, i + n)) n++;

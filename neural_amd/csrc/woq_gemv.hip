@@ -581,8 +581,10 @@ static bool lean_ok(const GemvArgs& a, int bits, int waves) {
 // b serves problem b / batch_wpp -- its activations, weight and output pointers come from the problem table (one
 // scalar-cache line) -- and that problem's share b % batch_wpp of the stripes, so a batch of decode-size problems
 // streams like one large launch instead of paying each launch's fixed chain.
+// The kernel body takes its workgroup index as an argument: woq_gemv_m1_dual_kernel runs two instantiations side by
+// side in one launch.
 template <int BITS, int GPT, int AT, bool ASYM, int KSN, int SPW, bool BATCH>
-__global__ __launch_bounds__((m1_max_threads<GPT, KSN>())) void woq_gemv_m1_kernel(GemvArgs a) {
+__device__ __forceinline__ void m1_body(GemvArgs& a, int bid) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int KT = BITS == 4 ? 128 : 256, SPT = KT / 32, SPG = SPT / GPT;
   constexpr int RB = lean_row_bytes(BITS, KSN);  // one fp16 row of a slice
@@ -599,7 +601,6 @@ __global__ __launch_bounds__((m1_max_threads<GPT, KSN>())) void woq_gemv_m1_kern
   const int nsl = (nt + KSN - 1) / KSN;
   const bool ulane = !PART || lane < UNITS;  // this lane holds a staging unit of each slice
   NAD_TRACE(0);
-  int bid = blockIdx.x;
   if constexpr (BATCH) {
     const int p = bid / a.batch_wpp;
     bid -= p * a.batch_wpp;
@@ -812,6 +813,23 @@ __global__ __launch_bounds__((m1_max_threads<GPT, KSN>())) void woq_gemv_m1_kern
   NAD_TRACE(3);
 }
 
+template <int BITS, int GPT, int AT, bool ASYM, int KSN, int SPW, bool BATCH>
+__global__ __launch_bounds__((m1_max_threads<GPT, KSN>())) void woq_gemv_m1_kernel(GemvArgs a) {
+  m1_body<BITS, GPT, AT, ASYM, KSN, SPW, BATCH>(a, int(blockIdx.x));
+}
+
+// Two weight formats in one decode launch: workgroups [0, ga) run format 1's body over a, the rest format 2's over b
+// (each exactly its own one-format launch's arithmetic).  The int2 policies' QKV (llama_utils.cpp:269-287: int2 Q, K
+// with an int4 V of the same group size) then costs one launch instead of two.  Both bodies take 16 waves at K = 4096
+// (int2: 1-tile slices of 256 k, int4: 2-tile slices of 256 k); the launch takes the larger LDS image.
+template <int B1, int G1, int K1, int B2, int G2, int K2, int AT>
+__global__ __launch_bounds__(1024) void woq_gemv_m1_dual_kernel(GemvArgs a, GemvArgs b, int ga) {
+  if (int(blockIdx.x) < ga)
+    m1_body<B1, G1, AT, false, K1, 2, false>(a, int(blockIdx.x));
+  else
+    m1_body<B2, G2, AT, false, K2, 2, false>(b, int(blockIdx.x) - ga);
+}
+
 // ------------------------------------------------------------------------------------------------ launcher
 template <int BITS, int HILO, int GPT, bool ASYM>
 static hipError_t gemv_launch4(const GemvArgs& a, dim3 g, dim3 b, size_t lds, hipStream_t st) {
@@ -977,6 +995,33 @@ int gemv_groups_per_tile(int bits, int nt, int ng, int bs, int* tpg) {
 }
 
 bool gemv_uses_m1(const GemvArgs& a, int bits, int waves) { return lean_ok(a, bits, waves); }
+
+bool gemv_dual_ok(const GemvArgs& a, int bits_a, const GemvArgs& b, int bits_b, int waves) {
+  int tpg = 0;
+  const int ga = gemv_groups_per_tile(bits_a, a.nt, a.ng, a.bs, &tpg), gb = gemv_groups_per_tile(bits_b, b.nt, b.ng, b.bs, &tpg);
+  const bool pair = bits_a == 2 && bits_b == 4 && ((ga == 4 && gb == 2) || (ga == 2 && gb == 1));
+  return pair && !a.asym && !b.asym && a.lean_ks == 1 && b.lean_ks == 2 && a.act_t == kActF32 && b.act_t == kActF32 &&
+         waves == 16 && lean_ok(a, bits_a, waves) && lean_ok(b, bits_b, waves);
+}
+
+hipError_t launch_gemv_dual(const GemvArgs& a, const GemvArgs& b, int ga, int gb, int waves, size_t lds,
+                            hipStream_t stream) {
+  int tpg = 0;
+  const int g1 = gemv_groups_per_tile(2, a.nt, a.ng, a.bs, &tpg);
+  auto go = [&](auto k) -> hipError_t {
+    static bool attr = false;
+    if (!attr) {
+      hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                         160 * 1024);
+      if (e != hipSuccess) return e;
+      attr = true;
+    }
+    hipLaunchKernelGGL(k, dim3(ga + gb), dim3(waves * 64), lds, stream, a, b, ga);
+    return hipGetLastError();
+  };
+  if (g1 == 4) return go(woq_gemv_m1_dual_kernel<2, 4, 1, 4, 2, 2, kActF32>);  // groups of 64
+  return go(woq_gemv_m1_dual_kernel<2, 2, 1, 4, 1, 2, kActF32>);              // groups of 128
+}
 
 hipError_t launch_gemv_batch(const GemvArgs& a, int bits, int waves, int grid, size_t lds, hipStream_t stream) {
   int tpg = 0;

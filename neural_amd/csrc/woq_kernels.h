@@ -212,6 +212,11 @@ void gemv_lean_slices(GemvArgs& a, int bits, int* waves, int ks_pref);
 hipError_t launch_gemv(const GemvArgs& a, int bits, int waves, int grid, size_t lds, hipStream_t stream);
 // whether launch_gemv would take woq_gemv_m1_kernel for these arguments
 bool gemv_uses_m1(const GemvArgs& a, int bits, int waves);
+// two M = 1 launches of different formats as one (int2 a + int4 b at groups of 64 or 128, fp32 activations, sym,
+// 16 waves each; a on workgroups [0, ga), b on [ga, ga + gb))
+bool gemv_dual_ok(const GemvArgs& a, int bits_a, const GemvArgs& b, int bits_b, int waves);
+hipError_t launch_gemv_dual(const GemvArgs& a, const GemvArgs& b, int ga, int gb, int waves, size_t lds,
+                            hipStream_t stream);
 // the batched M = 1 launch (requires gemv_uses_m1; grid = problems * a.batch_wpp)
 hipError_t launch_gemv_batch(const GemvArgs& a, int bits, int waves, int grid, size_t lds, hipStream_t stream);
 

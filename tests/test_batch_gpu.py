@@ -85,3 +85,27 @@ def test_batch_rejects_mixed_shapes():
     y1, y2 = torch.empty((1, 256), device="cuda"), torch.empty((1, 512), device="cuda")
     with pytest.raises(RuntimeError, match="differs in shape or format"):
         bestla.Batch([(a, x, y1), (c, x, y2)])
+
+
+@pytest.mark.parametrize("bs", [64, 128])
+def test_qkv_two_formats_one_launch(oracle, knob, bs):
+    """The int2 policy's decode QKV (llama_utils.cpp:269-287: int2 Q, K and an int4 V of one group size; Mistral-7B
+    shapes, 8 KV heads) as ONE launch of two formats (woq_gemv_m1_dual_kernel, NAD_GEMV_DUAL=1): bit-identical to the
+    two launches it replaces (NAD_GEMV_DUAL=0), and within the decode bar of the oracle."""
+    k = 4096
+    shapes = [(4096, S2), (1024, S2), (1024, S4)]
+    blobs = [_blob(oracle, n, k, bs, qt, F16, False, 4, seed=77 + n + i) for i, (n, qt) in enumerate(shapes)]
+    ws = [bestla.DeviceWeight(b) for b in blobs]
+    x = torch.from_numpy(np.random.default_rng(5).uniform(-0.5, 0.5, size=(1, k)).astype(np.float32)).cuda()
+    outs = {}
+    for dual in ("1", "0"):
+        knob("NAD_GEMV_DUAL", dual)
+        o = [torch.full((1, n), float("nan"), device="cuda") for n, _ in shapes]
+        bestla.qkv_forward(x, ws[0], ws[1], ws[2], out=tuple(o))
+        torch.cuda.synchronize()
+        outs[dual] = [t.cpu().numpy() for t in o]
+    for a, b in zip(outs["1"], outs["0"]):
+        assert np.array_equal(a, b)
+    for i, (n, _) in enumerate(shapes):
+        ref = oracle.forward(x.cpu().numpy(), blobs[i], n, k)
+        assert _rel_err(outs["1"][i], ref) <= TOL_DECODE
