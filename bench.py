@@ -416,7 +416,8 @@ def decode_workload(cfg, torch, reps=20, prefill=True, prefill_steps=5):
                         "frac": round(byts / best / 1e9 / HBM_PEAK_GBPS, 4)},
            "decode_path": path, "per_op_tokens_per_s": round(1.0 / t, 2),
            "engine_cut_tokens_per_s": round(1.0 / te, 2), "engine_whole_token_tokens_per_s": round(1.0 / eng["whole"][0], 2),
-           "launches_per_token": nl if t > te else sum(c for *_, c in L1)}
+           "launches_per_token": nl if t > te else sum(c for *_, c in L1),
+           "per_op_per_shape_us": {k: round(v * 1e6, 3) for k, v in time_launches(st, 1, reps, torch).items()}}
     if prefill:
         pre = Runner(st, 2048, None, "cuda")
         pdt = graph_time(lambda s: pre.step(stream=s), prefill_steps, torch)
