@@ -113,7 +113,10 @@ class Stack:
                 (m * H + m * (self.nq + 2 * self.nkv)) * a, 2 * m * (self.nq + 2 * self.nkv) * H, L)]
         # {Q, K} one launch (same format), V its own -- except at M = 1, where both formats share ONE launch
         # (woq_gemv_m1_dual_kernel, NAD_GEMV_DUAL=1)
-        if c.get("group_qkv") and not (m == 1 and os.environ.get("NAD_GEMV_DUAL", "1") != "0"):
+        dual = m == 1 and os.environ.get("NAD_GEMV_DUAL", "1") != "0"
+        if c.get("group_qkv") and dual:
+            pass                 # the fused entry above: one launch, the activations read once
+        elif c.get("group_qkv"):
             qkv = [("qk", wb("q", self.nq, H) + wb("k", self.nkv, H) + (m * H + m * (self.nq + self.nkv)) * a,
                     2 * m * (self.nq + self.nkv) * H, L),
                    ("v", wb("v", self.nkv, H) + (m * H + m * self.nkv) * a, 2 * m * self.nkv * H, L)]
