@@ -33,6 +33,7 @@ EPI_NONE, EPI_BIAS, EPI_SILU_MUL, EPI_GELU_MUL, EPI_GELU, EPI_ADD_GELU, EPI_SILU
 S1, S3, S5, S6, S7 = 1 | 0x100, 3 | 0x100, 5 | 0x100, 6 | 0x100, 7 | 0x100
 F4_E2M1, F4_BNB, F4_NF4 = 4, 4 | (1 << 16), 4 | (2 << 16)
 F8_E4M3, F8_E5M2, F8_E8M0 = 8, 8 | (1 << 16), 8 | (3 << 16)
+DQ8_BNB = 8 | (4 << 16)  # double-quantized u8 scale codes + fp32 block absmax / offset (bestla_storage.h:223-231)
 # quant_config.h:22-57 parse_bits ("int1" is not supported here); "fp4_bnb" names the F4_BNB type the reference packs
 # but has no command-line name for
 _WEIGHT_DTYPES = {"int4": S4, "int8": S8, "int2": S2, "int1": S1, "int3": S3, "int5": S5, "int6": S6, "int7": S7,
@@ -112,7 +113,8 @@ def qpack(int_weight, scales, zeros=None, g_idx=None, weight_dtype="int4", group
     z = np.ascontiguousarray(zeros, dtype=np.int8) if (asym and zeros is not None and np.size(zeros)) else None
     gi = np.ascontiguousarray(g_idx, dtype=np.int32) if (g_idx is not None and np.size(g_idx)) else None
     qt = parse_weight_dtype(weight_dtype)
-    st = F32 if scale_dtype == "fp32" else BF16
+    # "dq8_bnb" (no quant_utils name; the pack API's DQ8_BNB) double-quantizes the given scales at pack time
+    st = F32 if scale_dtype == "fp32" else (DQ8_BNB if scale_dtype == "dq8_bnb" else BF16)
     gsize = k if group_size == -1 else group_size
     comp = _COMP[compute_dtype]
     size = pack_size(n, k, gsize, qt, st, asym, comp, gi is not None)

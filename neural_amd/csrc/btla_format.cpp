@@ -186,11 +186,16 @@ Blob Blob::describe(int n, int k, int blocksize, uint32_t qtype, uint32_t scale_
   b.z_size = asym ? b.csize : 0;
   b.r_size = b.has_reduce ? b.csize * 2 : 0;
   b.shf_size = shuffle ? uint64_t(k) * 4 : 0;
+  if (scale_t == kDQ8_BNB) {  // resize -> initDoubleQuantBlkSize(Block, ...) (bestla_storage.h:750-758)
+    b.has_dq = true;
+    b.dq_blocksize = b.blocksize;
+    b.dq_size = (updiv(uint64_t(b.ngroups()) * n, uint64_t(b.dq_blocksize)) + 1) * 4;
+  }
   // update_size(): every aligned buffer is charged size + 16 + 64, optional ones + 1 flag byte
   uint64_t sz = 48 + (16 + b.q_size + 64) + 24 + (16 + b.s_size + 64);
   sz += 1 + (asym ? 16 + b.z_size + 64 : 0);
   sz += 1 + (b.has_reduce ? 16 + b.r_size + 64 : 0);
-  sz += 1;
+  sz += 1 + (b.has_dq ? 16 + b.dq_size + 64 : 0);
   sz += 1 + (shuffle ? 16 + b.shf_size + 64 : 0);
   b.size = padto(sz, 64);
   return b;
@@ -219,7 +224,8 @@ void Blob::write_header(int8_t* base) {
   if (asym) z_off = put_aligned(w, base, z_size);
   w.put<uint8_t>(has_reduce ? 1 : 0);
   if (has_reduce) r_off = put_aligned(w, base, r_size);
-  w.put<uint8_t>(0);
+  w.put<uint8_t>(has_dq ? 1 : 0);
+  if (has_dq) dq_off = put_aligned(w, base, dq_size);
   w.put<uint8_t>(has_shuffle ? 1 : 0);
   if (has_shuffle) shf_off = put_aligned(w, base, shf_size);
 }
@@ -256,7 +262,8 @@ bool Blob::parse(const void* buf, std::string* err) {
   if (asym) z_off = get_aligned(r, base, &z_size);
   has_reduce = r.get<uint8_t>() != 0;
   if (has_reduce) r_off = get_aligned(r, base, &r_size);
-  if (r.get<uint8_t>() != 0) return fail("double-quantized (DQ8_BNB) scales are not supported");
+  has_dq = r.get<uint8_t>() != 0;
+  if (has_dq) dq_off = get_aligned(r, base, &dq_size);
   has_shuffle = r.get<uint8_t>() != 0;
   if (has_shuffle) shf_off = get_aligned(r, base, &shf_size);
   if (prologue == 2) {
@@ -265,8 +272,15 @@ bool Blob::parse(const void* buf, std::string* err) {
   } else if (!dtype_is_int(qtype) || dtype_bits(qtype) < 1 || dtype_bits(qtype) > 8) {
     return fail("weight dtype must be an integer type S1_CLIP .. S8");
   }
-  if (scale_t != kF32 && scale_t != kBF16 && scale_t != kF16 && !(scale_t == kF8E8M0 && is_f8(qtype)))
-    return fail("scale dtype must be F32, BF16 or F16 (F8_E8M0 with F8 weights)");
+  if (scale_t == kDQ8_BNB || has_dq) {  // IsDoubleQuant(): sym integer or NF4 weights (bestla_prologue_b.h:170-176)
+    if (scale_t != kDQ8_BNB || !has_dq) return fail("DQ8_BNB scales without their double-quant buffer (or vice versa)");
+    if (asym) return fail("DQ8_BNB scales are symmetric only");
+    if (!dtype_is_int(qtype) && qtype != kF4NF4) return fail("DQ8_BNB scales go with integer or F4_NF4 weights");
+    if (dq_blocksize <= 0 || dq_blocksize % 8 || dq_size / 4 < updiv(uint64_t(ngroups()) * n, uint64_t(dq_blocksize)) + 1)
+      return fail("corrupt DQ8_BNB double-quant buffer");
+  } else if (scale_t != kF32 && scale_t != kBF16 && scale_t != kF16 && !(scale_t == kF8E8M0 && is_f8(qtype))) {
+    return fail("scale dtype must be F32, BF16, F16 or DQ8_BNB (F8_E8M0 with F8 weights)");
+  }
   CoreInfo ci = core_info(core_id);
   if (ci.ntile <= 0 || (ci.packrow != 1 && ci.packrow != 2 && ci.packrow != 4)) return fail("unknown core id");
   if (npad % ci.ntile || kpad % ci.packrow) return fail("blob padding does not match its core");
@@ -348,6 +362,80 @@ static inline float load_scale(const uint8_t* sp, size_t i, uint32_t t) {
   uint16_t h;
   std::memcpy(&h, sp + i * 2, 2);
   return t == kBF16 ? bf16_to_f32(h) : f16_to_f32(h);
+}
+
+// ----------------------------------------------------------------------------------------------- DQ8_BNB
+// bitsandbytes' signed dynamic map (create_dynamic_map, 7 exponent bits): for decade i = 0..6 the 2^i midpoints of
+// linspace(0.1, 1, 2^i + 1) scaled by 10^(i - 6), both signs, plus 0 and 1, sorted; bestla_utils.h:794-820 holds it
+// rounded to 5 decimals (tests/test_dq8.py checks all 256 values against the reference's table)
+float dq8_lut(int code) {
+  static const std::vector<float> t = [] {
+    std::vector<double> v;
+    for (int i = 0; i < 7; i++) {
+      const int items = (1 << i) + 1;
+      for (int j = 0; j + 1 < items; j++) {
+        const double b0 = 0.1 + 0.9 * j / (items - 1), b1 = 0.1 + 0.9 * (j + 1) / (items - 1);
+        const double m = std::pow(10.0, i - 6) * ((b0 + b1) / 2.0);
+        v.push_back(m);
+        v.push_back(-m);
+      }
+    }
+    v.push_back(0.0);
+    v.push_back(1.0);
+    std::sort(v.begin(), v.end());
+    std::vector<float> f(256);
+    for (int c = 0; c < 256; c++) f[c] = float(std::nearbyint(v[c] * 1e5) / 1e5);
+    return f;
+  }();
+  return t[size_t(code) & 255];
+}
+
+// get_dq8_bnb (kernel_ref.h:1930-1950): binary search, nearest neighbour on a miss (ties to the upper code)
+static uint8_t dq8_code(float v) {
+  int lo = 0, hi = 255;
+  while (lo <= hi) {
+    const int mid = lo + (hi - lo) / 2;
+    const float x = dq8_lut(mid);
+    if (x == v) return uint8_t(mid);
+    if (x < v)
+      lo = mid + 1;
+    else
+      hi = mid - 1;
+  }
+  if (hi < 0) return 0;
+  if (lo >= 256) return 255;
+  return uint8_t(v - dq8_lut(hi) < dq8_lut(lo) - v ? hi : lo);
+}
+
+void dq8_double_quant(float* scale, size_t n, int dqb, float* dq) {
+  float offset = 0.f;
+  for (size_t i = 0; i < n; i++) offset += scale[i];
+  offset /= float(n);
+  dq[updiv(n, size_t(dqb))] = offset;
+  size_t i = 0;
+  auto block = [&](size_t len) {
+    float absmax = std::numeric_limits<float>::min();
+    for (size_t j = 0; j < len; j++) {
+      scale[i + j] -= offset;
+      absmax = smax(absmax, std::fabs(scale[i + j]));
+    }
+    for (size_t j = 0; j < len; j++) scale[i + j] = float(dq8_code(scale[i + j] / absmax));
+    return absmax;
+  };
+  for (; i < n / dqb * dqb; i += dqb) dq[i / dqb] = block(size_t(dqb));
+  // a partial last block's absmax lands one slot further, on the offset (kernel_ref.h:1978); kept for parity
+  if (i < n) dq[i / dqb + 1] = block(n - i);
+}
+
+float Blob::scale_at(const int8_t* base, int g, int col) const {
+  const size_t c = size_t(g) * cstep + col;
+  const uint8_t* sp = reinterpret_cast<const uint8_t*>(base + s_off);
+  if (!has_dq) return load_scale(sp, c, scale_t);
+  float a, off;
+  std::memcpy(&a, base + dq_off + (size_t(g) * n + col) / dq_blocksize * 4, 4);
+  std::memcpy(&off, base + dq_off + dq_size - 4, 4);
+  const float p = dq8_lut(sp[c]) * a;  // two statements: no fused multiply-add, as the reference's scalar code
+  return p + off;
 }
 
 // ----------------------------------------------------------------------------------------------- quantizer
@@ -459,9 +547,26 @@ bool pack_quantized(Blob& b, int8_t* base, const int8_t* Q, int ldq, const float
   const int rawnk = b.ngroups_k(), nk = b.ngroups();
   // setQuantCorrection (bestla_prologue_b.h:244-335): scales/zp with zero padding rows and columns
   uint8_t* sp = reinterpret_cast<uint8_t*>(base + b.s_off);
+  std::vector<float> dqc;  // DQ8_BNB: packQWeight double-quantizes the [rawnk][N] scales first (bestla_prologue_b.h:381-386)
+  if (b.has_dq) {
+    if (nk != rawnk || b.asym) {
+      if (err) *err = b.asym ? "DQ8_BNB scales are symmetric only" : "DQ8_BNB scales need K padded within its last group";
+      return false;
+    }
+    dqc.assign(S, S + size_t(rawnk) * b.n);
+    std::vector<float> dq(updiv(dqc.size(), size_t(b.dq_blocksize)) + 1, 0.f);
+    dq8_double_quant(dqc.data(), dqc.size(), b.dq_blocksize, dq.data());
+    std::memset(base + b.dq_off, 0, b.dq_size);
+    std::memcpy(base + b.dq_off, dq.data(), dq.size() * 4);  // setDoubleQuantCorrection (:161-168)
+  }
   parallel_for(nk, [&](int g) {
-    for (int n = 0; n < b.npad; n++)
-      store_scale(sp, size_t(g) * b.npad + n, b.scale_t, (g < rawnk && n < b.n) ? S[size_t(g) * b.n + n] : 0.f);
+    for (int n = 0; n < b.npad; n++) {
+      const bool in = g < rawnk && n < b.n;
+      if (b.has_dq)  // setQuantCorrection DQ8_BNB (:313-329): static_cast<uint8_t>(code), zero padding
+        sp[size_t(g) * b.npad + n] = in ? uint8_t(dqc[size_t(g) * b.n + n]) : 0;
+      else
+        store_scale(sp, size_t(g) * b.npad + n, b.scale_t, in ? S[size_t(g) * b.n + n] : 0.f);
+    }
     if (b.asym) {
       int8_t* zp = base + b.z_off;
       for (int n = 0; n < b.npad; n++)
@@ -543,7 +648,7 @@ bool pack_quantized(Blob& b, int8_t* base, const int8_t* Q, int ldq, const float
     parallel_for(rawnk, [&](int g) {
       int k0 = g * b.blocksize, k1 = std::min(b.k, k0 + b.blocksize);
       for (int n = 0; n < b.n; n++) {
-        float s = load_scale(sp, size_t(g) * b.cstep + n, b.scale_t);
+        float s = b.scale_at(base, g, n);
         int z = b.asym ? (base + b.z_off)[size_t(g) * b.cstep + n] : 0;
         float t = 0.f;
         for (int kk = k0; kk < k1; kk++)  // from the stored codes (unpackWeight): S1 keeps compress_1bit's slot 4
@@ -585,7 +690,6 @@ static inline int8_t read_q(const Blob& b, const uint8_t* qp, const CoreInfo& ci
 void unpack_quantized(const Blob& b, const int8_t* base, int8_t* Q, float* S, int8_t* Z, int* shuffle) {
   const CoreInfo ci = core_info(b.core_id);
   const uint8_t* qp = reinterpret_cast<const uint8_t*>(base + b.q_off);
-  const uint8_t* sp = reinterpret_cast<const uint8_t*>(base + b.s_off);
   if (Q)
     parallel_for(b.k, [&](int kk) {
       for (int nn = 0; nn < b.n; nn++) Q[size_t(kk) * b.n + nn] = read_q(b, qp, ci, kk, nn);
@@ -593,7 +697,7 @@ void unpack_quantized(const Blob& b, const int8_t* base, int8_t* Q, float* S, in
   for (int g = 0; g < b.ngroups_k(); g++)
     for (int nn = 0; nn < b.n; nn++) {
       size_t ci2 = size_t(g) * b.cstep + nn;
-      if (S) S[size_t(g) * b.n + nn] = load_scale(sp, ci2, b.scale_t);
+      if (S) S[size_t(g) * b.n + nn] = b.scale_at(base, g, nn);
       if (Z) Z[size_t(g) * b.n + nn] = b.asym ? base[b.z_off + ci2] : 0;
     }
   if (shuffle && b.has_shuffle) std::memcpy(shuffle, base + b.shf_off, size_t(b.k) * 4);
@@ -602,7 +706,6 @@ void unpack_quantized(const Blob& b, const int8_t* base, int8_t* Q, float* S, in
 void unpack_fp32(const Blob& b, const int8_t* base, float* W, int ldw) {
   const CoreInfo ci = core_info(b.core_id);
   const uint8_t* qp = reinterpret_cast<const uint8_t*>(base + b.q_off);
-  const uint8_t* sp = reinterpret_cast<const uint8_t*>(base + b.s_off);
   parallel_for(b.k, [&](int kk) {
     int g = kk / b.blocksize;
     for (int nn = 0; nn < b.n; nn++) {
@@ -610,7 +713,7 @@ void unpack_fp32(const Blob& b, const int8_t* base, float* W, int ldw) {
       int z = b.asym ? base[b.z_off + c] : 0;
       const int f4 = f4_kind(b.qtype);
       const int8_t qv = read_q(b, qp, ci, kk, nn);
-      const float sc = load_scale(sp, c, b.scale_t);
+      const float sc = b.scale_at(base, g, nn);
       W[size_t(kk) * ldw + nn] = f4 >= 0 ? f4_lut(f4, qv) * sc : (is_f8(b.qtype) ? f8_to_f32(b.qtype, qv) * sc
                                                                                    : float(qv - z) * sc);
     }

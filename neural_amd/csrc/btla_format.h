@@ -83,10 +83,16 @@ struct Blob {
   // buffers: byte offsets from the blob base and sizes
   uint64_t q_off = 0, q_size = 0, s_off = 0, s_size = 0, z_off = 0, z_size = 0, r_off = 0, r_size = 0,
            shf_off = 0, shf_size = 0;
+  // DQ8_BNB double-quantized scales (mDQCorrectionBuf, bestla_storage.h:158,223-231): u8 codes in the scale buffer,
+  // then fp32 [updiv(ngroups * N, dq_blocksize)] block absmax + 1 offset (the mean of all scales) in this buffer
+  bool has_dq = false;
+  uint64_t dq_off = 0, dq_size = 0;
 
   int ngroups() const { return int((kpad + blocksize - 1) / blocksize); }      // rows of the scale buffer
   int ngroups_k() const { return int((k + blocksize - 1) / blocksize); }       // groups covering real K
-  size_t scale_bytes() const { return scale_t == kF32 ? 4 : (scale_t == kF8E8M0 ? 1 : 2); }
+  size_t scale_bytes() const { return scale_t == kF32 ? 4 : (scale_t == kF8E8M0 || scale_t == kDQ8_BNB ? 1 : 2); }
+  // fp32 scale of (group g, column n) whatever the stored dtype (DQ8_BNB: dq8_get_fp_scale, kernel_ref.h:1981-1991)
+  float scale_at(const int8_t* base, int g, int n) const;
 
   // describe a fresh blob (createStorage + resize, bestla_prologue_b.h:120-127, bestla_storage.h:725-753)
   static Blob describe(int n, int k, int blocksize, uint32_t qtype, uint32_t scale_t, bool asym, uint64_t core_id,
@@ -111,6 +117,12 @@ bool pack_quantized(Blob& b, int8_t* base, const int8_t* Q, int ldq, const float
 void unpack_quantized(const Blob& b, const int8_t* base, int8_t* Q, float* S, int8_t* Z, int* shuffle);
 // BTLAGemmUnPackB semantics: W[k][n] = float(q - zp) * s  (kernel_ref.h:1027-1056)
 void unpack_fp32(const Blob& b, const int8_t* base, float* W, int ldw);
+
+// DQ8_BNB (bitsandbytes' signed 8-bit dynamic map, bestla_utils.h:794-820): code -> value
+float dq8_lut(int code);
+// dq8_bnb_double_quant<false> (kernel_ref.h:1952-1979): scale[0, n) -> codes (as floats, in place); dq gets
+// updiv(n, dq_blocksize) + 1 floats (block absmax, then the offset).  dq must be zero-filled by the caller.
+void dq8_double_quant(float* scale, size_t n, int dq_blocksize, float* dq);
 
 // scale conversions used when storing scales in the blob's dtype
 uint16_t f32_to_bf16_rne(float v);   // bestla_utils.h:146-153

@@ -179,9 +179,10 @@ extern "C" void bestla_device_sync(void* queue) { (void)hipStreamSynchronize(sta
 extern "C" size_t bestla_device_storage_size(void) { return sizeof(DeviceWeight); }
 
 // ------------------------------------------------------------------------------------------------ load / repack
-// F8_E8M0 shared exponents become exact fp32 scales 2^e on the device
+// F8_E8M0 shared exponents become exact fp32 scales 2^e on the device; DQ8_BNB codes are decoded on the host at load
+// (dq8_get_fp_scale, kernel_ref.h:1981-1991) into the fp32 scales the reference computes
 static int scale_code(uint32_t t) {
-  return (t == kF32 || t == kF8E8M0) ? kScaleF32 : (t == kBF16 ? kScaleBF16 : kScaleF16);
+  return (t == kF32 || t == kF8E8M0 || t == kDQ8_BNB) ? kScaleF32 : (t == kBF16 ? kScaleBF16 : kScaleF16);
 }
 // NFloat kind of the device weight: 0..2 the F4 LUTs (int4 layout), 3 F8_E4M3 / 4 F8_E5M2 (int8 layout, raw codes)
 static int nfloat_kind(uint32_t qtype) {
@@ -233,24 +234,9 @@ static bool scale_in_fold_range(float s, float qmax) {
 static bool blob_fold_ok(const Blob& b, const uint8_t* base, int dev_bits) {
   if (b.scale_t == kF8E8M0 || nfloat_kind(b.qtype) >= 0) return false;  // F4 / F8 weights never take gemm3 / gemm4
   const float qmax = fold_qmax(dev_bits, b.asym);
-  const uint8_t* p = base + b.s_off;
-  const size_t es = b.scale_bytes(), n = b.s_size / es;
-  for (size_t i = 0; i < n; i++) {
-    float s;
-    if (es == 4) {
-      std::memcpy(&s, p + 4 * i, 4);
-    } else {
-      uint16_t h;
-      std::memcpy(&h, p + 2 * i, 2);
-      if (b.scale_t == kBF16) {
-        const uint32_t u = uint32_t(h) << 16;
-        std::memcpy(&s, &u, 4);
-      } else {
-        s = float(__builtin_bit_cast(_Float16, h));
-      }
-    }
-    if (!scale_in_fold_range(s, qmax)) return false;
-  }
+  for (int g = 0; g < b.ngroups_k(); g++)  // the padding rows and columns hold zeros
+    for (int n = 0; n < b.n; n++)
+      if (!scale_in_fold_range(b.scale_at(reinterpret_cast<const int8_t*>(base), g, n), qmax)) return false;
   return true;
 }
 
@@ -286,13 +272,20 @@ extern "C" int nad_device_load(const void* hostblob, void* devstor, void* device
   // stage the raw blob buffers on the device, repack there
   const uint8_t* base = static_cast<const uint8_t*>(hostblob);
   uint8_t* stage = nullptr;
-  const uint64_t qz = b.q_size, sz = b.s_size, zz = b.asym ? b.z_size : 0;
+  std::vector<float> dqs;  // DQ8_BNB: the decoded fp32 scales [ngroups][cstep], zero padding
+  if (b.has_dq) {
+    dqs.assign(size_t(b.ngroups()) * b.cstep, 0.f);
+    for (int g = 0; g < b.ngroups_k(); g++)
+      for (int n = 0; n < b.n; n++) dqs[size_t(g) * b.cstep + n] = b.scale_at(static_cast<const int8_t*>(hostblob), g, n);
+  }
+  const uint8_t* shost = b.has_dq ? reinterpret_cast<const uint8_t*>(dqs.data()) : base + b.s_off;
+  const uint64_t qz = b.q_size, sz = b.has_dq ? dqs.size() * 4 : b.s_size, zz = b.asym ? b.z_size : 0;
   HIP_OK(hipMalloc(&stage, align256(qz) + align256(sz) + align256(zz) + 256));
   uint8_t* dq = stage;
   uint8_t* ds = stage + align256(qz);
   uint8_t* dz = ds + align256(sz);
   HIP_OK(hipMemcpyAsync(dq, base + b.q_off, qz, hipMemcpyHostToDevice, st));
-  HIP_OK(hipMemcpyAsync(ds, base + b.s_off, sz, hipMemcpyHostToDevice, st));
+  HIP_OK(hipMemcpyAsync(ds, shost, sz, hipMemcpyHostToDevice, st));
   if (zz) HIP_OK(hipMemcpyAsync(dz, base + b.z_off, zz, hipMemcpyHostToDevice, st));
   if (b.has_shuffle) HIP_OK(hipMemcpyAsync(w.shuffle, base + b.shf_off, size_t(b.k) * 4, hipMemcpyHostToDevice, st));
   if (w.reduce) {  // bf16 rows [block][cstep] -> [block][red_ld], zero padded columns
@@ -2394,16 +2387,34 @@ extern "C" unsigned long long nad_host_blob_key(const void* blob) {
 }
 
 // ------------------------------------------------------------------------------------------------ pack API
+// scale dtype against weight dtype: F8_E8M0 with F8 weights (bestla_prologue_b.h:1198-1208); DQ8_BNB sym with integer
+// or NF4 weights and a group of a multiple of 8 (initDoubleQuantBlkSize asserts, bestla_storage.h:755-759)
+static bool pack_scale_ok(uint32_t qt, uint32_t st, bool asym, size_t bs, size_t K) {
+  if (st == kF8E8M0 && !is_f8(qt)) {
+    set_err("F8_E8M0 scales go with F8 weights only");
+    return false;
+  }
+  if (st == kDQ8_BNB) {
+    const size_t g = bs >= K || bs == 0 ? K : bs;
+    if (asym || (!dtype_is_int(qt) && qt != kF4NF4) || g % 8) {
+      set_err("DQ8_BNB scales need symmetric integer or F4_NF4 weights and a group size that is a multiple of 8");
+      return false;
+    }
+    return true;
+  }
+  if (st != kF32 && st != kBF16 && st != kF16 && st != kF8E8M0) {
+    set_err("scale dtype must be F32, BF16, F16, F8_E8M0 or DQ8_BNB");
+    return false;
+  }
+  return true;
+}
 extern "C" size_t BTLAGemmPackBSize(size_t N, size_t K, size_t BlkSize, uint32_t QuantType, uint32_t ScaleDtype,
                                     bool isAsym, int CompType, int* shuffle_indice) {
   if (!dtype_is_int(QuantType) && f4_kind(QuantType) < 0 && !is_f8(QuantType)) {
     set_err("weight dtype must be an integer, F4_BNB / F4_E2M1 / F4_NF4 or F8_E4M3 / F8_E5M2");
     return 0;
   }
-  if (ScaleDtype == kF8E8M0 && !is_f8(QuantType)) {
-    set_err("F8_E8M0 scales go with F8 weights only");
-    return 0;
-  }
+  if (!pack_scale_ok(QuantType, ScaleDtype, isAsym, BlkSize, K)) return 0;
   uint64_t core = select_core(CompType, QuantType, int(BlkSize), isAsym, host_isa_profile());
   if (!core) return 0;
   return Blob::describe(int(N), int(K), int(BlkSize), QuantType, ScaleDtype, isAsym, core, shuffle_indice != nullptr)
@@ -2414,7 +2425,7 @@ extern "C" bool BTLAGemmQuantPackB(void* PackedBuf, const float* FpData, size_t 
                                    size_t BlkSize, uint32_t QuantType, uint32_t ScaleDtype, bool isAsym, int CompType,
                                    bool isTrans, void* ThreadPool) {
   if ((!dtype_is_int(QuantType) && f4_kind(QuantType) < 0 && !is_f8(QuantType)) || !PackedBuf || !FpData) return false;
-  if (ScaleDtype == kF8E8M0 && !is_f8(QuantType)) return false;
+  if (!pack_scale_ok(QuantType, ScaleDtype, isAsym, BlkSize, K)) return false;
   uint64_t core = select_core(CompType, QuantType, int(BlkSize), isAsym, host_isa_profile());
   if (!core) return false;
   Blob b = Blob::describe(int(N), int(K), int(BlkSize), QuantType, ScaleDtype, isAsym, core, false);
@@ -2449,6 +2460,7 @@ extern "C" bool BTLAGemmPackB(void* PackedBuf, const int8_t* QData, const float*
                               size_t K, size_t ldb, size_t BlkSize, uint32_t QuantType, uint32_t ScaleDtype,
                               bool isAsym, int CompType, int* shuffle_indice, void* ThreadPool) {
   if (!dtype_is_int(QuantType) || !PackedBuf || !QData || !Scales) return false;
+  if (!pack_scale_ok(QuantType, ScaleDtype, isAsym, BlkSize, K)) return false;
   uint64_t core = select_core(CompType, QuantType, int(BlkSize), isAsym, host_isa_profile());
   if (!core) return false;
   Blob b = Blob::describe(int(N), int(K), int(BlkSize), QuantType, ScaleDtype, isAsym, core,
@@ -2570,6 +2582,10 @@ extern "C" size_t nad_blob_split(const void* src, int axis, int rank, int world,
   }
   if (b.has_shuffle && axis == 1) {
     set_err("act-order (g_idx) weights cannot be split along K");
+    return 0;
+  }
+  if (b.has_dq) {  // a slice would double-quantize its scales again around a new mean: not the same numbers
+    set_err("DQ8_BNB double-quantized weights cannot be split exactly");
     return 0;
   }
   int lo, hi;

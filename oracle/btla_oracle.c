@@ -299,9 +299,10 @@ typedef struct {
   int cstep;
   size_t csize, msize;
   int asym, has_red, has_shf;
-  size_t q_size, s_size, z_size, r_size, shf_size;
+  size_t q_size, s_size, z_size, r_size, shf_size, dq_size;
   /* offsets from blob base */
-  size_t q_off, s_off, z_off, r_off, shf_off;
+  size_t q_off, s_off, z_off, r_off, shf_off, dq_off;
+  int has_dq;
 } blob_t;
 
 /* StorageWeightKBlockNInteger::resize (bestla_storage.h:725-753) + createStorage (bestla_prologue_b.h:120-127) */
@@ -334,13 +335,18 @@ static void blob_describe(blob_t* b, int n, int k, int blocksize, uint32_t qtype
   b->z_size = asym ? b->csize * 1 : 0;
   b->r_size = b->has_red ? b->csize * 2 : 0;
   b->shf_size = shuffle ? (size_t)k * 4 : 0;
+  if (stype == ORC_DQ8_BNB) { /* initDoubleQuantBlkSize(Block, nk_scale, ..., N) (bestla_storage.h:750-759) */
+    b->has_dq = 1;
+    b->dq_bs = b->bs;
+    b->dq_size = (updiv((size_t)nk * n, (size_t)b->dq_bs) + 1) * sizeof(float); /* enable_double_quant :223-231 */
+  }
   /* update_size (bestla_storage.h:812-816): header 48 + aligned/optional buffer sizes, padto 64 */
   size_t sz = 48;
   sz += 16 + b->q_size + 64;
   sz += 24 + (16 + b->s_size + 64);
   sz += 1 + (asym ? 16 + b->z_size + 64 : 0);
   sz += 1 + (b->has_red ? 16 + b->r_size + 64 : 0);
-  sz += 1; /* DQ correction buffer: absent */
+  sz += 1 + (b->has_dq ? 16 + b->dq_size + 64 : 0); /* mDQCorrectionBuf */
   sz += 1 + (shuffle ? 16 + b->shf_size + 64 : 0);
   b->msize = padto(sz, 64);
 }
@@ -393,7 +399,8 @@ static void blob_write_header(blob_t* b, int8_t* base) {
   if (b->asym) b->z_off = aligned_buf(&p, base, b->z_size);
   w8(&p, (uint8_t)(b->has_red != 0));
   if (b->has_red) b->r_off = aligned_buf(&p, base, b->r_size);
-  w8(&p, 0); /* mDQCorrectionBuf */
+  w8(&p, (uint8_t)(b->has_dq != 0)); /* mDQCorrectionBuf */
+  if (b->has_dq) b->dq_off = aligned_buf(&p, base, b->dq_size);
   w8(&p, (uint8_t)(b->has_shf != 0));
   if (b->has_shf) b->shf_off = aligned_buf(&p, base, b->shf_size);
 }
@@ -451,7 +458,9 @@ static int blob_parse(blob_t* b, const void* buf) {
   if (b->asym) b->z_off = read_buf(&p, base, &b->z_size);
   b->has_red = r8(&p);
   if (b->has_red) b->r_off = read_buf(&p, base, &b->r_size);
-  if (r8(&p)) return -2; /* double quant unsupported */
+  b->has_dq = r8(&p);
+  if (b->has_dq) b->dq_off = read_buf(&p, base, &b->dq_size);
+  if (b->has_dq != (b->scat == ORC_DQ8_BNB)) return -2;
   b->has_shf = r8(&p);
   if (b->has_shf) b->shf_off = read_buf(&p, base, &b->shf_size);
   return 0;
@@ -475,6 +484,91 @@ int orc_blob_info(const void* buf, int64_t* o) {
                    (int64_t)b.shf_size};
   memcpy(o, v, sizeof(v));
   return 0;
+}
+
+/* ------------------------------------------------------------------ DQ8_BNB double quant */
+/* bestla_utils.h:794-820 dq8_bnb_LUT: bitsandbytes' signed dynamic map (7 exponent bits) rounded to 5 decimals.
+   Restated from its construction: decade i = 0..6 contributes the 2^i midpoints of linspace(0.1, 1, 2^i + 1) times
+   10^(i-6), both signs; plus 0 and 1; sorted.  tests/test_dq8.py pins all 256 values to the reference's table. */
+static float g_dq8[256];
+static int g_dq8_ready = 0;
+static int cmp_d(const void* a, const void* b) {
+  double x = *(const double*)a, y = *(const double*)b;
+  return x < y ? -1 : (x > y ? 1 : 0);
+}
+static const float* dq8_table(void) {
+  if (!g_dq8_ready) {
+    double v[256];
+    int c = 0;
+    for (int i = 0; i < 7; i++) {
+      int items = (1 << i) + 1;
+      for (int j = 0; j + 1 < items; j++) {
+        double b0 = 0.1 + 0.9 * j / (items - 1), b1 = 0.1 + 0.9 * (j + 1) / (items - 1);
+        double m = pow(10.0, i - 6) * ((b0 + b1) / 2.0);
+        v[c++] = m;
+        v[c++] = -m;
+      }
+    }
+    v[c++] = 0.0;
+    v[c++] = 1.0;
+    qsort(v, 256, sizeof(double), cmp_d);
+    for (int i = 0; i < 256; i++) g_dq8[i] = (float)(nearbyint(v[i] * 1e5) / 1e5);
+    g_dq8_ready = 1;
+  }
+  return g_dq8;
+}
+void orc_dq8_lut(float* out) { memcpy(out, dq8_table(), sizeof(float) * 256); }
+
+/* kernel_ref.h:1930-1950 get_dq8_bnb */
+static uint8_t dq8_encode(float v) {
+  const float* t = dq8_table();
+  int left = 0, right = 255;
+  while (left <= right) {
+    int mid = left + (right - left) / 2;
+    if (t[mid] == v) return (uint8_t)mid;
+    if (t[mid] < v)
+      left = mid + 1;
+    else
+      right = mid - 1;
+  }
+  if (right < 0) return 0;
+  if (left >= 256) return 255;
+  return (v - t[right] < t[left] - v) ? (uint8_t)right : (uint8_t)left;
+}
+
+/* kernel_ref.h:1952-1979 dq8_bnb_double_quant<false>: scale[] becomes codes (as floats); dq (zero-filled by the caller,
+   updiv(n, dq_bs) + 1 floats) gets each block's absmax and, last, the mean of all scales.  A partial last block writes
+   its absmax one slot further (:1978), over the mean; restated as is. */
+void orc_dq8_double_quant(float* scale, size_t n, int dq_bs, float* dq) {
+  float offset = 0.f;
+  for (size_t i = 0; i < n; i++) offset += scale[i];
+  offset /= (float)n;
+  dq[updiv(n, (size_t)dq_bs)] = offset;
+  size_t aligned = n / dq_bs * dq_bs;
+  for (size_t i = 0; i < n; i += dq_bs) {
+    size_t len = i < aligned ? (size_t)dq_bs : n - i;
+    float absmax = FLT_MIN;
+    for (size_t j = 0; j < len; j++) {
+      scale[i + j] -= offset;
+      absmax = smax(absmax, fabsf(scale[i + j]));
+    }
+    for (size_t j = 0; j < len; j++) scale[i + j] = (float)dq8_encode(scale[i + j] / absmax);
+    if (i < aligned)
+      dq[i / dq_bs] = absmax;
+    else
+      dq[i / dq_bs + 1] = absmax;
+  }
+}
+
+/* kernel_ref.h:1981-1991 dq8_get_fp_scale over [row][col] codes at src_stride, scale index (i * mN + j) / dq_bs */
+void orc_dq8_get_fp_scale(const uint8_t* src, float* dst, int row, int col, int dq_bs, int dq_offset_idx,
+                          const float* dq, int src_stride, int dst_stride, int mN) {
+  const float* t = dq8_table();
+  for (int i = 0; i < row; i++)
+    for (int j = 0; j < col; j++) {
+      float p = t[src[(size_t)i * src_stride + j]] * dq[((size_t)i * mN + j) / dq_bs];
+      dst[(size_t)i * dst_stride + j] = p + dq[dq_offset_idx];
+    }
 }
 
 /* store one scale value in the blob's scale dtype (setQuantCorrection, bestla_prologue_b.h:244-271):
@@ -504,6 +598,17 @@ static float get_scale(const uint8_t* sp, size_t idx, uint32_t scat) {
   return scat == ORC_BF16 ? orc_bf16_to_f32(h) : orc_fp16_to_f32(h);
 }
 
+/* fp32 scale of (group g, column nn): the stored dtype, or DQ8_BNB decoded as getScale does (bestla_prologue_b.h:699-706,
+   offset from the last slot of the double-quant buffer) */
+static float blob_scale(const blob_t* b, const int8_t* base, int g, int nn) {
+  const uint8_t* sp = (const uint8_t*)(base + b->s_off);
+  size_t ci = (size_t)g * b->cstep + nn;
+  if (!b->has_dq) return get_scale(sp, ci, b->scat);
+  const float* dq = (const float*)(base + b->dq_off);
+  float p = dq8_table()[sp[ci]] * dq[((size_t)g * b->n + nn) / b->dq_bs];
+  return p + dq[b->dq_size / 4 - 1];
+}
+
 /* dequantized W[k][n] (ld = ldw) from a parsed blob: getWeight + RevertPaddingInterleave (bestla_prologue_b.h:211-242) */
 static void blob_dequant(const blob_t* b, const int8_t* base, float* W, int ldw, int8_t* Qout, float* Sout,
                          int8_t* Zout) {
@@ -526,14 +631,13 @@ static void blob_dequant(const blob_t* b, const int8_t* base, float* W, int ldw,
     orc_decompress_planes(bits, q, flat, nel);
   int8_t* qkn = (int8_t*)malloc((size_t)b->k * b->n);
   orc_revert_padding_interleave(flat, qkn, b->k, b->n, b->kpad, b->npad, b->kpad, b->n, nt, pr);
-  const uint8_t* sp = (const uint8_t*)(base + b->s_off);
   const int8_t* zp = b->asym ? base + b->z_off : NULL;
   for (int kk = 0; kk < b->k; kk++) {
     int g = kk / b->bs;
     for (int nn = 0; nn < b->n; nn++) {
       size_t ci = (size_t)g * b->cstep + nn;
       int z = zp ? zp[ci] : 0;
-      float s = get_scale(sp, ci, b->scat);
+      float s = blob_scale(b, base, g, nn);
       int8_t qv = qkn[(size_t)kk * b->n + nn];
       if (W)
         W[(size_t)kk * ldw + nn] = f4 >= 0 ? orc_f4_lut(f4, qv) * s /* f4_dequantize, kernel_ref.h:1433-1438 */
@@ -546,7 +650,7 @@ static void blob_dequant(const blob_t* b, const int8_t* base, float* W, int ldw,
   for (int g = 0; g < nblk; g++)
     for (int nn = 0; nn < b->n; nn++) {
       size_t ci = (size_t)g * b->cstep + nn;
-      if (Sout) Sout[(size_t)g * b->n + nn] = get_scale(sp, ci, b->scat);
+      if (Sout) Sout[(size_t)g * b->n + nn] = blob_scale(b, base, g, nn);
       if (Zout) Zout[(size_t)g * b->n + nn] = zp ? zp[ci] : 0;
     }
   free(flat);
@@ -560,11 +664,28 @@ static int blob_pack_q_impl(blob_t* b, int8_t* base, const int8_t* Q, int ldb, c
   int rawnk = (int)updiv((size_t)k, (size_t)b->bs);
   int nk = (int)updiv((size_t)b->kpad, (size_t)b->bs);
   uint8_t* sp = (uint8_t*)(base + b->s_off);
-  for (int g = 0; g < nk; g++)
-    for (int nn = 0; nn < b->npad; nn++) {
-      float v = (g < rawnk && nn < n) ? S[(size_t)g * n + nn] : 0.f;
-      put_scale(sp, (size_t)g * b->npad + nn, b->scat, v);
-    }
+  if (b->has_dq) { /* packQWeight (bestla_prologue_b.h:381-386): double-quantize the [rawnk][N] scales, then
+                      setQuantCorrection stores static_cast<uint8_t>(code) with zero padding (:313-329) */
+    if (b->asym || nk != rawnk) return -4;
+    size_t ss = (size_t)rawnk * n, nd = updiv(ss, (size_t)b->dq_bs) + 1;
+    float* codes = (float*)malloc(sizeof(float) * ss);
+    float* dq = (float*)calloc(nd, sizeof(float));
+    memcpy(codes, S, sizeof(float) * ss);
+    orc_dq8_double_quant(codes, ss, b->dq_bs, dq);
+    memset(base + b->dq_off, 0, b->dq_size);
+    memcpy(base + b->dq_off, dq, nd * sizeof(float)); /* setDoubleQuantCorrection :161-168 */
+    for (int g = 0; g < nk; g++)
+      for (int nn = 0; nn < b->npad; nn++)
+        sp[(size_t)g * b->npad + nn] = (g < rawnk && nn < n) ? (uint8_t)codes[(size_t)g * n + nn] : 0;
+    free(codes);
+    free(dq);
+  } else {
+    for (int g = 0; g < nk; g++)
+      for (int nn = 0; nn < b->npad; nn++) {
+        float v = (g < rawnk && nn < n) ? S[(size_t)g * n + nn] : 0.f;
+        put_scale(sp, (size_t)g * b->npad + nn, b->scat, v);
+      }
+  }
   if (b->asym) {
     int8_t* zp = base + b->z_off;
     for (int g = 0; g < nk; g++)

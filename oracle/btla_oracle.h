@@ -34,6 +34,7 @@ extern "C" {
 #define ORC_F8_E4M3 (8u)                 /* EleBits8 | TypeFloat          (bestla.h:68-71) */
 #define ORC_F8_E5M2 (8u | (1u << 16))
 #define ORC_F8_E8M0 (8u | (3u << 16))    /* shared-exponent (mx) scale dtype */
+#define ORC_DQ8_BNB (8u | (4u << 16))    /* double-quantized u8 scale codes (bestla.h:72) */
 
 /* fp16/bf16 conversions (bestla/bestla/bestla_utils.h:116-229) */
 uint16_t orc_f32_to_bf16(float v);
@@ -143,6 +144,11 @@ void orc_quantize_f4_rowblock(const float* src, int8_t* dst, int row, int col, i
    quantize_f32_f8_rowblock_mxscale (e8m0 != 0: F8_E8M0 scales, else F32) */
 int8_t orc_f8_quantize(uint32_t t, float v, float scale, int e8m0);
 float orc_f8_to_f32(uint32_t t, int8_t code);
+/* DQ8_BNB double-quantized scales (kernel_ref.h:1930-1991, bestla_utils.h:794-820) */
+void orc_dq8_lut(float* out256);
+void orc_dq8_double_quant(float* scale, size_t n, int dq_bs, float* dq);
+void orc_dq8_get_fp_scale(const uint8_t* src, float* dst, int row, int col, int dq_bs, int dq_offset_idx,
+                          const float* dq, int src_stride, int dst_stride, int mN);
 void orc_quantize_f8_rowblock(const float* src, int8_t* dst, int row, int col, int ld_src, int ld_dst, float* scales,
                               int blocksize, uint32_t t, int e8m0);
 

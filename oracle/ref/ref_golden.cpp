@@ -389,6 +389,34 @@ static void case_layernorm(const char* cs, int rows, int size, bool isrms, float
   dump(cs, "dst", "f4", dst.data(), dst.size());
 }
 
+// DQ8_BNB double-quantized scales: the int4 sym scales of a [row][col] weight ([nblk][col], the ssize = N * nk_scale
+// array packQWeight hands over, bestla_prologue_b.h:381-386) through kernel_ref.h:1952-1979 dq8_bnb_double_quant
+// into u8 codes + dq_buf (zero-initialised like the avector doubleQuantScale resizes), and back through :1981-1991
+// dq8_get_fp_scale with the offset read from the buffer's last slot (getScale, bestla_prologue_b.h:699-706)
+static void case_dq8(const char* cs, int row, int col, int bs, int dq_blk, float amp) {
+  std::vector<float> src((size_t)row * col);
+  for (auto& v : src) v = urand(-amp, amp);
+  int nblk = (row + bs - 1) / bs;
+  std::vector<int8_t> q((size_t)row * col);
+  std::vector<float> s((size_t)nblk * col);
+  kernel::ref::quantize_f32_sign_int_rowblock(src.data(), q.data(), row, col, col, col, s.data(), nullptr, bs,
+                                              BTLA_DTYPE::S4_CLIP);
+  const size_t ssize = s.size(), nd = utils::updiv(ssize, (size_t)dq_blk) + 1;
+  std::vector<float> work(s), dq(nd, 0.f), dec(ssize), lut(dq8_bnb_LUT, dq8_bnb_LUT + 256);
+  kernel::ref::dq8_bnb_double_quant<false>(work.data(), ssize, dq_blk, dq.data());
+  std::vector<uint8_t> code(ssize);
+  for (size_t i = 0; i < ssize; i++) code[i] = static_cast<uint8_t>(work[i]);  // setQuantCorrection DQ8 (:313-329)
+  kernel::ref::dq8_get_fp_scale(code.data(), dec.data(), nblk, col, 0, dq_blk, (int)(nd - 1), dq.data(), col, col,
+                                false, col);
+  int meta[4] = {row, col, bs, dq_blk};
+  dump(cs, "meta", "i4", meta, 4);
+  dump(cs, "s", "f4", s.data(), ssize);
+  dump(cs, "code", "u1", code.data(), ssize);
+  dump(cs, "dq", "f4", dq.data(), nd);
+  dump(cs, "dec", "f4", dec.data(), ssize);
+  dump(cs, "lut", "f4", lut.data(), 256);
+}
+
 int main(int argc, char** argv) {
   if (argc < 2) {
     fprintf(stderr, "usage: %s <outdir>\n", argv[0]);
@@ -449,6 +477,9 @@ int main(int argc, char** argv) {
   case_layernorm("layernorm_ln_300", 7, 300, false, 1e-6f, 1.f, 0.75f);
   case_layernorm("layernorm_rms_11008", 2, 11008, true, 1e-6f, 40.f, 0.f);
   case_layernorm("layernorm_ln_4096", 3, 4096, false, 1e-5f, 3.f, -1.5f);
+  case_dq8("dq8_g32", 256, 40, 32, 32, 0.5f);           // 8 x 40 scales, dq blocks of 32: 10 full blocks
+  case_dq8("dq8_g128_ragged", 384, 21, 128, 128, 2.f);  // 63 scales in one partial dq block (the :1978 slot quirk)
+  case_dq8("dq8_g64_tail", 512, 100, 64, 64, 1.f);      // 800 scales = 12 full blocks + a 32-scale tail
   fclose(g_man);
   return 0;
 }

@@ -14,6 +14,7 @@ S8, S4, S2 = 8 | 0x100, 4 | 0x100, 2 | 0x100
 S1, S3, S5, S6, S7 = 1 | 0x100, 3 | 0x100, 5 | 0x100, 6 | 0x100, 7 | 0x100
 F4_E2M1, F4_BNB, F4_NF4 = 4, 4 | (1 << 16), 4 | (2 << 16)
 F8_E4M3, F8_E5M2, F8_E8M0 = 8, 8 | (1 << 16), 8 | (3 << 16)
+DQ8_BNB = 8 | (4 << 16)
 BITS_TO_QTYPE = {8: S8, 7: S7, 6: S6, 5: S5, 4: S4, 3: S3, 2: S2, 1: S1}
 
 _p = C.c_void_p
@@ -74,6 +75,9 @@ class Oracle:
         L.orc_core_ktile.argtypes = [C.c_uint64]
         L.orc_core_ntile.argtypes = [C.c_uint64]
         L.orc_core_packrow.argtypes = [C.c_uint64]
+        L.orc_dq8_lut.argtypes = [_p]
+        L.orc_dq8_double_quant.argtypes = [_p, C.c_size_t, C.c_int, _p]
+        L.orc_dq8_get_fp_scale.argtypes = [_p, _p] + [C.c_int] * 4 + [_p] + [C.c_int] * 3
         L.orc_f8_to_f32.restype = C.c_float
         L.orc_f8_to_f32.argtypes = [C.c_uint32, C.c_int8]
         L.orc_quantize_f8_rowblock.argtypes = [_p, _p] + [C.c_int] * 4 + [_p, C.c_int, C.c_uint32, C.c_int]
