@@ -53,7 +53,7 @@ static int env_int(const char* name, int def) {
 // Tuning / A-B switches.  Read from the environment ONCE (at the first forward, or by nad_reload_knobs), never per
 // launch: the eager path an NE graph takes (one bestla_device_f32f32_forward per node) must not scan the environment.
 struct Knobs {
-  int gemv_wpc, gemv_grid, gemv_waves, gemv_pre, gemv_lean, gemv_ks, gemv_spw, gemv_disable, gemv_dual;
+  int gemv_wpc, gemv_grid, gemv_waves, gemv_pre, gemv_lean, gemv_ks, gemv_spw, gemv_disable, gemv_dual, gemv_nst;
   int compute_int8;
   int gemm2_disable, gemm4_all, gemm4_disable, ffn_f32, gemm_kernel, splitk_disable;
   int gemm3_stagger, gemm4_stagger2, gemm_fold, gemm4_fold_all, gemm4_fold, gemm4_ksw;
@@ -66,6 +66,7 @@ static Knobs read_knobs() {
   k.gemv_grid = env_int("NAD_GEMV_GRID", 0);    // tests / tuning: cap the workgroups of a stripe-stream launch
   k.gemv_waves = env_int("NAD_GEMV_WAVES", 0);  // tests / tuning: waves of a stripe-stream launch
   k.gemv_pre = std::min(3, std::max(1, env_int("NAD_GEMV_PRE", 1)));
+  k.gemv_nst = env_int("NAD_GEMV_NST", 0);  // register stages per wave: 0 auto; 1 or 2 (M = 1 kernel), 1 or 3 (M <= 16)
   k.gemv_lean = env_int("NAD_GEMV_LEAN", 1);
   k.gemv_dual = env_int("NAD_GEMV_DUAL", 1);  // decode QKV of two formats (int2 Q, K + int4 V) as one launch
   k.gemv_ks = env_int("NAD_GEMV_KS", 2);        // K-slice width (tiles) of the M = 1 kernel's single-op launches
@@ -486,6 +487,7 @@ static int prepare_gemv(GemvArgs& a, int& waves, int& grid, int& gpt_out, const 
   a.dq_mask = 0x000F000Fu;
   a.dq_magic = 0x64006400u;
   a.pre_stages = kn.gemv_pre;
+  a.m1_nst = kn.gemv_nst;
   a.u_q = a.units / grid;
   a.u_r = a.units % grid;
   a.lean = kn.gemv_lean;

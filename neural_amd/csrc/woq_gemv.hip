@@ -289,7 +289,9 @@ constexpr int gemv_max_threads() {
   return GPT == 1 ? 1024 : 512;
 }
 
-template <int BITS, int HILO, int GPT, bool ASYM>
+// NST: register stages in flight per wave (3, or 1 where no wave streams more than two stages: the ring's extra slots
+// would only carry dead out-of-range loads, see m1_body)
+template <int BITS, int HILO, int GPT, bool ASYM, int NST>
 __global__ __launch_bounds__(gemv_max_threads<GPT>()) void woq_gemv_kernel(GemvArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int KT = BITS == 4 ? 128 : (BITS == 2 ? 256 : 64);
@@ -349,12 +351,13 @@ __global__ __launch_bounds__(gemv_max_threads<GPT>()) void woq_gemv_kernel(GemvA
   lc.rs = lc.rt;
   lc.rz = lc.rt;
   if (!idle && nv > 0) cursor_stripe(a, lc, v0);
-  StageRegs<GPT> S0, S1, S2;
+  StageRegs<GPT> S[NST];
   // Only `pre` stages go out before the activations are published: issuing all three first stalled the wave on
   // memory back-pressure and delayed the (already landed) activation staging by ~1-2 us (phase trace).
-  load_stage<GPT, ASYM>(a, S0, lc, nv, nsl, wave, NW, v0, lane, vs);
-  if (a.pre_stages > 1) load_stage<GPT, ASYM>(a, S1, lc, nv, nsl, wave, NW, v0, lane, vs);
-  if (a.pre_stages > 2) load_stage<GPT, ASYM>(a, S2, lc, nv, nsl, wave, NW, v0, lane, vs);
+  load_stage<GPT, ASYM>(a, S[0], lc, nv, nsl, wave, NW, v0, lane, vs);
+#pragma unroll
+  for (int i = 1; i < NST; i++)
+    if (a.pre_stages > i) load_stage<GPT, ASYM>(a, S[i], lc, nv, nsl, wave, NW, v0, lane, vs);
   NAD_TRACE(4);
 
   // 2) publish the activations (waits only for the loads issued before the weights)
@@ -386,8 +389,9 @@ __global__ __launch_bounds__(gemv_max_threads<GPT>()) void woq_gemv_kernel(GemvA
     for (int i = threadIdx.x; i < (Kp >> 3); i += bd) zr[i] = make_uint4(0u, 0u, 0u, 0u);
   }
   __syncthreads();
-  if (a.pre_stages <= 1) load_stage<GPT, ASYM>(a, S1, lc, nv, nsl, wave, NW, v0, lane, vs);
-  if (a.pre_stages <= 2) load_stage<GPT, ASYM>(a, S2, lc, nv, nsl, wave, NW, v0, lane, vs);
+#pragma unroll
+  for (int i = 1; i < NST; i++)
+    if (a.pre_stages <= i) load_stage<GPT, ASYM>(a, S[i], lc, nv, nsl, wave, NW, v0, lane, vs);
   NAD_TRACE(1);
 
   // 3) the stream
@@ -470,12 +474,11 @@ __global__ __launch_bounds__(gemv_max_threads<GPT>()) void woq_gemv_kernel(GemvA
   };
 
   while (cj < nv) {
-    compute_stage(S0);
-    load_stage<GPT, ASYM>(a, S0, lc, nv, nsl, wave, NW, v0, lane, vs);
-    compute_stage(S1);
-    load_stage<GPT, ASYM>(a, S1, lc, nv, nsl, wave, NW, v0, lane, vs);
-    compute_stage(S2);
-    load_stage<GPT, ASYM>(a, S2, lc, nv, nsl, wave, NW, v0, lane, vs);
+#pragma unroll
+    for (int i = 0; i < NST; i++) {
+      compute_stage(S[i]);
+      load_stage<GPT, ASYM>(a, S[i], lc, nv, nsl, wave, NW, v0, lane, vs);
+    }
   }
   NAD_TRACE_MAX(2);
   __syncthreads();
@@ -583,7 +586,20 @@ static bool lean_ok(const GemvArgs& a, int bits, int waves) {
 // streams like one large launch instead of paying each launch's fixed chain.
 // The kernel body takes its workgroup index as an argument: woq_gemv_m1_dual_kernel runs two instantiations side by
 // side in one launch.
-template <int BITS, int GPT, int AT, bool ASYM, int KSN, int SPW, bool BATCH>
+// NST: register stages in flight per wave.  Every stage slot is loaded again right after it is computed -- with
+// out-of-range offsets once the wave's run is done -- so a ring deeper than the wave's own stages only adds dead
+// loads to the CU's memory queue, in front of the live ones.  Measured (profiles/r04_gemv_ring_depth_ab.txt,
+// r04_gemv_nst_ab.txt): one stage (1-2 KiB per wave) is fastest until a wave streams about seven, two beyond that
+// or for 1 KiB int2 stages from four (O 5.78 -> 4.83 us, down K = 11008 9.6 -> 7.8, gate/up 13.2 -> 12.2, QKV 8.6 ->
+// 8.1); deeper rings are slower everywhere except the batched launch's long streams (3: 1.43 vs 1.46 us per problem).
+#ifndef NAD_M1_BATCH_NST
+#define NAD_M1_BATCH_NST 3
+#endif
+#ifndef NAD_M1_DUAL_NST
+#define NAD_M1_DUAL_NST 2
+#endif
+
+template <int BITS, int GPT, int AT, bool ASYM, int KSN, int SPW, bool BATCH, int NST>
 __device__ __forceinline__ void m1_body(GemvArgs& a, int bid) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int KT = BITS == 4 ? 128 : 256, SPT = KT / 32, SPG = SPT / GPT;
@@ -637,8 +653,8 @@ __device__ __forceinline__ void m1_body(GemvArgs& a, int bid) {
   lc.rs = lc.rt;
   lc.rz = lc.rt;
   if (!idle && nv > 0) cursor_stripe(a, lc, v0);
-  StageRegs<GPT, KSN> S0, S1, S2;
-  load_stage<GPT, ASYM, KSN>(a, S0, lc, nv, nsl, wave, NW, v0, lane, vs);
+  StageRegs<GPT, KSN> S[NST];
+  load_stage<GPT, ASYM, KSN>(a, S[0], lc, nv, nsl, wave, NW, v0, lane, vs);
   NAD_TRACE(4);
 
   // 2) stage the slices into this wave's rows (LDS ops of one wave complete in order: no barrier)
@@ -665,8 +681,8 @@ __device__ __forceinline__ void m1_body(GemvArgs& a, int bid) {
     *reinterpret_cast<h8_t*>(row) = hi;
     if constexpr (HL) *reinterpret_cast<h8_t*>(row + RB) = lo;
   }
-  load_stage<GPT, ASYM, KSN>(a, S1, lc, nv, nsl, wave, NW, v0, lane, vs);
-  load_stage<GPT, ASYM, KSN>(a, S2, lc, nv, nsl, wave, NW, v0, lane, vs);
+#pragma unroll
+  for (int i = 1; i < NST; i++) load_stage<GPT, ASYM, KSN>(a, S[i], lc, nv, nsl, wave, NW, v0, lane, vs);
   NAD_TRACE(1);
 
   // 3) the stream: MFMA row 0 = hi (lane m 0), row 8 = lo (lane m 8), every other row reads the zero row
@@ -731,12 +747,11 @@ __device__ __forceinline__ void m1_body(GemvArgs& a, int bid) {
   };
 
   while (cj < nv) {
-    compute_stage(S0);
-    load_stage<GPT, ASYM, KSN>(a, S0, lc, nv, nsl, wave, NW, v0, lane, vs);
-    compute_stage(S1);
-    load_stage<GPT, ASYM, KSN>(a, S1, lc, nv, nsl, wave, NW, v0, lane, vs);
-    compute_stage(S2);
-    load_stage<GPT, ASYM, KSN>(a, S2, lc, nv, nsl, wave, NW, v0, lane, vs);
+#pragma unroll
+    for (int i = 0; i < NST; i++) {
+      compute_stage(S[i]);
+      load_stage<GPT, ASYM, KSN>(a, S[i], lc, nv, nsl, wave, NW, v0, lane, vs);
+    }
   }
   NAD_TRACE_MAX(2);
   __syncthreads();
@@ -813,9 +828,9 @@ __device__ __forceinline__ void m1_body(GemvArgs& a, int bid) {
   NAD_TRACE(3);
 }
 
-template <int BITS, int GPT, int AT, bool ASYM, int KSN, int SPW, bool BATCH>
+template <int BITS, int GPT, int AT, bool ASYM, int KSN, int SPW, bool BATCH, int NST>
 __global__ __launch_bounds__((m1_max_threads<GPT, KSN>())) void woq_gemv_m1_kernel(GemvArgs a) {
-  m1_body<BITS, GPT, AT, ASYM, KSN, SPW, BATCH>(a, int(blockIdx.x));
+  m1_body<BITS, GPT, AT, ASYM, KSN, SPW, BATCH, NST>(a, int(blockIdx.x));
 }
 
 // Two weight formats in one decode launch: workgroups [0, ga) run format 1's body over a, the rest format 2's over b
@@ -825,15 +840,15 @@ __global__ __launch_bounds__((m1_max_threads<GPT, KSN>())) void woq_gemv_m1_kern
 template <int B1, int G1, int K1, int B2, int G2, int K2, int AT>
 __global__ __launch_bounds__(1024) void woq_gemv_m1_dual_kernel(GemvArgs a, GemvArgs b, int ga) {
   if (int(blockIdx.x) < ga)
-    m1_body<B1, G1, AT, false, K1, 2, false>(a, int(blockIdx.x));
+    m1_body<B1, G1, AT, false, K1, 2, false, NAD_M1_DUAL_NST>(a, int(blockIdx.x));
   else
-    m1_body<B2, G2, AT, false, K2, 2, false>(b, int(blockIdx.x) - ga);
+    m1_body<B2, G2, AT, false, K2, 2, false, NAD_M1_DUAL_NST>(b, int(blockIdx.x) - ga);
 }
 
 // ------------------------------------------------------------------------------------------------ launcher
-template <int BITS, int HILO, int GPT, bool ASYM>
-static hipError_t gemv_launch4(const GemvArgs& a, dim3 g, dim3 b, size_t lds, hipStream_t st) {
-  auto k = woq_gemv_kernel<BITS, HILO, GPT, ASYM>;
+template <int BITS, int HILO, int GPT, bool ASYM, int NST>
+static hipError_t gemv_launch5(const GemvArgs& a, dim3 g, dim3 b, size_t lds, hipStream_t st) {
+  auto k = woq_gemv_kernel<BITS, HILO, GPT, ASYM, NST>;
   static bool attr_set = false;  // opt in to > 64 KiB of dynamic LDS once per instantiation
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -844,11 +859,38 @@ static hipError_t gemv_launch4(const GemvArgs& a, dim3 g, dim3 b, size_t lds, hi
   hipLaunchKernelGGL(k, g, b, lds, st, a);
   return hipGetLastError();
 }
+template <int BITS, int HILO, int GPT, bool ASYM>
+static hipError_t gemv_launch4(const GemvArgs& a, dim3 g, dim3 b, size_t lds, hipStream_t st) {
+  // stages of the busiest wave: its (stripe, KS-tile slice) pairs
+  const int nsl = (a.nt + KS - 1) / KS, waves = int(b.x / 64);
+  const int spw = (a.u_q + (a.u_r ? 1 : 0)) * (a.dual ? 2 : 1) * ((nsl + waves - 1) / waves);
+  const int nst = a.m1_nst == 1 ? 1 : (a.m1_nst == 3 ? 3 : (spw <= 2 ? 1 : 3));
+  return nst == 1 ? gemv_launch5<BITS, HILO, GPT, ASYM, 1>(a, g, b, lds, st)
+                  : gemv_launch5<BITS, HILO, GPT, ASYM, 3>(a, g, b, lds, st);
+}
 
+template <int BITS, int GPT, int AT, bool ASYM, int KSN, int SPW, int NST>
+static hipError_t gemv_m1_launch6(const GemvArgs& a, dim3 g, dim3 b, size_t lds, hipStream_t st) {
+  auto k = woq_gemv_m1_kernel<BITS, GPT, AT, ASYM, KSN, SPW, false, NST>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       160 * 1024);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(k, g, b, lds, st, a);
+  return hipGetLastError();
+}
+// register stages per wave of a single-problem launch: the most (stripe, K-slice) stages any wave streams
+static int m1_stages_per_wave(const GemvArgs& a, int ksn, int waves) {
+  const int nsl = (a.nt + ksn - 1) / ksn;
+  return (a.u_q + (a.u_r ? 1 : 0)) * (a.dual ? 2 : 1) * ((nsl + waves - 1) / waves);
+}
 template <int BITS, int GPT, int AT, bool ASYM, int KSN, int SPW>
 static hipError_t gemv_m1_launch5(const GemvArgs& a, dim3 g, dim3 b, size_t lds, hipStream_t st) {
   if (a.batch) {
-    auto kb = woq_gemv_m1_kernel<BITS, GPT, AT, ASYM, KSN, SPW, true>;
+    auto kb = woq_gemv_m1_kernel<BITS, GPT, AT, ASYM, KSN, SPW, true, NAD_M1_BATCH_NST>;
     static bool attr_b = false;
     if (!attr_b) {
       hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kb), hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -859,16 +901,10 @@ static hipError_t gemv_m1_launch5(const GemvArgs& a, dim3 g, dim3 b, size_t lds,
     hipLaunchKernelGGL(kb, g, b, lds, st, a);
     return hipGetLastError();
   }
-  auto k = woq_gemv_m1_kernel<BITS, GPT, AT, ASYM, KSN, SPW, false>;
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       160 * 1024);
-    if (e != hipSuccess) return e;
-    attr_set = true;
-  }
-  hipLaunchKernelGGL(k, g, b, lds, st, a);
-  return hipGetLastError();
+  const int spw = m1_stages_per_wave(a, KSN, int(b.x / 64));
+  const int nst = a.m1_nst == 1 || a.m1_nst == 2 ? a.m1_nst : (spw >= 7 || (KSN == 1 && spw >= 4) ? 2 : 1);
+  return nst == 1 ? gemv_m1_launch6<BITS, GPT, AT, ASYM, KSN, SPW, 1>(a, g, b, lds, st)
+                  : gemv_m1_launch6<BITS, GPT, AT, ASYM, KSN, SPW, 2>(a, g, b, lds, st);
 }
 template <int BITS, int GPT, int AT, bool ASYM>
 static hipError_t gemv_m1_launch4(const GemvArgs& a, dim3 g, dim3 b, size_t lds, hipStream_t st) {

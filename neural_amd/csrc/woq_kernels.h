@@ -136,6 +136,7 @@ struct GemvArgs {
   SkinnyWeight w[3];
   const GemvBatchEnt* batch;  // batched M = 1 launch (woq_gemv_m1_kernel<..., BATCH>): problem p = blockIdx / batch_wpp
   int batch_wpp;              //   reads its activations / weight / output from batch[p]; u_q / u_r split one problem
+  int m1_nst;                 // woq_gemv_m1_kernel: register stages in flight per wave (0 = by the stages per wave)
 };
 
 hipError_t launch_repack(const RepackArgs& a, hipStream_t stream);

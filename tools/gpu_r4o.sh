@@ -4,7 +4,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 for i in 1 2; do
-  for L in xa tree xb; do
+  for L in xc xd xe; do
     if [ $L = tree ]; then P=$PWD/neural_amd/libneural_amd.so; else P=$PWD/neural_amd/libneural_amd_$L.so; fi
     echo "#### round $i: $L"
     NAD_LIB_PATH=$P timeout -k 10 200 python tools/mistral_decode.py mistral 2>/dev/null | python -c "import json,sys; d=json.load(sys.stdin); print('mistral per-op tok/s', d['tokens_per_s'], d['per_op_per_shape_us'])" || exit 4
