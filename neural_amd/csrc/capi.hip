@@ -494,7 +494,7 @@ static int prepare_gemv(GemvArgs& a, int& waves, int& grid, int& gpt_out, const 
   // M = 1 single-op launches may stream 2-tile K-slices, one per wave (up to 16 waves); the chain keeps 4-tile ones
   if (single_op)
     gemv_lean_slices(a, w0.bits, &waves, kn.gemv_waves > 0 ? 4 : kn.gemv_ks);
-  if (kn.gemv_spw != 4) a.lean_spw = 2;  // A/B: long K back on the general stream kernel
+  if (kn.gemv_spw != 4 && a.lean_spw == 4) a.lean_spw = 2;  // A/B: long K back on the general stream kernel
   const size_t lds = gemv_lds_layout(a, w0.bits, waves, grid);
   if (lds > 160 * 1024) return 0;
   // buffer-resource offsets are 32-bit: every tile array, scale array and the activations must stay below 2 GiB

@@ -569,7 +569,9 @@ template <int GPT, int KSN>
 constexpr int m1_max_threads() {
   return GPT == 1 || KSN <= 2 ? 1024 : 512;
 }
-static int lean_spw(const GemvArgs& a) { return a.lean_spw == 4 ? 4 : 2; }
+// K-slices per wave staged: 1 for the narrow-slice launches (exactly one slice per wave: a second would only be a
+// dead out-of-range activation load in front of the weights), 4 for long K, else 2
+static int lean_spw(const GemvArgs& a) { return a.lean_spw == 4 ? 4 : (a.lean_spw == 1 ? 1 : 2); }
 
 static bool lean_ok(const GemvArgs& a, int bits, int waves) {
   int tpg = 0;
@@ -840,9 +842,9 @@ __global__ __launch_bounds__((m1_max_threads<GPT, KSN>())) void woq_gemv_m1_kern
 template <int B1, int G1, int K1, int B2, int G2, int K2, int AT>
 __global__ __launch_bounds__(1024) void woq_gemv_m1_dual_kernel(GemvArgs a, GemvArgs b, int ga) {
   if (int(blockIdx.x) < ga)
-    m1_body<B1, G1, AT, false, K1, 2, false, NAD_M1_DUAL_NST>(a, int(blockIdx.x));
+    m1_body<B1, G1, AT, false, K1, 1, false, NAD_M1_DUAL_NST>(a, int(blockIdx.x));
   else
-    m1_body<B2, G2, AT, false, K2, 2, false, NAD_M1_DUAL_NST>(b, int(blockIdx.x) - ga);
+    m1_body<B2, G2, AT, false, K2, 1, false, NAD_M1_DUAL_NST>(b, int(blockIdx.x) - ga);
 }
 
 // ------------------------------------------------------------------------------------------------ launcher
@@ -908,8 +910,8 @@ static hipError_t gemv_m1_launch5(const GemvArgs& a, dim3 g, dim3 b, size_t lds,
 }
 template <int BITS, int GPT, int AT, bool ASYM>
 static hipError_t gemv_m1_launch4(const GemvArgs& a, dim3 g, dim3 b, size_t lds, hipStream_t st) {
-  if (a.lean_ks == 1) return gemv_m1_launch5<BITS, GPT, AT, ASYM, 1, 2>(a, g, b, lds, st);
-  if (a.lean_ks == 2) return gemv_m1_launch5<BITS, GPT, AT, ASYM, 2, 2>(a, g, b, lds, st);
+  if (a.lean_ks == 1) return gemv_m1_launch5<BITS, GPT, AT, ASYM, 1, 1>(a, g, b, lds, st);
+  if (a.lean_ks == 2) return gemv_m1_launch5<BITS, GPT, AT, ASYM, 2, 1>(a, g, b, lds, st);
   return a.lean_spw == 4 ? gemv_m1_launch5<BITS, GPT, AT, ASYM, KS, 4>(a, g, b, lds, st)
                          : gemv_m1_launch5<BITS, GPT, AT, ASYM, KS, 2>(a, g, b, lds, st);
 }
@@ -1005,8 +1007,10 @@ void gemv_lean_slices(GemvArgs& a, int bits, int* waves, int ks_pref) {
   if (nsl > 16 || nsl <= *waves) return;  // narrow slices only where each wave gets one and there are more waves
   if (!lean_ok(a, bits, *waves)) return;  // the 4-tile launch would not take the M = 1 kernel either
   a.lean_ks = ks;
+  a.lean_spw = 1;  // one slice per wave
   if (!lean_ok(a, bits, nsl)) {
     a.lean_ks = KS;
+    a.lean_spw = 2;
     return;
   }
   *waves = nsl;

@@ -132,7 +132,7 @@ struct GemvArgs {
   int u_q, u_r;         // units per workgroup: u_q, one more for the first u_r workgroups (host-divided)
   int lean;             // M = 1 int4 single-group-per-tile launches may take woq_gemv_m1_kernel (NAD_GEMV_LEAN)
   int lean_ks;          // woq_gemv_m1_kernel: K tiles per K-slice (4, or 1 / 2 where that gives each of up to 16 waves one)
-  int lean_spw;         // woq_gemv_m1_kernel: K-slices per wave at most (2, or 4 for long K)
+  int lean_spw;         // woq_gemv_m1_kernel: K-slices per wave at most (2; 4 for long K; 1 for narrow slices)
   SkinnyWeight w[3];
   const GemvBatchEnt* batch;  // batched M = 1 launch (woq_gemv_m1_kernel<..., BATCH>): problem p = blockIdx / batch_wpp
   int batch_wpp;              //   reads its activations / weight / output from batch[p]; u_q / u_r split one problem
