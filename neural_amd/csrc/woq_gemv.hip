@@ -22,8 +22,8 @@
 //     ShuffleActivationKBlock, bestla_prologue_a.h:407-422, is applied while staging), and the workgroup's group scales
 //     loads of each stage are issued with it (one dword per tile: L2-merged 32 B rows);
 //   * wave w owns K-slices w, w + NW, ... (KS = 4 tiles) of every stripe in the run: a pipeline stage is one
-//     (stripe, slice) -- four loads at immediate offsets from one base -- and three stages are in flight per wave
-//     (register ring), the stage being computed the oldest;
+//     (stripe, slice) -- four loads at immediate offsets from one base -- and NST stages are in flight per wave
+//     (register ring, 1 or 3 chosen per launch: see NST below), the stage being computed the oldest;
 //   * int4 dequantization takes 1 shift + 4 v_and_or + 4 packed fp16 ops per 8 weights (the 0x6400 magic makes
 //     1024 + q and 1024 + 16 q exact fp16 without per-nibble shifts), then one
 //     v_mfma_f32_16x16x32_f16 with the activation rows in the A operand; the group scale multiplies an fp32 group
