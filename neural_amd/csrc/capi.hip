@@ -53,23 +53,20 @@ static int env_int(const char* name, int def) {
 // Tuning / A-B switches.  Read from the environment ONCE (at the first forward, or by nad_reload_knobs), never per
 // launch: the eager path an NE graph takes (one bestla_device_f32f32_forward per node) must not scan the environment.
 struct Knobs {
-  int gemv_wpc, gemv_grid, gemv_waves, gemv_pre, gemv_lean, gemv_ks, gemv_spw, gemv_disable, gemv_dual, gemv_nst;
+  int gemv_grid, gemv_waves, gemv_lean, gemv_spw, gemv_disable, gemv_dual, gemv_nst;
   int compute_int8;
   int gemm2_disable, gemm4_all, gemm4_disable, ffn_f32, gemm_kernel, splitk_disable;
-  int gemm3_stagger, gemm4_stagger2, gemm_fold, gemm4_fold_all, gemm4_fold, gemm4_ksw;
+  int gemm3_stagger, gemm4_fold_all, gemm4_fold, gemm4_ksw;
   int engine_loaders, engine_slots;
-  int host_cache_mb, tile_kmajor;
+  int host_cache_mb;
 };
 static Knobs read_knobs() {
   Knobs k{};
-  k.gemv_wpc = std::max(1, env_int("NAD_GEMV_WPC", 1));
   k.gemv_grid = env_int("NAD_GEMV_GRID", 0);    // tests / tuning: cap the workgroups of a stripe-stream launch
   k.gemv_waves = env_int("NAD_GEMV_WAVES", 0);  // tests / tuning: waves of a stripe-stream launch
-  k.gemv_pre = std::min(3, std::max(1, env_int("NAD_GEMV_PRE", 1)));
   k.gemv_nst = env_int("NAD_GEMV_NST", 0);  // register stages per wave: 0 auto; 1 or 2 (M = 1 kernel), 1 or 3 (M <= 16)
   k.gemv_lean = env_int("NAD_GEMV_LEAN", 1);
   k.gemv_dual = env_int("NAD_GEMV_DUAL", 1);  // decode QKV of two formats (int2 Q, K + int4 V) as one launch
-  k.gemv_ks = env_int("NAD_GEMV_KS", 2);        // K-slice width (tiles) of the M = 1 kernel's single-op launches
   k.gemv_spw = env_int("NAD_GEMV_SPW", 4);
   k.gemv_disable = env_int("NAD_GEMV_DISABLE", 0);
   k.compute_int8 = env_int("NAD_COMPUTE_INT8", 0);
@@ -77,18 +74,15 @@ static Knobs read_knobs() {
   k.gemm4_all = env_int("NAD_GEMM4_ALL", 0);
   k.gemm4_disable = env_int("NAD_GEMM4_DISABLE", 0);
   k.ffn_f32 = env_int("NAD_FFN_F32", 0);
-  k.gemm_kernel = env_int("NAD_GEMM_KERNEL", 3);
+  k.gemm_kernel = env_int("NAD_GEMM_KERNEL", 7);  // int4 g128 * 2^j prefill: 7 = gemm7, 3 = gemm3 (exact), 2 = gemm2
   k.splitk_disable = env_int("NAD_SPLITK_DISABLE", 0);
   k.gemm3_stagger = env_int("NAD_GEMM3_STAGGER", 1);  // measured +3-7 % (profiles/r02_gemm3_stagger.txt)
-  k.gemm4_stagger2 = env_int("NAD_GEMM4_STAGGER2", 0);
-  k.gemm_fold = env_int("NAD_GEMM_FOLD", 0);
   k.gemm4_fold_all = env_int("NAD_GEMM4_FOLD_ALL", 1);
   k.gemm4_fold = env_int("NAD_GEMM4_FOLD", 1);
   k.gemm4_ksw = env_int("NAD_GEMM4_KSW", 2);  // folded gemm4 launches with the waves split over K: 0 off, 1 on, 2 auto
   k.engine_loaders = env_int("NAD_ENGINE_LOADERS", 2);
   k.engine_slots = env_int("NAD_ENGINE_SLOTS", 16);
   k.host_cache_mb = env_int("NAD_HOST_CACHE_MB", 64 * 1024);
-  k.tile_kmajor = env_int("NAD_TILE_KMAJOR", 0);
   return k;
 }
 static Knobs g_knobs = read_knobs();  // library load
@@ -257,7 +251,7 @@ extern "C" int nad_device_load(const void* hostblob, void* devstor, void* device
   // per-channel (group >= K) is one group covering all tiles
   const int bs = b.blocksize >= b.k ? b.kpad : b.blocksize;
   const uint64_t need = layout_geometry(w, device_bits(b.qtype), b.n, b.k, bs, scale_code(b.scale_t), b.asym,
-                                        b.has_shuffle, knobs().tile_kmajor, b.has_reduce);
+                                        b.has_shuffle, false, b.has_reduce);
   if (need > capacity) {
     set_err("device buffer too small for the tile layout: need %llu bytes, have %zu (see nad_device_weight_size)",
             (unsigned long long)need, capacity);
@@ -479,21 +473,19 @@ static int prepare_gemv(GemvArgs& a, int& waves, int& grid, int& gpt_out, const 
   for (int i = nw; i < 3; i++) a.w[i] = a.w[0];
   a.units = a.dual ? ws[0]->ns : stripes;
   const Knobs& kn = knobs();
-  const int wpc = kn.gemv_wpc;
-  grid = std::max(1, std::min(a.units, device_cus() * wpc));
+  grid = std::max(1, std::min(a.units, device_cus()));
   if (kn.gemv_grid > 0) grid = std::min(a.units, kn.gemv_grid);  // tests / tuning
   waves = gemv_waves(w0.bits, w0.nt, w0.ng, w0.blocksize);
   if (kn.gemv_waves > 0) waves = std::min(gpt > 1 ? 8 : 16, kn.gemv_waves);
   a.dq_mask = 0x000F000Fu;
   a.dq_magic = 0x64006400u;
-  a.pre_stages = kn.gemv_pre;
   a.m1_nst = kn.gemv_nst;
   a.u_q = a.units / grid;
   a.u_r = a.units % grid;
   a.lean = kn.gemv_lean;
   // M = 1 single-op launches may stream 2-tile K-slices, one per wave (up to 16 waves); the chain keeps 4-tile ones
   if (single_op)
-    gemv_lean_slices(a, w0.bits, &waves, kn.gemv_waves > 0 ? 4 : kn.gemv_ks);
+    gemv_lean_slices(a, w0.bits, &waves, kn.gemv_waves > 0 ? 4 : 2);
   if (kn.gemv_spw != 4 && a.lean_spw == 4) a.lean_spw = 2;  // A/B: long K back on the general stream kernel
   const size_t lds = gemv_lds_layout(a, w0.bits, waves, grid);
   if (lds > 160 * 1024) return 0;
@@ -1041,9 +1033,8 @@ static int run_gemm(const void* act, int act_t, int lda, int m, int k, const Dev
   a.ld_aux = ld_aux;
   const Knobs& kn = knobs();
   a.stagger = kn.gemm3_stagger;  // measured +3-7 % (profiles/r02_gemm3_stagger.txt)
-  a.stagger2 = kn.gemm4_stagger2;
-  // scale folding measured 1-5 % SLOWER on gemm3 (profiles/r03_gemm3_fold.txt) and it rounds q * s to fp16: opt-in
-  a.fold = w.fold_ok && kn.gemm_fold ? 1 : 0;
+  // scale folding measured 1-5 % SLOWER on gemm3 (profiles/r03_gemm3_fold.txt): gemm3 keeps the exact fp32 group scale
+  a.fold = 0;
   a.w = view(w, out, ldo, bias, bias_ld);
   const int pg = pipelined_gemm(w, m);
   // gemm4 at groups of 32 / 64 scales the products into the result every 32 / 64 k (4 / 2 FMAs per MFMA): there the
@@ -1077,6 +1068,10 @@ static int run_gemm(const void* act, int act_t, int lda, int m, int k, const Dev
       pre = &own;
     }
     const bool g2 = pg == 3 && kn.gemm_kernel == 2;
+    // gemm7 (group scale folded, waves split over K) is the default for int4 groups of 128 * 2^j: +5-10 % over gemm3
+    // (profiles/r05_gemm7_*); a weight whose q * s leaves the fp16 normal range, or NAD_GEMM_KERNEL=3, runs gemm3
+    const bool g7 = pg == 3 && kn.gemm_kernel == 7 && gemm7_ok(w.bits, w.blocksize, w.fold_ok);
+    if (g7) a.fold = 1;
     int ktiles = w.nt;
     const int ks = !g2 ? splitk_plan(w, m, &ktiles) : 1;
     if (ks > 1 && kn.gemm4_ksw == 2) a.ksw = 0;  // auto KSW was measured on whole-K launches only
@@ -1090,13 +1085,14 @@ static int run_gemm(const void* act, int act_t, int lda, int m, int k, const Dev
       a.part = reinterpret_cast<float*>(base + a16);
     }
     const int tiles = ((m + 255) / 256) * ((w.n + 127) / 128);
-    if (planned(pg == 4 ? NAD_KERNEL_GEMM4 : (g2 ? NAD_KERNEL_GEMM2 : NAD_KERNEL_GEMM3),
+    if (planned(pg == 4 ? NAD_KERNEL_GEMM4 : (g2 ? NAD_KERNEL_GEMM2 : (g7 ? NAD_KERNEL_GEMM7 : NAD_KERNEL_GEMM3)),
                 tiles * ks, 512, ks, a.fold | (a.ksw << 1))) {
       if (ks > 1) planned(0, 0, 0, 1, 0, false);  // the split-K reduce
       return 0;
     }
     hipError_t e = pg == 4 ? launch_gemm4(a, w.bits, pre->p, pre->ld, st)
                    : g2    ? launch_gemm2(a, pre->p, pre->ld, st)
+                   : g7    ? launch_gemm7(a, pre->p, pre->ld, st)
                            : launch_gemm3(a, pre->p, pre->ld, st);
     if (e == hipSuccess && ks > 1) e = launch_splitk_reduce(a, st);
     if (e != hipSuccess) {
@@ -1185,7 +1181,7 @@ extern "C" int nad_plan_forward(int bits, int n, int k, int blocksize, int scale
   }
   if (blocksize <= 0) blocksize = k;
   DeviceWeight w{};
-  layout_geometry(w, bits, n, k, blocksize, scale_t, asym != 0, false, knobs().tile_kmajor);
+  layout_geometry(w, bits, n, k, blocksize, scale_t, asym != 0, false, false);
   layout_assign(w, reinterpret_cast<void*>(uintptr_t(1) << 41));  // never dereferenced on the host
   w.f4kind = -1;
   w.fold_ok = 1;
@@ -1830,7 +1826,7 @@ extern "C" int nad_synthetic_weight(void* devstor, void* deviceptr, size_t capac
     return -1;
   }
   DeviceWeight w{};
-  uint64_t need = layout_geometry(w, bits, n, k, blocksize, scale_t, asym != 0, false, knobs().tile_kmajor);
+  uint64_t need = layout_geometry(w, bits, n, k, blocksize, scale_t, asym != 0, false, false);
   if (need > capacity) {
     set_err("capacity %zu < needed %llu", capacity, (unsigned long long)need);
     return -1;

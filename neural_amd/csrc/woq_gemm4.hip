@@ -700,7 +700,7 @@ hipError_t launch_gemm4(const GemmArgs& a, int bits, const _Float16* A16, int ld
   GemmArgs ga = a;
   // the stagger measured +4-14 % for int4 / int8 and neutral to -5 % for int2 (profiles/r02_gemm4_stagger.txt); with
   // the scale fold int2 gains too, +5-11 % (profiles/r03_gemm4_int2_stagger_fold.txt): off only for unfolded int2
-  if (bits == 2 && !a.fold && !a.stagger2) ga.stagger = 0;
+  if (bits == 2 && !a.fold) ga.stagger = 0;
   auto go = [&](auto k, int lds) -> hipError_t {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
                                        lds);

@@ -1,0 +1,420 @@
+// woq_gemm7.hip -- the default prefill (M > 16) int4 WOQ GEMM for gfx950: groups of 128 * 2^j, the group scale folded
+// into the fp16 B operand.
+//
+// Replaces LauncherBase::gemm / run_block + WeightKBlockNInteger::getFpWeight + the AMX / AVX512 GEMM cores
+// (bestla/bestla/bestla_wrapper.h:481-542, bestla_prologue_b.h:732-838) for prefill-sized M.  q * s is rounded once to
+// fp16, as the reference's own AMX-BF16 / FP16 cores dequantize to a 16-bit float (DeviceWeight::fold_ok range-checks
+// every q * s at load; an unfoldable weight stays on gemm3, woq_gemm2.hip, which applies the scale exactly in fp32).
+//
+// Why it replaced gemm3 (profiles/r05_*): gemm3 runs 8 waves as 2 (M) x 4 (N) on a 256 x 128 tile, so
+// every B fragment is dequantized by both M-waves and each wave scales 64 group accumulators per group (2.65 non-MFMA
+// VALU per v_mfma_f32_16x16x32_f16).  gemm7 keeps the tile and gemm3's LDS-DMA plan (A three 64-deep half steps ahead
+// in a ring of four 32 KiB slots, the K tile of B + scale / zero-point dwords in a ring of three) but splits the waves
+// over K: wave (wn, wk) owns the 256 x 32 partial of stripes 2 wn, 2 wn + 1 over the 32-deep step wk of every half
+// step, so each B fragment is dequantized once per workgroup (1.44 VALU per MFMA measured incl. addressing) and the two
+// K halves meet once, in the epilogue.  DMAs are raw buffer loads with per-lane offsets fixed for the whole loop (no
+// 64-bit address arithmetic per piece); the MFMA accumulators live in VGPRs (-amdgpu-mfma-vgpr-form in the Makefile:
+// left to its heuristics hipcc split them over both register files and copied them every half step).
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <utility>
+
+#include "woq_device.h"
+#include "woq_kernels.h"
+
+namespace nad {
+namespace g7 {
+
+constexpr int BM = 256, BN = 128, KT = 128, ROWB = 128;  // ROWB: bytes of one A row per 64-deep half step
+constexpr int HBUF = BM * ROWB;                          // one half step of A: 32 KiB
+constexpr int NA = 4;                                    // A ring: three half steps in flight
+constexpr int NS = BN / 16;                              // stripes per tile
+constexpr int BTILES = NS * 1024, BSC = 512, BZP = 512;
+constexpr int BBUF = BTILES + BSC + BZP;                 // one K tile of B + scale and zero-point dwords
+constexpr int NBR = 3;                                   // B ring
+constexpr int LDS_BYTES = NA * HBUF + NBR * BBUF;        // 155 KiB
+constexpr int EPI_LD = 36;                               // epilogue transpose row stride (floats)
+static_assert(4 * BM * EPI_LD * 4 <= LDS_BYTES, "epilogue transpose must fit the rings");
+
+// LDS-DMA as raw buffer loads: 32-bit per-lane offsets fixed for the whole K loop, the moving part in an SGPR
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t brsrc(const void* p) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, -1, 0x00020000);
+}
+__device__ __forceinline__ void blds16(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, char* l) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)l, 16, voff, soff, 0, 0);
+}
+__device__ __forceinline__ void blds4(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, char* l) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)l, 4, voff, soff, 0, 0);
+}
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+// LDS reads in inline asm (hipcc would put vmcnt(0) in front of every LDS read it sees while an LDS-DMA is in flight);
+// results are consumed only after an explicit lgkmcnt wait that names them
+template <int OFF>
+__device__ __forceinline__ h8_t lds_b128(uint32_t addr) {
+  h8_t r;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "n"(OFF));
+  return r;
+}
+template <int OFF>
+__device__ __forceinline__ uint2 lds_b64(uint32_t addr) {
+  uint2 r;
+  asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "n"(OFF));
+  return r;
+}
+template <int OFF>
+__device__ __forceinline__ uint32_t lds_b32(uint32_t addr) {
+  uint32_t r;
+  asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "n"(OFF));
+  return r;
+}
+template <class T>
+__device__ __forceinline__ void tie(T& r) {
+  asm volatile("" : "+v"(r));
+}
+template <int N, class... T>
+__device__ __forceinline__ void wait_lgk(T&... regs) {
+  asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(N));
+  (tie(regs), ...);
+}
+__device__ __forceinline__ uint32_t lds_addr(const char* p) {
+  return uint32_t(reinterpret_cast<uintptr_t>((const __attribute__((address_space(3))) char*)p));
+}
+__device__ __forceinline__ uint32_t and_or(uint32_t x, uint32_t m, uint32_t c) {
+  uint32_t r;
+  asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "s"(m), "v"(c));
+  return r;
+}
+__device__ __forceinline__ h2_t splat(float v) {
+  h2_t r;
+  r[0] = _Float16(v);
+  r[1] = _Float16(v);
+  return r;
+}
+// one 32-deep step's B fragment: 8 nibbles -> fp16 (q - 8 - zp) * s, the product rounded once
+__device__ __forceinline__ h8_t dequant_fold(uint32_t w, uint32_t mag, h2_t s16, h2_t c0, h2_t c1, h2_t sc) {
+  const uint32_t w8 = w >> 8;
+  const h2_t p0 = (as_h2(and_or(w, 0x000F000Fu, mag)) + c0) * sc;
+  const h2_t p1 = __builtin_elementwise_fma(as_h2(and_or(w, 0x00F000F0u, mag)), s16, c1) * sc;
+  const h2_t p2 = (as_h2(and_or(w8, 0x000F000Fu, mag)) + c0) * sc;
+  const h2_t p3 = __builtin_elementwise_fma(as_h2(and_or(w8, 0x00F000F0u, mag)), s16, c1) * sc;
+  h8_t r;
+  r[0] = p0[0];
+  r[1] = p0[1];
+  r[2] = p1[0];
+  r[3] = p1[1];
+  r[4] = p2[0];
+  r[5] = p2[1];
+  r[6] = p3[0];
+  r[7] = p3[1];
+  return r;
+}
+
+#define NAD_SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
+
+// 8 waves (two per SIMD) split over K: wave (wn = w & 3, wk = w >> 2) owns the 256 x 32 partial of stripes 2 wn,
+// 2 wn + 1 over the 32-deep step wk of every 64-deep half step.  Its 16 A fragments per half step rotate in two halves
+// around the half step's barrier: fragments 0..7 of half step u + 1 are read into the registers fragments 0..7 of u
+// just left (their 16 MFMAs done, barrier of u + 1 passed), fragments 8..15 after the other 16 MFMAs.  A 4-wave form
+// (one wave per SIMD owning both K steps) measured 5-15 % slower than gemm3 (profiles/r05_gemm6_vs_gemm3_sweep.txt);
+// wider-N tiles (128 x 256, 128 x 512, 256 x 256: 8 waves as 1 or 2 (M) x 8 or 4 (N), each B fragment dequantized by
+// every M-wave) 3-35 % slower than this one (profiles/r05_gemm8_tile_shapes_sweep.txt).
+template <bool ASYM, int ST>
+__global__ __launch_bounds__(512, 1) void woq_gemm7_kernel(GemmArgs a, const _Float16* __restrict__ A16, int lda16) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));
+  const int wn = wave & 3, wk = wave >> 2;
+  const SkinnyWeight& W = a.w;
+  const int M = a.M, nt = W.nt, ng = W.ng, ns = W.ns;
+  const int tpg = W.bs / KT;
+  const int tsh = __builtin_ctz(unsigned(tpg));
+
+  const int nbm = (M + BM - 1) / BM;
+  const int nbn = (ns + NS - 1) / NS;
+  const int ntile = nbm * nbn;
+  const int nsplit = a.ksplit > 1 ? a.ksplit : 1;
+  const int nwg = ntile * nsplit;
+  int bid = blockIdx.x;
+  {
+    const int q = nwg / 8, r = nwg % 8, x = bid % 8, o = bid / 8;
+    bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + o;
+  }
+  const int ks = bid / ntile;
+  bid -= ks * ntile;
+  const int kt0 = nsplit > 1 ? ks * a.ktiles : 0;
+  const int ntl = nsplit > 1 ? min(a.ktiles, nt - kt0) : nt;
+  const int nh = 2 * ntl;
+  const int bm = bid / nbn, bn = bid % nbn;
+  const int m0 = bm * BM;
+  const int nl = lane & 15, kq = lane >> 4;
+
+  // A piece p = 4 wave + i: rows 8p .. 8p + 7
+  uint32_t aoff[4];
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const int row = (wave * 4 + i) * 8 + (lane >> 3);
+    const int grow = min(m0 + row, M - 1);
+    aoff[i] = uint32_t(grow) * uint32_t(lda16) * 2u + uint32_t(((lane & 7) ^ ((row >> 1) & 7)) * 16);
+  }
+  const auto ra = brsrc(reinterpret_cast<const char*>(A16) + size_t(kt0) * KT * 2);
+  const auto rb = brsrc(static_cast<const char*>(W.tiles) + size_t(kt0) * 1024);
+  const uint32_t boffd = (uint32_t(min(bn * NS + wave, ns - 1)) * nt * 64 + lane) * 16;
+  const int sstripe = min(bn * NS + (wave & 1) * 4 + (lane >> 4), ns - 1);
+  const uint32_t srow0 = uint32_t(sstripe) * ng * 16 + nl + uint32_t(kt0 >> tsh) * 16;
+  constexpr int st = ST;
+  const auto rs = brsrc(W.scales);
+  const auto rz = brsrc(W.zps);
+  const uint32_t svo = st == kScaleF32 ? srow0 * 4 : (srow0 >> 1) * 4, zvo = (srow0 >> 2) * 4;
+
+  auto issue = [&](auto Hc, int u) {
+    constexpr int H = decltype(Hc)::value;
+    const int ua = u + 3;
+    char* ab = smem + (ua & 3) * HBUF;
+  #pragma unroll
+    for (int i = 0; i < 4; i++) blds16(ra, aoff[i], uint32_t(ua) * ROWB, ab + (wave * 4 + i) * 1024);
+    if constexpr (H == 1) {
+      const int t = ua >> 1;
+      char* bb = smem + NA * HBUF + (t % NBR) * BBUF;
+      blds16(rb, boffd, uint32_t(t) * 1024, bb + wave * 1024);
+      const uint32_t g = uint32_t(t >> tsh) * 16;
+      blds4(rs, svo, st == kScaleF32 ? g * 4 : g * 2, bb + BTILES + (wave & 1) * 256);
+      if constexpr (ASYM) blds4(rz, zvo, g, bb + BTILES + BSC + (wave & 1) * 256);
+    }
+  };
+  constexpr int NBW = ASYM ? 3 : 2;
+
+  const uint32_t mag = 0x64006400u;
+  const h2_t s16 = splat(1.f / 16.f);
+  const h2_t zc0 = splat(-(1024.f + 8.f)), zc1 = splat(-(64.f + 8.f));
+  const uint32_t roff = uint32_t(nl * ROWB + (((wk * 4 + kq) ^ ((nl >> 1) & 7)) * 16));
+  const int boff = (wn * 2) * 1024 + lane * 16 + wk * 4;
+  const int soff = BTILES + ((wn * 2) * 16 + nl) * 4;
+  const int zoff = BTILES + BSC + ((wn * 2) * 16 + nl) * 4;
+  const int ssh = st == kScaleF32 ? 0 : (nl & 1) * 16;
+  const int zsh = (nl & 3) * 8;
+  auto scale_h2 = [&](uint32_t x) {
+    const uint32_t h = (x >> ssh) & 0xFFFFu;
+    if (st == kScaleF16) return as_h2(h | (h << 16));
+    const float f = st == kScaleF32 ? __uint_as_float(x)
+                                    : (st == kScaleBF16 ? __uint_as_float(h << 16) : f16_bits_to_f32(uint16_t(h)));
+    return splat(f);
+  };
+
+  f4_t acc[16][2];
+#pragma unroll
+  for (int i = 0; i < 16; i++)
+#pragma unroll
+    for (int j = 0; j < 2; j++) acc[i][j] = f4_t{0.f, 0.f, 0.f, 0.f};
+
+  h8_t af[16];
+  h8_t bf[2];
+  h2_t sc[2];
+  h2_t c0[2] = {zc0, zc0}, c1[2] = {zc1, zc1};
+  uint32_t bw0 = 0, bw1 = 0, sw0 = 0, sw1 = 0, zw0 = 0, zw1 = 0;
+
+  // B words (+ scale / zp at a tile start) and A fragments 0..7 of half step u
+  auto read_lo = [&](auto Hc, int u) {
+    constexpr int H = decltype(Hc)::value;
+    const int t = u >> 1;
+    const uint32_t bl = lds_addr(smem + NA * HBUF + (t % NBR) * BBUF);
+    bw0 = lds_b32<H * 8>(bl + boff);
+    bw1 = lds_b32<1024 + H * 8>(bl + boff);
+    if constexpr (H == 0) {
+      sw0 = lds_b32<0>(bl + soff);
+      sw1 = lds_b32<64>(bl + soff);
+      if constexpr (ASYM) {
+        zw0 = lds_b32<0>(bl + zoff);
+        zw1 = lds_b32<64>(bl + zoff);
+      }
+    }
+    const uint32_t al = lds_addr(smem + (u & 3) * HBUF) + roff;
+    af[0] = lds_b128<0 * 16 * ROWB>(al);
+    af[1] = lds_b128<1 * 16 * ROWB>(al);
+    af[2] = lds_b128<2 * 16 * ROWB>(al);
+    af[3] = lds_b128<3 * 16 * ROWB>(al);
+    af[4] = lds_b128<4 * 16 * ROWB>(al);
+    af[5] = lds_b128<5 * 16 * ROWB>(al);
+    af[6] = lds_b128<6 * 16 * ROWB>(al);
+    af[7] = lds_b128<7 * 16 * ROWB>(al);
+  };
+  auto read_hi = [&](int u) {
+    const uint32_t al = lds_addr(smem + (u & 3) * HBUF) + roff;
+    af[8] = lds_b128<8 * 16 * ROWB>(al);
+    af[9] = lds_b128<9 * 16 * ROWB>(al);
+    af[10] = lds_b128<10 * 16 * ROWB>(al);
+    af[11] = lds_b128<11 * 16 * ROWB>(al);
+    af[12] = lds_b128<12 * 16 * ROWB>(al);
+    af[13] = lds_b128<13 * 16 * ROWB>(al);
+    af[14] = lds_b128<14 * 16 * ROWB>(al);
+    af[15] = lds_b128<15 * 16 * ROWB>(al);
+  };
+  auto dequant = [&](auto Hc) {
+    constexpr int H = decltype(Hc)::value;
+    if constexpr (H == 0) {
+      sc[0] = scale_h2(sw0);
+      sc[1] = scale_h2(sw1);
+      if constexpr (ASYM) {
+        const float z0 = float(int(int8_t((zw0 >> zsh) & 0xFFu))), z1 = float(int(int8_t((zw1 >> zsh) & 0xFFu)));
+        c0[0] = zc0 - splat(z0);
+        c1[0] = zc1 - splat(z0);
+        c0[1] = zc0 - splat(z1);
+        c1[1] = zc1 - splat(z1);
+      }
+    }
+    bf[0] = dequant_fold(bw0, mag, s16, c0[0], c1[0], sc[0]);
+    bf[1] = dequant_fold(bw1, mag, s16, c0[1], c1[1], sc[1]);
+  };
+
+  // prologue
+  issue(std::integral_constant<int, 1>{}, -3);
+  issue(std::integral_constant<int, 0>{}, -2);
+  if (nh > 2) {
+    issue(std::integral_constant<int, 1>{}, -1);
+    wait_vm<8 + NBW>();
+  } else {
+    wait_vm<4>();
+  }
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  read_lo(std::integral_constant<int, 0>{}, 0);
+  read_hi(0);
+  wait_lgk<8>(bw0, bw1, sw0, sw1, zw0, zw1);
+  dequant(std::integral_constant<int, 0>{});
+
+  // half step u: entering, B of u is dequantized, A fragments 0..7 of u were issued before 8..15 (both may be in
+  // flight).  The barrier of buffer u + 1 sits between the two MFMA halves.  (Waves 4-7 with that barrier after both
+  // halves instead -- a stagger, MI355X_MICROARCH item 9 -- measured 6-15 % slower: profiles/r05_gemm7_stagger_ab.txt.)
+  auto half = [&](auto Hc, auto IssC, auto WvC, int u) {
+    constexpr int H = decltype(Hc)::value;
+    constexpr bool ISS = decltype(IssC)::value;
+    constexpr int WV = decltype(WvC)::value;
+    constexpr bool MORE = WV >= 0;
+    auto sync = [&]() {
+      wait_vm<WV>();
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      NAD_SCHED_FENCE();
+      read_lo(std::integral_constant<int, 1 - H>{}, u + 1);
+    };
+    NAD_SCHED_FENCE();
+    wait_lgk<8>(af[0], af[1], af[2], af[3], af[4], af[5], af[6], af[7]);
+    NAD_SCHED_FENCE();
+    if constexpr (ISS) issue(Hc, u);
+#pragma unroll
+    for (int i = 0; i < 8; i++)
+#pragma unroll
+      for (int j = 0; j < 2; j++) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
+    NAD_SCHED_FENCE();
+    wait_lgk<0>(af[8], af[9], af[10], af[11], af[12], af[13], af[14], af[15]);
+    if constexpr (MORE) sync();
+    NAD_SCHED_FENCE();
+#pragma unroll
+    for (int i = 8; i < 16; i++) {
+      acc[i][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bf[0], acc[i][0], 0, 0, 0);
+      acc[i][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bf[1], acc[i][1], 0, 0, 0);
+    }
+    NAD_SCHED_FENCE();
+    if constexpr (MORE) {
+      read_hi(u + 1);
+      wait_lgk<8>(bw0, bw1, sw0, sw1, zw0, zw1);  // B words (issued before the 16 A fragments) have landed
+      dequant(std::integral_constant<int, 1 - H>{});
+    }
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using Yes = std::true_type;
+  using No = std::false_type;
+  using Steady = std::integral_constant<int, 8 + NBW>;
+  for (int u = 0; u + 4 < nh; u += 2) {
+    half(I0{}, Yes{}, Steady{}, u);
+    half(I1{}, Yes{}, Steady{}, u + 1);
+  }
+  if (nh >= 4) {
+    half(I0{}, Yes{}, Steady{}, nh - 4);
+    half(I1{}, No{}, std::integral_constant<int, 4>{}, nh - 3);
+  }
+  half(I0{}, No{}, std::integral_constant<int, 0>{}, nh - 2);
+  half(I1{}, No{}, std::integral_constant<int, -1>{}, nh - 1);
+
+  // epilogue: the two K halves of each 256 x 32 tile meet in LDS (gemm5's order: (k-half 0) + (k-half 1) for every
+  // output).  Wave (wn, wk) finishes rows wk * 128 .. + 127.
+  NAD_SCHED_FENCE();
+  __syncthreads();
+  float* const tw = reinterpret_cast<float*>(smem) + wave * (128 * EPI_LD);
+  float* const tp = reinterpret_cast<float*>(smem) + (wave ^ 4) * (128 * EPI_LD);
+#pragma unroll
+  for (int i = 0; i < 8; i++)
+#pragma unroll
+    for (int j = 0; j < 2; j++)
+#pragma unroll
+      for (int rr = 0; rr < 4; rr++) {
+        const float v = wk ? acc[i][j][rr] : acc[8 + i][j][rr];  // the partner's rows
+        tp[(i * 16 + kq * 4 + rr) * EPI_LD + j * 16 + nl] = v;
+      }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 8; i++)
+#pragma unroll
+    for (int j = 0; j < 2; j++)
+#pragma unroll
+      for (int rr = 0; rr < 4; rr++) {
+        float* p = tw + (i * 16 + kq * 4 + rr) * EPI_LD + j * 16 + nl;
+        const float mine = wk ? acc[8 + i][j][rr] : acc[i][j][rr];
+        *p = wk == 0 ? mine + *p : *p + mine;
+      }
+  const int col0 = (bn * NS + wn * 2) * 16;
+#pragma unroll 4
+  for (int q = 0; q < 16; q++) {
+    const int c = q * 64 + lane;
+    const int rl = c >> 3, c4 = c & 7;
+    const int row = m0 + wk * 128 + rl;
+    const int n0 = col0 + c4 * 4;
+    const float4 t = *reinterpret_cast<const float4*>(tw + rl * EPI_LD + c4 * 4);
+    if (row >= M || n0 >= W.n) continue;
+    if (nsplit > 1) {
+      *reinterpret_cast<float4*>(a.part + (size_t(ks) * M + row) * a.ldp + n0) = t;
+      continue;
+    }
+    float v[4] = {t.x, t.y, t.z, t.w};
+    gemm_epilogue4(a, row, n0, v);
+  }
+}
+
+}  // namespace g7
+
+bool gemm7_ok(int bits, int blocksize, int fold_ok) {
+  const int tpg = blocksize / g7::KT;
+  return bits == 4 && fold_ok && blocksize % g7::KT == 0 && (tpg & (tpg - 1)) == 0;
+}
+
+hipError_t launch_gemm7(const GemmArgs& a, const _Float16* A16, int lda16, hipStream_t st) {
+  const int nbm = (a.M + g7::BM - 1) / g7::BM, nbn = (a.w.ns + g7::NS - 1) / g7::NS;
+  auto go = [&](auto k, bool& done) -> hipError_t {
+    if (!done) {
+      hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                         g7::LDS_BYTES);
+      if (e != hipSuccess) return e;
+      done = true;
+    }
+    hipLaunchKernelGGL(k, dim3(nbm * nbn * (a.ksplit > 1 ? a.ksplit : 1)), dim3(512), g7::LDS_BYTES, st, a, A16,
+                       lda16);
+    return hipGetLastError();
+  };
+  static bool attr[2][3] = {};
+  const bool asym = a.w.zps != nullptr;
+  bool& d = attr[asym][a.scale_t];
+  switch (a.scale_t) {
+    case kScaleF32:
+      return asym ? go(g7::woq_gemm7_kernel<true, kScaleF32>, d) : go(g7::woq_gemm7_kernel<false, kScaleF32>, d);
+    case kScaleBF16:
+      return asym ? go(g7::woq_gemm7_kernel<true, kScaleBF16>, d) : go(g7::woq_gemm7_kernel<false, kScaleBF16>, d);
+    default:
+      return asym ? go(g7::woq_gemm7_kernel<true, kScaleF16>, d) : go(g7::woq_gemm7_kernel<false, kScaleF16>, d);
+  }
+}
+
+}  // namespace nad

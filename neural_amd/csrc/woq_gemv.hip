@@ -352,12 +352,10 @@ __global__ __launch_bounds__(gemv_max_threads<GPT>()) void woq_gemv_kernel(GemvA
   lc.rz = lc.rt;
   if (!idle && nv > 0) cursor_stripe(a, lc, v0);
   StageRegs<GPT> S[NST];
-  // Only `pre` stages go out before the activations are published: issuing all three first stalled the wave on
-  // memory back-pressure and delayed the (already landed) activation staging by ~1-2 us (phase trace).
+  // Only the first stage goes out before the activations are published: issuing all three first stalled the wave on
+  // memory back-pressure and delayed the (already landed) activation staging by ~1-2 us (phase trace; the pre-issue
+  // A/B of round 4, profiles/r04_gemv_preissue_ab.txt).
   load_stage<GPT, ASYM>(a, S[0], lc, nv, nsl, wave, NW, v0, lane, vs);
-#pragma unroll
-  for (int i = 1; i < NST; i++)
-    if (a.pre_stages > i) load_stage<GPT, ASYM>(a, S[i], lc, nv, nsl, wave, NW, v0, lane, vs);
   NAD_TRACE(4);
 
   // 2) publish the activations (waits only for the loads issued before the weights)
@@ -390,8 +388,7 @@ __global__ __launch_bounds__(gemv_max_threads<GPT>()) void woq_gemv_kernel(GemvA
   }
   __syncthreads();
 #pragma unroll
-  for (int i = 1; i < NST; i++)
-    if (a.pre_stages <= i) load_stage<GPT, ASYM>(a, S[i], lc, nv, nsl, wave, NW, v0, lane, vs);
+  for (int i = 1; i < NST; i++) load_stage<GPT, ASYM>(a, S[i], lc, nv, nsl, wave, NW, v0, lane, vs);
   NAD_TRACE(1);
 
   // 3) the stream

@@ -72,7 +72,6 @@ struct GemmArgs {
   const float* aux;
   int ld_aux;
   int stagger;          // gemm3: waves 4-7 half a step behind waves 0-3 (NAD_GEMM3_STAGGER)
-  int stagger2;         // gemm4: the stagger for int2 too (NAD_GEMM4_STAGGER2, A/B)
   int fold;             // gemm3 / gemm4: group scale folded into the fp16 B fragment (DeviceWeight::fold_ok)
   int ksw;              // gemm4 (folded): waves split over K, 1 (M) x 4 (N) x 2 (K) -- each B fragment dequantized once
   // split-K (gemm3 / gemm4 when the output tiles alone cannot fill the chip): the K tiles are cut into ksplit runs of
@@ -124,7 +123,6 @@ struct GemvArgs {
   int part_off;         // LDS byte offset of the partial-sum slots
   uint32_t dq_mask;     // 0x000F000F and 0x64006400: int4 dequant constants, passed in so they stay in registers
   uint32_t dq_magic;
-  int pre_stages;       // woq_gemv_kernel: weight stages issued before the activation staging (1..3)
   int nwa;              // woq_chain: waves that own K slices in this op (the single-op launch's wave count)
   int norm;             // woq_chain: RMS-normalise each activation row while staging (x / rms(x) * norm_w)
   float norm_eps;
@@ -198,6 +196,10 @@ hipError_t launch_q8_0_quant(const Q80Args& a, int act_t, hipStream_t stream);
 hipError_t launch_quant_u8(const QuantU8Args& a, int act_t, hipStream_t stream);
 hipError_t launch_i8(const I8Args& a, int bits, hipStream_t stream);
 hipError_t launch_gemm4(const GemmArgs& a, int bits, const _Float16* A16, int lda16, hipStream_t stream);
+// prefill GEMM v7 (woq_gemm7.hip, the default for int4 groups of 128 * 2^j): gemm3's contract (256 x 128 tiles,
+// split-K partials, fp16 A padded to the 128-deep tile) with the group scale folded (needs DeviceWeight::fold_ok)
+bool gemm7_ok(int bits, int blocksize, int fold_ok);
+hipError_t launch_gemm7(const GemmArgs& a, const _Float16* A16, int lda16, hipStream_t stream);
 // sum a.ksplit partials of a split-K gemm3 / gemm4 launch in run order and apply a.epi into a.w.out (woq_gemm2.hip)
 hipError_t launch_splitk_reduce(const GemmArgs& a, hipStream_t stream);
 hipError_t launch_cvt_act(const void* A, int act_t, int lda, int M, int K, int Kp, const int32_t* shuffle,

@@ -212,21 +212,21 @@ def test_host_cache_key_is_constant_time_at_lm_head_shape():
 
 def test_plan_forward_kernel_choice():
     """nad_plan_forward (the host side of nad_device_forward with every launch recorded, no GPU): the decode shapes take
-    the M = 1 / stripe-stream GEMVs, prefill takes gemm3 (int4 g128) or gemm4 (g32 / g64 with the scale folded, int2,
-    int8), and few output tiles split K."""
+    the M = 1 / stripe-stream GEMVs, prefill takes gemm7 (int4 g128, the scale folded; gemm3 under NAD_GEMM_KERNEL=3)
+    or gemm4 (g32 / g64 with the scale folded, int2, int8), and few output tiles split K."""
     p = bestla.plan_forward
     assert p(4, 4096, 4096, 128, m=1)["kernel"] == "woq_gemv_m1_kernel"
     assert p(2, 14336, 4096, 64, m=1)["kernel"] == "woq_gemv_m1_kernel"
     assert p(4, 4096, 4096, 128, m=8)["kernel"] == "woq_gemv_kernel"
     r = p(4, 4096, 4096, 128, m=2048)
-    assert (r["kernel"], r["fold"], r["ksplit"]) == ("woq_gemm3_kernel", False, 1)
+    assert (r["kernel"], r["fold"], r["ksplit"]) == ("woq_gemm7_kernel", True, 1)
     assert r["launches"] == 2                       # fp32 activations: one fp16 conversion pass, then the GEMM
     assert p(4, 4096, 4096, 128, m=2048, act="fp16")["launches"] == 1
     for bits, g in ((4, 32), (4, 64), (2, 64)):
         r = p(bits, 4096, 4096, g, m=2048)
         assert (r["kernel"], r["fold"]) == ("woq_gemm4_kernel", True), (bits, g, r)
     r = p(4, 4096, 4096, 128, m=64)
-    assert r["kernel"] == "woq_gemm3_kernel" and r["ksplit"] > 1 and r["launches"] == 3   # + the split-K reduce
+    assert r["kernel"] == "woq_gemm7_kernel" and r["ksplit"] > 1 and r["launches"] == 3   # + the split-K reduce
     # int8 / int2 at g128 fold too (NAD_GEMM4_FOLD_ALL default since round 4)
     assert p(8, 4096, 4096, 128, m=2048)["fold"] and p(2, 4096, 4096, 128, m=2048)["fold"]
 
@@ -241,7 +241,7 @@ def test_plan_gemm4_waves_split_over_k():
     assert p(4, 4096, 11008, 32, m=2048)["ksw"]             # down: K = 11008
     r = p(4, 4096, 11008, 32, m=64)
     assert r["ksplit"] > 1 and not r["ksw"]                 # split-K launches keep the M-split waves
-    assert not p(4, 4096, 4096, 128, m=4096)["ksw"]         # int4 g128: gemm3
+    assert not p(4, 4096, 4096, 128, m=4096)["ksw"]         # int4 g128: gemm7 (its own K split, not reported as ksw)
 
 
 def test_host_cost_per_forward_under_3us():

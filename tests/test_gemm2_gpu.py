@@ -38,7 +38,7 @@ GEMM2_CASES = [
 ]
 
 
-@pytest.mark.parametrize("kernel", ["3", "2"])
+@pytest.mark.parametrize("kernel", ["7", "3", "2"])
 @pytest.mark.parametrize("cfg", GEMM2_CASES)
 @pytest.mark.parametrize("act", ["fp32", "fp16", "bf16"])
 def test_gemm_parity(oracle, knob, kernel, cfg, act):

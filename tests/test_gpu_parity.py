@@ -322,7 +322,8 @@ M1_SLICES = [
 @pytest.mark.parametrize("grid", [None, "1", "7"])
 def test_gemv_m1_two_tile_slices(oracle, knob, cfg, grid):
     """M = 1 with 2-tile K-slices (one per wave, up to 16 waves) against the oracle,
-    and within 1e-6 of the 4-tile-slice launch (NAD_GEMV_KS=4; only the partial-sum order differs).  Forced grids make
+    and within 1e-6 of a 4-tile-slice launch (a forced wave count takes 4-tile slices; only the partial-sum order
+    differs).  Forced grids make
     workgroups stream many stripes through the 3-stage ring."""
     n, k, bs, qt, st, asym, adt = cfg
     if grid:
@@ -333,7 +334,7 @@ def test_gemv_m1_two_tile_slices(oracle, knob, cfg, grid):
     xa = torch.from_numpy(A).cuda().to(dict(f32=torch.float32, f16=torch.float16, bf16=torch.bfloat16)[adt])
     ref = oracle.forward(xa.float().cpu().numpy(), blob, n, k)
     y2 = w.forward(xa).cpu().numpy()
-    knob("NAD_GEMV_KS", "4")
+    knob("NAD_GEMV_WAVES", "16")
     y4 = w.forward(xa).cpu().numpy()
     assert _rel_err(y2, ref) <= TOL_DECODE
     assert _rel_err(y2, y4) <= 1e-6

@@ -40,7 +40,8 @@ def main():
                 x = (torch.rand((m, k), device=dev) - 0.5).to(dt)
                 out = torch.empty((m, n), device=dev)
                 s = torch.cuda.current_stream()
-                for kern in args.kernels.split(","):
+                for kname in args.kernels.split(","):
+                    kern = kname
                     os.environ["NAD_GEMM_KERNEL"] = kern[0]
                     os.environ["NAD_GEMM2_DISABLE"] = "1" if kern[0] == "0" else "0"
                     os.environ["NAD_GEMM4_DISABLE"] = "1" if kern[0] != "4" else "0"
@@ -63,7 +64,7 @@ def main():
                     torch.cuda.synchronize()
                     us = e0.elapsed_time(e1) * 1e3 / args.reps
                     tf = 2.0 * m * n * k / us / 1e6
-                    print(f"{name:8s} b{args.bits} g{args.group}{'a' if args.asym else 's'} N={n:5d} K={k:5d} M={m:5d} {act} gemm{kern}: {us:9.1f} us  {tf:7.1f} TFLOP/s",
+                    print(f"{name:8s} b{args.bits} g{args.group}{'a' if args.asym else 's'} N={n:5d} K={k:5d} M={m:5d} {act} gemm{kname}: {us:9.1f} us  {tf:7.1f} TFLOP/s",
                           flush=True)
                 del x, out
         del w
