@@ -176,66 +176,6 @@ class Runner:
         st.lm_head.forward(self.x, out=self.logits)
 
 
-class ChainRunner:
-    """The decode step on the weight-stream engine (nad_chain_*, woq_chain.hip) with its real data dependencies:
-    x -> RMSNorm -> QKV -> (attention) -> O + x -> RMSNorm -> gate/up SiLU*mul -> down + h -> next layer ...
-    -> RMSNorm -> lm_head.  cut=True (the headline): one launch per segment between attention nodes -- the form the
-    reference graph dispatches (ne_layers.c:11915-12028; llama.cpp op order) -- i.e. [QKV_0], then per layer
-    [O, gate/up, down, next QKV] (the last: [O, gate/up, down, lm_head]): 33 launches per Llama-2-7B token.  The
-    attention between launches is outside the WOQ path; its output here is V, which is exact for a
-    single-token context (softmax over one key).  cut=False: the whole token as ONE launch (printed beside it)."""
-
-    def __init__(self, stack, device, cut=True):
-        import torch
-        from neural_amd import bestla
-        H, L = stack.cfg["hidden"], len(stack.layers)
-        f = dict(dtype=torch.float32, device=device)
-        g = torch.Generator(device="cpu").manual_seed(7)
-        self.xs = [((torch.rand((1, H), generator=g) - 0.5)).to(device)] + [torch.empty((1, H), **f) for _ in range(L)]
-        self.q = [torch.empty((1, stack.nq), **f) for _ in range(L)]
-        self.k = [torch.empty((1, stack.nkv), **f) for _ in range(L)]
-        self.v = [torch.empty((1, stack.nkv), **f) for _ in range(L)]
-        self.h = [torch.empty((1, H), **f) for _ in range(L)]
-        self.t = [torch.empty((1, stack.nf), **f) for _ in range(L)]
-        self.logits = torch.empty((1, stack.nv), **f)
-        # O's input: V itself when it is the whole attention output (kv == hidden: softmax over one key returns V);
-        # with grouped KV heads (Mistral) the attention output is hidden-wide -- an external vector here, exactly as the
-        # per-op Runner's (the attention node between launches writes it; its work is outside the WOQ path)
-        self.o_in = self.v if stack.nkv == stack.nq else [((torch.rand((1, stack.nq), generator=g) - 0.5)).to(device)
-                                                          for _ in range(L)]
-        bits = stack.cfg["bits"]
-        ops, bounds = [], [0]
-        for li, Lw in enumerate(stack.layers):
-            x = self.xs[li]
-            if bits["v"] == bits["q"]:
-                ops.append(dict(kind=bestla.CHAIN_QKV, w=[Lw["wq"], Lw["wk"], Lw["wv"]], act=x,
-                                out=[self.q[li], self.k[li], self.v[li]], norm=True))
-            else:  # Mistral's policy: {Q, K} int2 in one op, V int4 in its own (one format per op)
-                ops.append(dict(kind=bestla.CHAIN_QKV, w=[Lw["wq"], Lw["wk"]], act=x, out=[self.q[li], self.k[li]],
-                                norm=True))
-                ops.append(dict(kind=bestla.CHAIN_LINEAR, w=[Lw["wv"]], act=x, out=[self.v[li]], norm=True))
-            bounds.append(len(ops))   # a cut after each layer's QKV: attention follows
-            ops.append(dict(kind=bestla.CHAIN_LINEAR, w=[Lw["wo"]], act=self.o_in[li], out=[self.h[li]],
-                            epi=bestla.EPI_RES_ADD, res=x))
-            ops.append(dict(kind=bestla.CHAIN_GATE_UP, w=[Lw["w1"], Lw["w3"]], act=self.h[li], out=[self.t[li]],
-                            norm=True))
-            ops.append(dict(kind=bestla.CHAIN_LINEAR, w=[Lw["w2"]], act=self.t[li], out=[self.xs[li + 1]],
-                            epi=bestla.EPI_RES_ADD, res=self.h[li]))
-        ops.append(dict(kind=bestla.CHAIN_LINEAR, w=[stack.lm_head], act=self.xs[L], out=[self.logits], norm=True))
-        # [QKV_0], then per layer [O, gate/up, down, next QKV] and [O, gate/up, down, lm_head] last
-        bounds = bounds + [len(ops)] if cut else [0, len(ops)]
-        self.chains = [bestla.Chain(ops[a:b], 1) for a, b in zip(bounds, bounds[1:])]
-        self.n_ops = len(ops)
-        self.n_launches = len(self.chains)
-
-    def step(self, stream=None):
-        for c in self.chains:
-            c.run(stream=stream)
-
-    def status(self):
-        return max(c.status() for c in self.chains)
-
-
 def graph_time(fn, reps, torch):
     """Average device time of fn() (one decode token), captured once in a HIP graph and replayed `reps` times; HIP
     events recorded on the stream the kernels run on."""
@@ -280,7 +220,7 @@ def graph_times(fn, reps, torch):
     return out
 
 
-SYN_MS = [1, 2, 4, 8, 16, 64, 256, 1024, 2048, 4096]
+SYN_MS = [1, 2, 4, 8, 16, 17, 32, 64, 128, 256, 512, 1024, 2048, 4096]
 
 
 def synthetic_sweep(torch, copies=128, reps=5, batch=64):
@@ -290,8 +230,7 @@ def synthetic_sweep(torch, copies=128, reps=5, batch=64):
     of back-to-back launches replayed `reps` times -- min and median per launch.  Bytes per section 8(d) with 2-byte
     activations (in and out); M <= 64 is priced against HBM, larger M against the dense fp16 MFMA peak.
     Config 2 (M = 1) is also run as BTLAGemmBatchDriver-style batches (bestla_gemm.cpp:508-624): `batch` independent
-    problems in ONE launch -- of the batched M = 1 GEMV (nad_batch_*, the reported form) and of the weight-stream
-    engine (no hand-off between them); fp32 activations."""
+    problems in ONE launch of the batched M = 1 GEMV (nad_batch_*); fp32 activations."""
     from neural_amd import bestla
     K = N = 4096
     g = 128
@@ -318,24 +257,10 @@ def synthetic_sweep(torch, copies=128, reps=5, batch=64):
                      "frac": round(gbps / HBM_PEAK_GBPS if hbm else tfl / MFMA_F16_PEAK_TFLOPS, 4),
                      "kernel": bestla.plan_forward(4, N, K, g, "fp16", False, m, "fp16")["kernel"]})
         del x, y
-    # config 2 as batches of independent problems, one engine launch per batch, two batches per replay
     sets = copies // batch
     xs = [(torch.rand((1, K), generator=gen) - 0.5).cuda() for _ in range(batch)]
     ys = [torch.empty((1, N), dtype=torch.float32, device="cuda") for _ in range(batch)]
-    chains = [bestla.Chain([dict(kind=bestla.CHAIN_LINEAR, w=[ws[j * batch + i]], act=xs[i], out=[ys[i]])
-                            for i in range(batch)], 1) for j in range(sets)]
-
-    def fe(st):
-        for c in chains:
-            c.run(stream=st)
-    per = sorted(t / (sets * batch) for t in graph_times(fe, reps, torch))
-    assert max(c.status() for c in chains) == 0
     byts = wb + (K + N) * 4
-    t_med = per[len(per) // 2]
-    batched = {"problems_per_launch": batch, "launches_per_replay": sets, "us_per_problem_min": round(per[0] * 1e6, 3),
-               "us_per_problem_median": round(t_med * 1e6, 3), "GBps": round(byts / t_med / 1e9, 1),
-               "frac": round(byts / t_med / 1e9 / HBM_PEAK_GBPS, 4), "bytes_per_problem": byts,
-               "kernel": "woq_engine_kernel (independent ops: no hand-off)", "act": "fp32"}
     # config 2 as BTLAGemmBatchDriver batches on the M = 1 GEMV (nad_batch_*): one launch per batch, workgroups dealt
     # out problem by problem (the batch's problems stream like one large launch)
     batches = [bestla.Batch([(ws[j * batch + i], xs[i], ys[i]) for i in range(batch)]) for j in range(sets)]
@@ -350,7 +275,7 @@ def synthetic_sweep(torch, copies=128, reps=5, batch=64):
                     "GBps": round(byts / t_med / 1e9, 1), "frac": round(byts / t_med / 1e9 / HBM_PEAK_GBPS, 4),
                     "bytes_per_problem": byts, "kernel": "woq_gemv_m1_kernel (batched: nad_batch_run)", "act": "fp32"}
     single = next(r for r in rows if r["m"] == 1)
-    del chains, batches, ws
+    del batches, ws
     torch.cuda.empty_cache()
     return {"config": "K=N=4096 int4 g128 sym, fp16 scales, fp16 activations; 128 weight copies (1.1 GB) rotated "
                       "(cold); graph-replayed back-to-back launches, min / median over replays",
@@ -358,7 +283,6 @@ def synthetic_sweep(torch, copies=128, reps=5, batch=64):
             "per_m": rows,
             "config2_m1_single_launches": {k: single[k] for k in ("us_min", "us_median", "GBps", "frac", "kernel")},
             "config2_m1_batched": batched_gemv,
-            "config2_m1_batched_engine": batched,
             "m4096_mfma_frac": next(r for r in rows if r["m"] == 4096)["frac"]}
 
 
@@ -403,23 +327,10 @@ def decode_workload(cfg, torch, reps=20, prefill=True, prefill_steps=5):
     L1 = st.launches(1)
     byts = sum(b * c for _, b, _, c in L1)
     del run
-    # the same token on the weight-stream engine: cut at the attention nodes (the headline form) and as one launch
-    eng = {}
-    for cut in (True, False):
-        cr = ChainRunner(st, "cuda", cut=cut)
-        te = graph_time(lambda s: cr.step(stream=s), reps, torch)
-        assert cr.status() == 0, "decode engine hand-off timed out"
-        eng["cut" if cut else "whole"] = (te, cr.n_launches)
-        del cr
-    te, nl = eng["cut"]
-    best = min(t, te)
-    path = "per-op launches" if t <= te else f"weight-stream engine ({nl} launches per token)"
-    out = {"tokens_per_s": round(1.0 / best, 2), "ms_per_token": round(best * 1e3, 4), "bytes_per_token": int(byts),
-           "roofline": {"bound": "hbm", "achieved": round(byts / best / 1e9, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                        "frac": round(byts / best / 1e9 / HBM_PEAK_GBPS, 4)},
-           "decode_path": path, "per_op_tokens_per_s": round(1.0 / t, 2),
-           "engine_cut_tokens_per_s": round(1.0 / te, 2), "engine_whole_token_tokens_per_s": round(1.0 / eng["whole"][0], 2),
-           "launches_per_token": nl if t > te else sum(c for *_, c in L1),
+    out = {"tokens_per_s": round(1.0 / t, 2), "ms_per_token": round(t * 1e3, 4), "bytes_per_token": int(byts),
+           "roofline": {"bound": "hbm", "achieved": round(byts / t / 1e9, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                        "frac": round(byts / t / 1e9 / HBM_PEAK_GBPS, 4)},
+           "decode_path": "per-op launches", "launches_per_token": sum(c for *_, c in L1),
            "per_op_per_shape_us": {k: round(v * 1e6, 3) for k, v in time_launches(st, 1, reps, torch).items()}}
     if prefill:
         pre = Runner(st, 2048, None, "cuda")
@@ -537,7 +448,6 @@ def main(argv=None):
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the secondary BASELINE workloads")
     ap.add_argument("--no-synthetic", action="store_true", help="skip the synthetic K=N=4096 M sweep")
-    ap.add_argument("--per-op", action="store_true", help="headline from per-op launches instead of the decode chain")
     ap.add_argument("--dry-run", action="store_true", help="print the rank layout and exit (no GPU)")
     args = ap.parse_args(argv)
 
@@ -600,32 +510,17 @@ def main(argv=None):
             dt = pc.max_over_ranks(dt)
         return dt
 
-    # ---- decode (headline): M = 1.  One GPU: the faster of the weight-stream engine cut at the attention nodes (33
-    # launches per token) and per-op launches; the whole token as one engine launch is measured beside it.
-    # Tensor parallel: per-op launches + C-ABI all-reduce after O and down.
+    # ---- decode (headline): M = 1, one launch per WOQ matmul (graph-replayed; the eager drop-in path beside it).
+    # Tensor parallel: the same launches on this rank's shards + C-ABI all-reduce after O and down.  (The round-3/4
+    # weight-stream engine -- one persistent launch per segment -- stayed slower than these launches and left the
+    # product in round 5: tools/engine/)
     use_graph = not args.no_graph
-    chain = None
-    chain_tok_s = uncut_tok_s = None
-    if world == 1 and not args.per_op:
-        chain = ChainRunner(stack, "cuda", cut=True)
-        dt_chain = timed(chain, args.steps, args.warmup, use_graph)
-        assert chain.status() == 0, "decode engine hand-off timed out"
-        chain_tok_s = args.steps / dt_chain
-        uncut = ChainRunner(stack, "cuda", cut=False)
-        dt_uncut = timed(uncut, args.steps, args.warmup, use_graph)
-        assert uncut.status() == 0, "decode engine hand-off timed out"
-        uncut_tok_s = args.steps / dt_uncut
-        del uncut
     dec = Runner(stack, 1, pc, "cuda")
-    dt_op = timed(dec, args.steps, args.warmup, use_graph)
-    per_op_tok_s = args.steps / dt_op
+    dt = timed(dec, args.steps, args.warmup, use_graph)
+    tok_s = args.steps / dt
     # the eager drop-in path (what ne_graph_compute does: one host call per WOQ node, no graph)
     dt_eager = timed(dec, args.steps, args.warmup, False)
     eager_tok_s = args.steps / dt_eager
-    if chain is not None and dt_chain >= dt_op:
-        chain = None
-    dt = dt_chain if chain is not None else dt_op
-    tok_s = args.steps / dt
 
     # ---- prefill: M = 2048 tokens
     pre = Runner(stack, 2048, pc, "cuda")
@@ -642,20 +537,14 @@ def main(argv=None):
     tot_bytes = sum(b * c for _, b, _, c in L1)
     per_op_time = sum(per[n] * c for n, _, _, c in L1)
     n_per_op_launches = sum(c for *_, c in L1)
-    if chain is not None:
-        token_s = graph_time(lambda s: chain.step(stream=s), 20, torch)
-        kernel, bytes_per_launch, launch_s = (f"woq_engine_kernel (weight-stream engine, {chain.n_launches} launches per "
-                                              f"token cut at the attention nodes)", tot_bytes / chain.n_launches,
-                                              token_s / chain.n_launches)
-    else:
-        kernel, bytes_per_launch, launch_s = "woq_gemv_m1_kernel (decode GEMV, one launch per matmul)", \
-            tot_bytes / n_per_op_launches, per_op_time / n_per_op_launches
+    kernel, bytes_per_launch, launch_s = "woq_gemv_m1_kernel (decode GEMV, one launch per matmul)", \
+        tot_bytes / n_per_op_launches, per_op_time / n_per_op_launches
     achieved = bytes_per_launch / launch_s / 1e9
     traffic = None
     pmc = latest_pmc()
     if os.path.exists(pmc):
         try:
-            rec = json.load(open(pmc))["woq_engine_kernel" if chain is not None else "woq_gemv_m1_kernel"]
+            rec = json.load(open(pmc))["woq_gemv_m1_kernel"]
             traffic = int(rec["traffic_over_algorithmic"] * bytes_per_launch)
         except Exception:
             traffic = None
@@ -690,15 +579,10 @@ def main(argv=None):
             "vs_baseline": None,
             "dtype": "f16",
             "data": "synthetic: random int4 codes + fp16 group scales U[0.001,0.01] in Llama-2-7B shapes (no checkpoint)",
-            "config": {"workload": "Llama-2-7B int4-g128 sym decode step, M=1: 32 x [RMSNorm, fused QKV, O + residual, "
-                                   "RMSNorm, gate/up + SiLU*mul, down + residual] + RMSNorm + lm_head, fp32 activations; "
-                                   "one engine launch per segment between attention nodes (attention output = V, exact "
-                                   "for a single-token context)" if chain is not None else
-                                   "Llama-2-7B int4-g128 sym decode linear stack, M=1 (32 x [QKV, O, gate/up+SiLU*mul, "
+            "config": {"workload": "Llama-2-7B int4-g128 sym decode linear stack, M=1 (32 x [QKV, O, gate/up+SiLU*mul, "
                                    "down] + lm_head), fp32 activations", "group_size": LLAMA["group"], "batch": 1,
                        "tp": world, "parallelism": f"tp{world}", "hip_graph": use_graph,
-                       "decode_path": f"weight-stream engine ({chain.n_launches} launches per token)"
-                       if chain is not None else "per-op launches"},
+                       "decode_path": "per-op launches"},
             "prefill_tflops": round(prefill_tflops, 2),
             "prefill_ms_per_2048_tokens": round(pdt / args.prefill_steps * 1e3, 3),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
@@ -706,10 +590,8 @@ def main(argv=None):
                          "traffic_source": os.path.basename(pmc) if traffic is not None else None,
                          "kernel": kernel, "bytes_per_launch": int(bytes_per_launch),
                          "avg_launch_us": round(launch_s * 1e6, 3)},
-            "decode_engine_cut_tokens_per_s": None if chain_tok_s is None else round(chain_tok_s, 2),
-            "decode_engine_whole_token_tokens_per_s": None if uncut_tok_s is None else round(uncut_tok_s, 2),
             "decode_eager_tokens_per_s": round(eager_tok_s, 2),
-            "per_op_launches": {"tokens_per_s": round(per_op_tok_s, 2), "eager_tokens_per_s": round(eager_tok_s, 2),
+            "per_op_launches": {"tokens_per_s": round(tok_s, 2), "eager_tokens_per_s": round(eager_tok_s, 2),
                                 "gemv_achieved_GBps": round(tot_bytes / per_op_time / 1e9, 1),
                                 "per_shape_us": {k: round(v * 1e6, 3) for k, v in per.items()}},
             "prefill_roofline": {"bound": "mfma", "achieved": round(prefill_tflops / world, 2),

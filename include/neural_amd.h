@@ -262,41 +262,6 @@ int nad_quant_q8_0(const void* act, int act_dtype, int m, int k, int lda, void* 
 /* host convenience: (re)pack one blob into fp32 dequantized [K][N] from the device tile layout (round-trip check) */
 int nad_device_unpack_fp32(const void* devstor, float* host_out, void* queue);
 
-/* ===== decode chain: one decode step's WOQ matmuls as ONE persistent launch.  Replaces the sequence of device WOQ
- * nodes of a decode graph (ne_layers.c:7219-7316, fused QKV/FFN nodes ne_layers.c:8050-8170) -- a dependency-aware
- * BTLAGemmBatchDriver (bestla_gemm.cpp:508-624).  Ops run in order; op i may read any output of ops < i (written and
- * read through the device-wide hand-off inside the launch).  Constraints (nad_chain_create fails with a message
- * otherwise): m = 1; fp32 activations; stripe-major int4 weights with groups of 64 or >= 128, or int2 with groups of
- * 64, 128 or >= 256, at most two formats per chain and only the pairs (int2 g64, int4 g64) / (int2 g128, int4 g128);
- * one symmetry; no act-order shuffle; fp arithmetic (not int8 compute); LINEAR epilogues NONE / RES_ADD, GATE_UP
- * SILU_MUL / GELU_MUL; no op may write a vector (out or aux) that an earlier op of the chain reads from outside the
- * chain (act, res, norm_w) or that it reads itself. */
-#define NAD_CHAIN_LINEAR 0   /* out[0] = epi(act . w[0]^T)                         (bestla_device_f32f32_forward) */
-#define NAD_CHAIN_QKV 1      /* out[j] = act . w[j]^T, j = 0..2                    (bestla_fusion_QKV_f32f32_forward) */
-#define NAD_CHAIN_GATE_UP 2  /* out[0] = silu/gelu(act . w[0]^T) * (act . w[1]^T) (ip_fusion_ffn.cpp:407-433); aux = act1 */
-typedef struct nad_chain_op {
-  int kind;
-  const void* w[3];        /* device weight descriptors (devstor) */
-  const void* act;         /* [m][lda] activations, act_dtype NAD_ACT_* */
-  int act_dtype, lda;
-  float* out[3];
-  int ldo[3];
-  int epi;                 /* NAD_EPI_*: LINEAR NONE / RES_ADD; GATE_UP SILU_MUL / GELU_MUL */
-  const float* bias;
-  int bias_ld;
-  const float* res;        /* NAD_EPI_RES_ADD residual [m][ld_res] (may be an earlier op's output) */
-  int ld_res;
-  float* aux;
-  int ld_aux;
-  int norm;                /* RMS-normalise the activation rows while staging: x / sqrt(mean(x^2) + eps) * norm_w */
-  float norm_eps;
-  const float* norm_w;     /* [K] or NULL (= 1) */
-} nad_chain_op;
-void* nad_chain_create(const nad_chain_op* ops, int n_ops, int m);
-int nad_chain_run(void* chain, void* queue);  /* asynchronous on queue; graph-capturable */
-int nad_chain_status(void* chain);            /* 0, or the first give-up code of a bounded wait (synchronous) */
-void nad_chain_destroy(void* chain);
-
 /* ===== batched independent decode problems: BTLAGemmBatchDriver (bestla_gemm.cpp:508-624) for device tensors.  n
  * problems y_i = x_i W_i (M = 1, fp32 x_i [K] 16-B aligned, fp32 y_i [N]) whose weights share N, K and format (int4 /
  * int2, no act-order, fp arithmetic, a geometry the M = 1 GEMV takes) run as ONE launch: workgroups are dealt out

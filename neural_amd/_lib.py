@@ -92,10 +92,6 @@ SIGNATURES = {
     "nad_q4_0_device_size": (_sz, [_i, _i]),
     "nad_q4_0_device_load": (_i, [_p, _i, _i, _p, _p, _sz, _p]),
     "nad_quant_q8_0": (_i, [_p, _i, _i, _i, _i, _p, _p]),
-    "nad_chain_create": (_p, [_p, _i, _i]),
-    "nad_chain_run": (_i, [_p, _p]),
-    "nad_chain_status": (_i, [_p]),
-    "nad_chain_destroy": (None, [_p]),
     "nad_batch_create": (_p, [_p, _i]),
     "nad_batch_run": (_i, [_p, _p]),
     "nad_batch_destroy": (None, [_p]),
@@ -132,13 +128,6 @@ SIGNATURES = {
     "nad_bind_workspace": (_i, [_p, _p, _sz]),
     "nad_device_workspace_size": (_sz, [_i, _i]),
 }
-
-
-class ChainOp(C.Structure):
-    """Mirror of include/neural_amd.h's nad_chain_op."""
-    _fields_ = [("kind", _i), ("w", _p * 3), ("act", _p), ("act_dtype", _i), ("lda", _i), ("out", _p * 3),
-                ("ldo", _i * 3), ("epi", _i), ("bias", _p), ("bias_ld", _i), ("res", _p), ("ld_res", _i),
-                ("aux", _p), ("ld_aux", _i), ("norm", _i), ("norm_eps", C.c_float), ("norm_w", _p)]
 
 
 class NativeLibraryMissing(RuntimeError):

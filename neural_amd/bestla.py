@@ -410,9 +410,6 @@ def ffn_forward(x, w1, w2, w3, act="silu", tmp1=None, tmp2=None, out=None, strea
     return out
 
 
-CHAIN_LINEAR, CHAIN_QKV, CHAIN_GATE_UP = 0, 1, 2
-
-
 class Batch:
     """Independent M = 1 problems y_i = x_i W_i of one weight shape as ONE launch (include/neural_amd.h nad_batch_*:
     BTLAGemmBatchDriver, bestla_gemm.cpp:508-624, for device tensors).  problems: list of (DeviceWeight, x [K] or [1][K]
@@ -443,68 +440,6 @@ class Batch:
         if h:
             try:
                 lib().nad_batch_destroy(h)
-            except Exception:
-                pass
-            self.handle = None
-
-
-class Chain:
-    """A decode step's WOQ matmuls as ONE persistent launch (include/neural_amd.h nad_chain_*).
-
-    ops: list of dicts with keys kind (CHAIN_*), w (list of DeviceWeight), act (cuda tensor [m][k]), out (list of
-    cuda fp32 tensors), and optionally epi, res (tensor), aux (tensor), bias (tensor), norm (bool), norm_eps,
-    norm_w (tensor).  The tensors are bound at creation (their addresses are baked into the device op table): keep them
-    alive and reuse them across run() calls."""
-
-    def __init__(self, ops, m):
-        from . import _lib
-        torch = _torch()
-        arr = (_lib.ChainOp * len(ops))()
-        self._keep = []
-        for i, o in enumerate(ops):
-            c = arr[i]
-            c.kind = o["kind"]
-            for j, w in enumerate(o["w"]):
-                c.w[j] = C.cast(w.desc, C.c_void_p)
-                self._keep.append(w)
-            x = o["act"]
-            c.act = x.data_ptr()
-            c.act_dtype = _act_code(x)
-            c.lda = x.stride(0)
-            for j, t in enumerate(o["out"]):
-                c.out[j] = t.data_ptr()
-                c.ldo[j] = t.stride(0)
-            c.epi = o.get("epi", EPI_SILU_MUL if o["kind"] == CHAIN_GATE_UP else EPI_NONE)
-            for key, ld in (("bias", "bias_ld"), ("res", "ld_res"), ("aux", "ld_aux")):
-                t = o.get(key)
-                if t is not None:
-                    setattr(c, key, t.data_ptr())
-                    setattr(c, ld, t.stride(0) if t.dim() > 1 else 0)
-            c.norm = 1 if o.get("norm") else 0
-            c.norm_eps = float(o.get("norm_eps", 1e-5))
-            if o.get("norm_w") is not None:
-                c.norm_w = o["norm_w"].data_ptr()
-            self._keep.extend(t for t in [x, *o["out"], o.get("res"), o.get("aux"), o.get("bias"), o.get("norm_w")]
-                              if t is not None)
-        self._ops = arr
-        self.n_ops = len(ops)
-        h = lib().nad_chain_create(C.cast(arr, C.c_void_p), len(ops), m)
-        if not h:
-            raise RuntimeError(f"nad_chain_create failed: {last_error()}")
-        self.handle = h
-        self.torch = torch
-
-    def run(self, stream=None):
-        check(lib().nad_chain_run(self.handle, _stream(stream)), "nad_chain_run")
-
-    def status(self):
-        return lib().nad_chain_status(self.handle)
-
-    def __del__(self):
-        h = getattr(self, "handle", None)
-        if h:
-            try:
-                lib().nad_chain_destroy(h)
             except Exception:
                 pass
             self.handle = None

@@ -16,7 +16,6 @@
 
 #include "../../include/neural_amd.h"
 #include "btla_format.h"
-#include "woq_chain.h"
 #include "woq_kernels.h"
 
 using namespace nad;
@@ -55,9 +54,8 @@ static int env_int(const char* name, int def) {
 struct Knobs {
   int gemv_grid, gemv_waves, gemv_lean, gemv_spw, gemv_disable, gemv_dual, gemv_nst;
   int compute_int8;
-  int gemm2_disable, gemm4_all, gemm4_disable, ffn_f32, gemm_kernel, splitk_disable;
+  int gemm2_disable, gemm4_all, gemm4_disable, ffn_f32, gemm_kernel, gemm7_bm, splitk_disable;
   int gemm3_stagger, gemm4_fold_all, gemm4_fold, gemm4_ksw;
-  int engine_loaders, engine_slots;
   int host_cache_mb;
 };
 static Knobs read_knobs() {
@@ -75,13 +73,12 @@ static Knobs read_knobs() {
   k.gemm4_disable = env_int("NAD_GEMM4_DISABLE", 0);
   k.ffn_f32 = env_int("NAD_FFN_F32", 0);
   k.gemm_kernel = env_int("NAD_GEMM_KERNEL", 7);  // int4 g128 * 2^j prefill: 7 = gemm7, 3 = gemm3 (exact), 2 = gemm2
+  k.gemm7_bm = env_int("NAD_GEMM7_BM", 0);        // gemm7 tile height (A/B): 0 auto, 32, 64, 128, 256
   k.splitk_disable = env_int("NAD_SPLITK_DISABLE", 0);
   k.gemm3_stagger = env_int("NAD_GEMM3_STAGGER", 1);  // measured +3-7 % (profiles/r02_gemm3_stagger.txt)
   k.gemm4_fold_all = env_int("NAD_GEMM4_FOLD_ALL", 1);
   k.gemm4_fold = env_int("NAD_GEMM4_FOLD", 1);
   k.gemm4_ksw = env_int("NAD_GEMM4_KSW", 2);  // folded gemm4 launches with the waves split over K: 0 off, 1 on, 2 auto
-  k.engine_loaders = env_int("NAD_ENGINE_LOADERS", 2);
-  k.engine_slots = env_int("NAD_ENGINE_SLOTS", 16);
   k.host_cache_mb = env_int("NAD_HOST_CACHE_MB", 64 * 1024);
   return k;
 }
@@ -483,7 +480,7 @@ static int prepare_gemv(GemvArgs& a, int& waves, int& grid, int& gpt_out, const 
   a.u_q = a.units / grid;
   a.u_r = a.units % grid;
   a.lean = kn.gemv_lean;
-  // M = 1 single-op launches may stream 2-tile K-slices, one per wave (up to 16 waves); the chain keeps 4-tile ones
+  // M = 1 single-op launches may stream 2-tile K-slices, one per wave (up to 16 waves); fused launches keep 4-tile ones
   if (single_op)
     gemv_lean_slices(a, w0.bits, &waves, kn.gemv_waves > 0 ? 4 : 2);
   if (kn.gemv_spw != 4 && a.lean_spw == 4) a.lean_spw = 2;  // A/B: long K back on the general stream kernel
@@ -987,10 +984,10 @@ static int prepare_a16(A16& r, const void* act, int act_t, int lda, int m, int k
 // Split-K plan of a pipelined GEMM whose 256 x 128 output tiles alone leave most CUs idle (M up to a few hundred, or
 // narrow N): runs of whole groups, at least two K tiles each, at most one workgroup per CU in total.  Returns the run
 // count (1 = no split) and the K tiles per run.
-static int splitk_plan(const DeviceWeight& w, int m, int* ktiles) {
+static int splitk_plan(const DeviceWeight& w, int m, int* ktiles, int bm = 256) {
   *ktiles = w.nt;
   if (knobs().splitk_disable) return 1;
-  const int tiles = ((m + 255) / 256) * ((w.ns + 7) / 8);
+  const int tiles = ((m + bm - 1) / bm) * ((w.ns + 7) / 8);
   if (tiles > 128) return 1;
   const int tpg = std::max(1, w.blocksize / k_tile(w));
   const int unit = tpg >= 2 ? tpg : 2;  // K tiles per run at least: one whole group and two tiles
@@ -1072,8 +1069,15 @@ static int run_gemm(const void* act, int act_t, int lda, int m, int k, const Dev
     // (profiles/r05_gemm7_*); a weight whose q * s leaves the fp16 normal range, or NAD_GEMM_KERNEL=3, runs gemm3
     const bool g7 = pg == 3 && kn.gemm_kernel == 7 && gemm7_ok(w.bits, w.blocksize, w.fold_ok);
     if (g7) a.fold = 1;
+    // gemm7's tile height: the problem's rows rounded up to 32 / 64 / 128, else 256 (mid-M launches split K so the
+    // output tiles fill the chip: 17 <= M <= 256 was a 256-row tile of which most rows re-read the last one)
+    int bm = 256;
+    if (g7) {
+      bm = kn.gemm7_bm > 0 ? kn.gemm7_bm : (m <= 32 ? 32 : (m <= 64 ? 64 : (m <= 128 ? 128 : 256)));
+      if (bm != 32 && bm != 64 && bm != 128) bm = 256;
+    }
     int ktiles = w.nt;
-    const int ks = !g2 ? splitk_plan(w, m, &ktiles) : 1;
+    const int ks = !g2 ? splitk_plan(w, m, &ktiles, bm) : 1;
     if (ks > 1 && kn.gemm4_ksw == 2) a.ksw = 0;  // auto KSW was measured on whole-K launches only
     if (ks > 1) {  // partials after the fp16 activations in the same workspace (stream-ordered reuse)
       a.ksplit = ks;
@@ -1084,7 +1088,7 @@ static int run_gemm(const void* act, int act_t, int lda, int m, int k, const Dev
       if (!base) return -1;
       a.part = reinterpret_cast<float*>(base + a16);
     }
-    const int tiles = ((m + 255) / 256) * ((w.n + 127) / 128);
+    const int tiles = ((m + bm - 1) / bm) * ((w.n + 127) / 128);
     if (planned(pg == 4 ? NAD_KERNEL_GEMM4 : (g2 ? NAD_KERNEL_GEMM2 : (g7 ? NAD_KERNEL_GEMM7 : NAD_KERNEL_GEMM3)),
                 tiles * ks, 512, ks, a.fold | (a.ksw << 1))) {
       if (ks > 1) planned(0, 0, 0, 1, 0, false);  // the split-K reduce
@@ -1092,7 +1096,7 @@ static int run_gemm(const void* act, int act_t, int lda, int m, int k, const Dev
     }
     hipError_t e = pg == 4 ? launch_gemm4(a, w.bits, pre->p, pre->ld, st)
                    : g2    ? launch_gemm2(a, pre->p, pre->ld, st)
-                   : g7    ? launch_gemm7(a, pre->p, pre->ld, st)
+                   : g7    ? launch_gemm7(a, bm, pre->p, pre->ld, st)
                            : launch_gemm3(a, pre->p, pre->ld, st);
     if (e == hipSuccess && ks > 1) e = launch_splitk_reduce(a, st);
     if (e != hipSuccess) {
@@ -1369,323 +1373,6 @@ extern "C" int nad_device_ffn_forward(const void* act, int act_dtype, const void
                                       const void* w3p, float* tmp1, float* tmp2, float* out, int m, int fin, int fmid,
                                       int fout, int lda, int epi, void* queue) {
   return ffn_forward(act, act_dtype, w1p, w2p, w3p, tmp1, tmp2, out, m, fin, fmid, fout, lda, epi, queue, true);
-}
-
-// ------------------------------------------------------------------------------------------------ decode chain
-// A segment of a decode step's WOQ matmuls as ONE persistent launch on the weight-stream engine (woq_chain.hip).
-// Ops run in order; an op whose input (act) or residual (res) is exactly an earlier op's output receives it through
-// that op's granules inside the launch, anything else is an external vector written before the launch.  Eligible:
-// M = 1, fp32 activations, every op int4 (or every op int2) with the same groups-per-tile class and symmetry,
-// stripe-major layout, no act-order shuffle, fp arithmetic; LINEAR epilogues NONE / RES_ADD, GATE_UP SILU_MUL /
-// GELU_MUL.  The reference graph cuts such a segment at every attention node (ne_layers.c:11915-12028).
-struct NadChain {
-  EngOp* dev_ops = nullptr;
-  unsigned* ctl = nullptr;              // [1] status, [2] workgroup arrivals (monotonic; the launch generation is arrivals / grid)
-  unsigned long long* gran = nullptr;   // granule arrays of the results read inside the launch
-  int n_ops = 0, grid = 0, bump = 0;
-  EngGeometry g{};
-};
-
-namespace {
-struct ChainOut {
-  const float* p;
-  int n, op, wi;
-};
-struct ChainWrite {
-  std::pair<const char*, const char*> range;
-  int op;
-  bool aux;
-};
-}  // namespace
-
-extern "C" void* nad_chain_create(const nad_chain_op* ops, int n_ops, int m) {
-  if (!ops || n_ops <= 0 || n_ops > 255 || m != 1) {
-    set_err("nad_chain_create: the decode engine takes m = 1 and 1..255 ops (got m = %d, %d ops)", m, n_ops);
-    return nullptr;
-  }
-  const int grid = device_cus();
-  std::vector<EngOp> host(static_cast<size_t>(n_ops));
-  std::vector<ChainOut> outs;                       // every result of the launch, in op order
-  std::vector<ChainWrite> writes, ext_reads;        // byte ranges written (results, aux) / read from outside the chain
-  std::vector<std::vector<int>> need_gran(static_cast<size_t>(n_ops), std::vector<int>(3, 0));
-  EngGeometry g{};
-  g.bits = 0;
-  int kp = 0;
-  size_t sd_bytes = 0;
-  bool bump = false;
-  // the LATEST earlier op writing exactly this vector (a buffer may be rewritten by later layers of one launch)
-  auto find_out = [&](const float* p, int upto, int len, const char* what, int i, int* op, int* wi) -> int {
-    int found = 0;
-    for (const ChainOut& c : outs) {
-      if (c.op >= upto) break;
-      if (c.p == p) {
-        if (c.n != len) {
-          set_err("nad_chain_create: op %d reads %s from op %d's result of length %d, expected %d", i, what, c.op, c.n,
-                  len);
-          return -1;
-        }
-        *op = c.op;
-        *wi = c.wi;
-        found = 1;
-      } else if (p < c.p + c.n && c.p < p + len) {
-        set_err("nad_chain_create: op %d's %s overlaps op %d's result without being it", i, what, c.op);
-        return -1;
-      }
-    }
-    return found;
-  };
-  for (int i = 0; i < n_ops; i++) {
-    const nad_chain_op& o = ops[i];
-    EngOp& e = host[size_t(i)];
-    // QKV: three weights, or two ({Q, K} of a GQA model whose V has another format, w[2] = NULL)
-    const int nw = o.kind == NAD_CHAIN_QKV ? (o.w[2] ? 3 : 2) : (o.kind == NAD_CHAIN_GATE_UP ? 2 : 1);
-    const DeviceWeight* ws[3] = {nullptr, nullptr, nullptr};
-    for (int j = 0; j < nw; j++)
-      if (!(ws[j] = as_weight(o.w[j]))) return nullptr;
-    const DeviceWeight& w0 = *ws[0];
-    int tpg = 0;
-    const int gpt = gemv_groups_per_tile(w0.bits, w0.nt, w0.ng, w0.blocksize, &tpg);
-    for (int j = 0; j < nw; j++) {
-      const DeviceWeight& w = *ws[j];
-      if ((w.bits != 4 && w.bits != 2) || w.f4kind >= 0 || w.has_shuffle || w.kmajor || int8_compute(w) ||
-          w.k != w0.k || w.nt != w0.nt || w.ng != w0.ng || w.blocksize != w0.blocksize || w.bits != w0.bits ||
-          w.scale_t != w0.scale_t || w.asym != w0.asym) {
-        set_err("nad_chain_create: op %d weight %d is not an engine weight (int4 / int2, stripe-major, no act-order, "
-                "fp arithmetic, one geometry per op)", i, j);
-        return nullptr;
-      }
-    }
-    if (gpt == 0 || (w0.bits == 4 && gpt > 2)) {
-      set_err("nad_chain_create: op %d's group size %d does not tile the K tiles", i, w0.blocksize);
-      return nullptr;
-    }
-    // at most two weight formats per launch (EngOp::fmt), one symmetry
-    int fmt = 0;
-    if (g.bits == 0) {
-      g.bits = g.bits1 = w0.bits;
-      g.gpt = g.gpt1 = gpt;
-      g.asym = w0.asym;
-    } else if (g.asym != w0.asym) {
-      set_err("nad_chain_create: op %d's symmetry (asym %d) differs from op 0's", i, w0.asym);
-      return nullptr;
-    } else if (g.bits != w0.bits || g.gpt != gpt) {
-      if (g.bits1 == g.bits && g.gpt1 == g.gpt) {
-        g.bits1 = w0.bits;
-        g.gpt1 = gpt;
-      }
-      if (g.bits1 != w0.bits || g.gpt1 != gpt || !(engine_format_pair_ok(g.bits, g.gpt, g.bits1, g.gpt1) ||
-                                                     engine_format_pair_ok(g.bits1, g.gpt1, g.bits, g.gpt))) {
-        set_err("nad_chain_create: op %d's format (bits %d, %d groups per tile) cannot join the launch's (bits %d / %d, "
-                "%d / %d groups per tile)", i, w0.bits, gpt, g.bits, g.bits1, g.gpt, g.gpt1);
-        return nullptr;
-      }
-      fmt = 1;
-    }
-    e.fmt = fmt;
-    e.gpt = gpt;
-    if (o.act_dtype != kActF32 || !o.act) {
-      set_err("nad_chain_create: op %d: the engine takes fp32 activations", i);
-      return nullptr;
-    }
-    int epi = o.epi;
-    if (o.kind == NAD_CHAIN_GATE_UP) {
-      if (epi != kEpiSiluMul && epi != kEpiGeluMul) epi = kEpiSiluMul;
-    } else if (epi != kEpiNone && epi != kEpiResAdd) {
-      set_err("nad_chain_create: op %d: epilogue %d is not an engine epilogue (NONE / RES_ADD)", i, epi);
-      return nullptr;
-    }
-    const int KT = w0.bits == 4 ? 128 : 256;
-    e.nw = nw;
-    e.dual = o.kind == NAD_CHAIN_GATE_UP ? 1 : 0;
-    e.K = w0.k;
-    e.nt = w0.nt;
-    e.ng = w0.ng;
-    e.tpg_shift = (gpt == 1 && tpg > 0) ? __builtin_ctz(unsigned(tpg)) : 31;
-    e.scale_t = w0.scale_t;
-    e.norm = o.norm;
-    e.norm_eps = o.norm_eps;
-    e.norm_w = o.norm_w;
-    e.epi = epi;
-    e.aux = o.kind == NAD_CHAIN_GATE_UP ? o.aux : nullptr;
-    e.tag = unsigned(i + 1);
-    int stripes = 0;
-    for (int j = 0; j < 4; j++) e.stripe_base[j] = INT_MAX;
-    for (int j = 0; j < nw; j++) {
-      EngWeight& W = e.w[j];
-      W.tiles = ws[j]->tiles;
-      W.scales = ws[j]->scales;
-      W.zps = ws[j]->zps;
-      W.ns = ws[j]->ns;
-      W.n = ws[j]->n;
-      W.out = (o.kind == NAD_CHAIN_GATE_UP && j == 1) ? nullptr : o.out[j];
-      e.stripe_base[j] = stripes;
-      stripes += ws[j]->ns;
-    }
-    if (e.dual && (ws[1]->n != w0.n)) {
-      set_err("nad_chain_create: op %d: gate and up differ in N", i);
-      return nullptr;
-    }
-    e.units = e.dual ? w0.ns : stripes;
-    e.u_q = e.units / grid;
-    e.u_r = e.units % grid;
-    if ((e.u_q + (e.u_r ? 1 : 0)) * (e.dual ? 2 : 1) > kEngMaxStripes) {
-      set_err("nad_chain_create: op %d has more than %d stripes per CU", i, kEngMaxStripes);
-      return nullptr;
-    }
-    // input / residual: an earlier result of this launch, or external
-    int pop, pwi;
-    int r = find_out(static_cast<const float*>(o.act), i, e.K, "its input", i, &pop, &pwi);
-    if (r < 0) return nullptr;
-    if (r) {
-      e.act_tag = unsigned(pop + 1);
-      need_gran[size_t(pop)][size_t(pwi)] = 1;
-      bump = true;
-    }
-    e.act = static_cast<const float*>(o.act);
-    if (epi == kEpiResAdd) {
-      if (!o.res || nw != 1) {
-        set_err("nad_chain_create: op %d: RES_ADD needs a residual and one weight", i);
-        return nullptr;
-      }
-      r = find_out(o.res, i, w0.n, "its residual", i, &pop, &pwi);
-      if (r < 0) return nullptr;
-      if (r) {
-        e.res_tag = unsigned(pop + 1);
-        need_gran[size_t(pop)][size_t(pwi)] = 1;
-        bump = true;
-      }
-      e.res = o.res;
-    }
-    // write-after-read: the engine orders only the hand-offs that go through granules, so a vector read from outside
-    // the chain (an external act / res, norm_w) must not be written by this or any later op while slower workgroups
-    // may still read it, and nothing may read an op's aux (it has no granules)
-    {
-      auto span = [](const void* p, size_t n) { return std::make_pair(static_cast<const char*>(p),
-                                                                       static_cast<const char*>(p) + 4 * n); };
-      auto hit = [](std::pair<const char*, const char*> x, std::pair<const char*, const char*> y) {
-        return x.first < y.second && y.first < x.second;
-      };
-      std::vector<std::pair<const char*, const char*>> rd;
-      if (!e.act_tag) rd.push_back(span(o.act, size_t(e.K)));
-      if (epi == kEpiResAdd && !e.res_tag) rd.push_back(span(o.res, size_t(w0.n)));
-      if (o.norm && o.norm_w) rd.push_back(span(o.norm_w, size_t(e.K)));
-      for (const auto& r0 : rd) {
-        for (const ChainWrite& wv : writes)
-          if (hit(r0, wv.range)) {
-            set_err("nad_chain_create: op %d reads a vector from outside the chain that overlaps op %d's %s", i, wv.op,
-                    wv.aux ? "aux (aux has no in-launch hand-off)" : "result without being it");
-            return nullptr;
-          }
-        ext_reads.push_back(ChainWrite{r0, i, false});
-      }
-      std::vector<ChainWrite> mine;
-      for (int j = 0; j < nw; j++)
-        if (e.w[j].out) mine.push_back(ChainWrite{span(e.w[j].out, size_t(e.w[j].n)), i, false});
-      if (e.aux) mine.push_back(ChainWrite{span(e.aux, size_t(w0.n)), i, true});
-      for (const ChainWrite& wv : mine) {
-        for (const ChainWrite& r0 : ext_reads)
-          if (hit(wv.range, r0.range)) {
-            set_err("nad_chain_create: op %d writes its %s over a vector op %d reads from outside the chain "
-                    "(write-after-read inside one launch)", i, wv.aux ? "aux" : "result", r0.op);
-            return nullptr;
-          }
-        writes.push_back(wv);
-      }
-    }
-    for (int j = 0; j < nw; j++)
-      if (e.w[j].out) outs.push_back(ChainOut{e.w[j].out, e.w[j].n, i, j});
-    kp = std::max(kp, w0.nt * KT);
-    // scale (+ zero point) bytes of one fill of 16 tiles
-    const int ssz = w0.scale_t == kScaleF32 ? 4 : 2;
-    const size_t groups = gpt == 1 ? size_t((kEngFillTiles + std::max(tpg, 1) - 1) / std::max(tpg, 1) + 1)
-                                   : size_t(kEngFillTiles) * gpt;
-    sd_bytes = std::max(sd_bytes, std::min(groups, size_t(w0.ng)) * 16 * ssz);
-  }
-  // a mixed launch is instantiated with the int2 member as format 0: swap when the first op was the other one
-  if ((g.bits != g.bits1 || g.gpt != g.gpt1) && !engine_format_pair_ok(g.bits, g.gpt, g.bits1, g.gpt1)) {
-    std::swap(g.bits, g.bits1);
-    std::swap(g.gpt, g.gpt1);
-    for (EngOp& e : host) e.fmt ^= 1;
-  }
-  const Knobs& kn = knobs();
-  g.loaders = kn.engine_loaders;  // loader waves (tools/dma_probe.hip: 2 loaders with one fill in flight each best)
-  g.sd = int((sd_bytes + 1023) / 1024);
-  if (g.sd < 1) g.sd = 1;
-  g.max_slots = kn.engine_slots;  // ring slots at most (A/B of the ring's size)
-  if (g.sd > 2 || !engine_geometry(g, kp)) {
-    set_err("nad_chain_create: the engine's LDS ring does not fit (K up to %d, %zu scale bytes per fill)", kp,
-            sd_bytes);
-    return nullptr;
-  }
-  // granule arrays for the results read inside the launch
-  size_t ngran = 0;
-  for (int i = 0; i < n_ops; i++)
-    for (int j = 0; j < host[size_t(i)].nw; j++)
-      if (need_gran[size_t(i)][size_t(j)]) ngran += size_t(host[size_t(i)].w[j].n);
-  NadChain* c = new NadChain();
-  c->n_ops = n_ops;
-  c->grid = grid;
-  c->bump = bump ? 1 : 0;
-  c->g = g;
-  if (hipMalloc(&c->dev_ops, sizeof(EngOp) * size_t(n_ops)) != hipSuccess || hipMalloc(&c->ctl, 256) != hipSuccess ||
-      hipMemset(c->ctl, 0, 256) != hipSuccess ||
-      (ngran && (hipMalloc(&c->gran, ngran * 8) != hipSuccess || hipMemset(c->gran, 0, ngran * 8) != hipSuccess))) {
-    set_err("nad_chain_create: device allocation failed");
-    nad_chain_destroy(c);
-    return nullptr;
-  }
-  size_t off = 0;
-  std::vector<std::vector<unsigned long long*>> gp(static_cast<size_t>(n_ops), std::vector<unsigned long long*>(3));
-  for (int i = 0; i < n_ops; i++)
-    for (int j = 0; j < host[size_t(i)].nw; j++)
-      if (need_gran[size_t(i)][size_t(j)]) {
-        host[size_t(i)].w[j].gran = c->gran + off;
-        gp[size_t(i)][size_t(j)] = c->gran + off;
-        off += size_t(host[size_t(i)].w[j].n);
-      }
-  // resolve the readers' granule pointers
-  for (int i = 0; i < n_ops; i++) {
-    EngOp& e = host[size_t(i)];
-    for (const ChainOut& o : outs) {
-      if (o.op >= i) break;
-      if (e.act_tag && unsigned(o.op + 1) == e.act_tag && o.p == e.act) e.act_gran = gp[size_t(o.op)][size_t(o.wi)];
-      if (e.res_tag && unsigned(o.op + 1) == e.res_tag && o.p == e.res) e.res_gran = gp[size_t(o.op)][size_t(o.wi)];
-    }
-  }
-  if (hipMemcpy(c->dev_ops, host.data(), sizeof(EngOp) * size_t(n_ops), hipMemcpyHostToDevice) != hipSuccess) {
-    set_err("nad_chain_create: op table upload failed");
-    nad_chain_destroy(c);
-    return nullptr;
-  }
-  return c;
-}
-
-extern "C" int nad_chain_run(void* chain, void* queue) {
-  NadChain* c = static_cast<NadChain*>(chain);
-  if (!c) return -1;
-  hipError_t e = launch_engine(c->dev_ops, c->n_ops, c->g, c->ctl, c->grid, c->bump, static_cast<hipStream_t>(queue));
-  if (e != hipSuccess) {
-    set_err("nad_chain_run: launch failed: %s", hipGetErrorString(e));
-    return -1;
-  }
-  return 0;
-}
-
-extern "C" int nad_chain_status(void* chain) {
-  NadChain* c = static_cast<NadChain*>(chain);
-  if (!c) return -1;
-  unsigned s = 0;
-  if (hipMemcpy(&s, c->ctl + 1, sizeof(unsigned), hipMemcpyDeviceToHost) != hipSuccess) return -1;
-  return int(s);
-}
-
-extern "C" void nad_chain_destroy(void* chain) {
-  NadChain* c = static_cast<NadChain*>(chain);
-  if (!c) return;
-  if (c->dev_ops) (void)hipFree(c->dev_ops);
-  if (c->ctl) (void)hipFree(c->ctl);
-  if (c->gran) (void)hipFree(c->gran);
-  delete c;
 }
 
 // ------------------------------------------------------------------------------------------------ batched problems

@@ -26,16 +26,30 @@
 namespace nad {
 namespace g7 {
 
-constexpr int BM = 256, BN = 128, KT = 128, ROWB = 128;  // ROWB: bytes of one A row per 64-deep half step
-constexpr int HBUF = BM * ROWB;                          // one half step of A: 32 KiB
-constexpr int NA = 4;                                    // A ring: three half steps in flight
-constexpr int NS = BN / 16;                              // stripes per tile
+constexpr int KT = 128, ROWB = 128;  // ROWB: bytes of one A row per 64-deep half step
+constexpr int NS = 8;                // stripes per tile (128 columns)
 constexpr int BTILES = NS * 1024, BSC = 512, BZP = 512;
-constexpr int BBUF = BTILES + BSC + BZP;                 // one K tile of B + scale and zero-point dwords
-constexpr int NBR = 3;                                   // B ring
-constexpr int LDS_BYTES = NA * HBUF + NBR * BBUF;        // 155 KiB
-constexpr int EPI_LD = 36;                               // epilogue transpose row stride (floats)
-static_assert(4 * BM * EPI_LD * 4 <= LDS_BYTES, "epilogue transpose must fit the rings");
+constexpr int BBUF = BTILES + BSC + BZP;  // one K tile of B + scale and zero-point dwords
+constexpr int EPI_LD = 36;                // epilogue transpose row stride (floats)
+
+// Geometry per tile height BMT (32, 64, 128, 256 rows; every wave covers all of them): the A ring runs DA = NA - 1 half
+// steps ahead -- deeper for the short tiles, whose K runs are split-K runs of a few tiles -- and the B ring holds a
+// tile no shorter than the two half steps after its last read.
+template <int BMT>
+struct Geo {
+  static constexpr int RF = BMT / 16;                  // row fragments per wave
+  static constexpr int HF = RF / 2;                    // fragments per half of the register rotation
+  static constexpr int HBUF = BMT * ROWB;              // one half step of A
+  static constexpr int PIECES = HBUF / 1024;           // A pieces per half step
+  static constexpr int PA = PIECES >= 8 ? PIECES / 8 : 1;  // per wave (BMT = 32: waves 4-7 repeat pieces 0-3)
+  static constexpr int NA = BMT == 256 ? 4 : (BMT == 128 ? 6 : 8);
+  static constexpr int DA = NA - 1;
+  static constexpr int NBR = (DA + 3) / 2;
+  static constexpr int LDS_RING = NA * HBUF + NBR * BBUF;
+  static constexpr int LDS_EPI = 8 * (BMT / 2) * EPI_LD * 4;
+  static constexpr int LDS = LDS_RING > LDS_EPI ? LDS_RING : LDS_EPI;
+  static_assert(LDS <= 160 * 1024 && DA % 2 == 1, "geometry");
+};
 
 // LDS-DMA as raw buffer loads: 32-bit per-lane offsets fixed for the whole K loop, the moving part in an SGPR
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t brsrc(const void* p) {
@@ -80,6 +94,14 @@ __device__ __forceinline__ void wait_lgk(T&... regs) {
   asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(N));
   (tie(regs), ...);
 }
+template <int B, size_t... I>
+__device__ __forceinline__ void read_frags(h8_t* f, uint32_t addr, std::index_sequence<I...>) {
+  ((f[B + I] = lds_b128<int(B + I) * 16 * ROWB>(addr)), ...);
+}
+template <int B, size_t... I>
+__device__ __forceinline__ void tie_frags(h8_t* f, std::index_sequence<I...>) {
+  (tie(f[B + I]), ...);
+}
 __device__ __forceinline__ uint32_t lds_addr(const char* p) {
   return uint32_t(reinterpret_cast<uintptr_t>((const __attribute__((address_space(3))) char*)p));
 }
@@ -115,15 +137,20 @@ __device__ __forceinline__ h8_t dequant_fold(uint32_t w, uint32_t mag, h2_t s16,
 
 #define NAD_SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
 
-// 8 waves (two per SIMD) split over K: wave (wn = w & 3, wk = w >> 2) owns the 256 x 32 partial of stripes 2 wn,
-// 2 wn + 1 over the 32-deep step wk of every 64-deep half step.  Its 16 A fragments per half step rotate in two halves
-// around the half step's barrier: fragments 0..7 of half step u + 1 are read into the registers fragments 0..7 of u
-// just left (their 16 MFMAs done, barrier of u + 1 passed), fragments 8..15 after the other 16 MFMAs.  A 4-wave form
-// (one wave per SIMD owning both K steps) measured 5-15 % slower than gemm3 (profiles/r05_gemm6_vs_gemm3_sweep.txt);
+// 8 waves (two per SIMD) split over K: wave (wn = w & 3, wk = w >> 2) owns the BMT x 32 partial of stripes 2 wn,
+// 2 wn + 1 over the 32-deep step wk of every 64-deep half step.  Its RF A fragments per half step rotate in two halves
+// around the half step's barrier: fragments 0 .. HF - 1 of half step u + 1 are read into the registers the same
+// fragments of u just left (their MFMAs done, barrier of u + 1 passed), the rest after the other MFMAs.  Batches past
+// the end of the K run load from a zero-record buffer, so every half step issues and waits the same counts.  A 4-wave
+// form (one wave per SIMD owning both K steps) measured 5-15 % slower than gemm3 (profiles/r05_gemm6_vs_gemm3_sweep.txt);
 // wider-N tiles (128 x 256, 128 x 512, 256 x 256: 8 waves as 1 or 2 (M) x 8 or 4 (N), each B fragment dequantized by
-// every M-wave) 3-35 % slower than this one (profiles/r05_gemm8_tile_shapes_sweep.txt).
-template <bool ASYM, int ST>
+// every M-wave) 3-35 % slower than this one (profiles/r05_gemm8_tile_shapes_sweep.txt).  BMT < 256 serves 17 <= M <= 256
+// with split-K runs (the mid-M range): the tile's rows are what the problem has, not 256 rows of which most re-read the
+// last one.
+template <int BMT, bool ASYM, int ST>
 __global__ __launch_bounds__(512, 1) void woq_gemm7_kernel(GemmArgs a, const _Float16* __restrict__ A16, int lda16) {
+  using G = Geo<BMT>;
+  constexpr int RF = G::RF, HF = G::HF, HBUF = G::HBUF, PA = G::PA, NA = G::NA, DA = G::DA, NBR = G::NBR;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));
@@ -133,7 +160,8 @@ __global__ __launch_bounds__(512, 1) void woq_gemm7_kernel(GemmArgs a, const _Fl
   const int tpg = W.bs / KT;
   const int tsh = __builtin_ctz(unsigned(tpg));
 
-  const int nbm = (M + BM - 1) / BM;
+  // XCD-aware remap (one XCD walks the N tiles of one (M tile, K run)) and split-K runs, as gemm3
+  const int nbm = (M + BMT - 1) / BMT;
   const int nbn = (ns + NS - 1) / NS;
   const int ntile = nbm * nbn;
   const int nsplit = a.ksplit > 1 ? a.ksplit : 1;
@@ -149,19 +177,23 @@ __global__ __launch_bounds__(512, 1) void woq_gemm7_kernel(GemmArgs a, const _Fl
   const int ntl = nsplit > 1 ? min(a.ktiles, nt - kt0) : nt;
   const int nh = 2 * ntl;
   const int bm = bid / nbn, bn = bid % nbn;
-  const int m0 = bm * BM;
+  const int m0 = bm * BMT;
   const int nl = lane & 15, kq = lane >> 4;
 
-  // A piece p = 4 wave + i: rows 8p .. 8p + 7
-  uint32_t aoff[4];
+  // A piece p: rows 8p .. 8p + 7, lane -> row 8p + (lane >> 3), chunk (lane & 7) ^ ((row >> 1) & 7)
+  uint32_t aoff[PA];
+  char* adst[PA];
 #pragma unroll
-  for (int i = 0; i < 4; i++) {
-    const int row = (wave * 4 + i) * 8 + (lane >> 3);
-    const int grow = min(m0 + row, M - 1);
+  for (int i = 0; i < PA; i++) {
+    const int p = (wave * PA + i) % G::PIECES;
+    const int row = p * 8 + (lane >> 3);
+    const int grow = min(m0 + row, M - 1);  // rows past M re-read row M - 1 (never stored)
     aoff[i] = uint32_t(grow) * uint32_t(lda16) * 2u + uint32_t(((lane & 7) ^ ((row >> 1) & 7)) * 16);
+    adst[i] = smem + p * 1024;
   }
   const auto ra = brsrc(reinterpret_cast<const char*>(A16) + size_t(kt0) * KT * 2);
   const auto rb = brsrc(static_cast<const char*>(W.tiles) + size_t(kt0) * 1024);
+  const auto rnull = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(W.tiles), 0, 0, 0x00020000);
   const uint32_t boffd = (uint32_t(min(bn * NS + wave, ns - 1)) * nt * 64 + lane) * 16;
   const int sstripe = min(bn * NS + (wave & 1) * 4 + (lane >> 4), ns - 1);
   const uint32_t srow0 = uint32_t(sstripe) * ng * 16 + nl + uint32_t(kt0 >> tsh) * 16;
@@ -170,22 +202,28 @@ __global__ __launch_bounds__(512, 1) void woq_gemm7_kernel(GemmArgs a, const _Fl
   const auto rz = brsrc(W.zps);
   const uint32_t svo = st == kScaleF32 ? srow0 * 4 : (srow0 >> 1) * 4, zvo = (srow0 >> 2) * 4;
 
-  auto issue = [&](auto Hc, int u) {
-    constexpr int H = decltype(Hc)::value;
-    const int ua = u + 3;
-    char* ab = smem + (ua & 3) * HBUF;
-  #pragma unroll
-    for (int i = 0; i < 4; i++) blds16(ra, aoff[i], uint32_t(ua) * ROWB, ab + (wave * 4 + i) * 1024);
-    if constexpr (H == 1) {
+  // batch(u): A(u + DA) and, when u + DA is even, B tile (u + DA) / 2 with its scale / zero-point pieces
+  auto issue = [&](int u) {
+    const int ua = u + DA;
+    const bool live = ua < nh;
+    const int aslot = ua % NA;
+    const auto rA = live ? ra : rnull;
+#pragma unroll
+    for (int i = 0; i < PA; i++) blds16(rA, aoff[i], uint32_t(ua) * ROWB, adst[i] + aslot * HBUF);
+    if ((ua & 1) == 0) {
       const int t = ua >> 1;
       char* bb = smem + NA * HBUF + (t % NBR) * BBUF;
-      blds16(rb, boffd, uint32_t(t) * 1024, bb + wave * 1024);
+      blds16(live ? rb : rnull, boffd, uint32_t(t) * 1024, bb + wave * 1024);
       const uint32_t g = uint32_t(t >> tsh) * 16;
-      blds4(rs, svo, st == kScaleF32 ? g * 4 : g * 2, bb + BTILES + (wave & 1) * 256);
-      if constexpr (ASYM) blds4(rz, zvo, g, bb + BTILES + BSC + (wave & 1) * 256);
+      blds4(live ? rs : rnull, svo, st == kScaleF32 ? g * 4 : g * 2, bb + BTILES + (wave & 1) * 256);
+      if constexpr (ASYM) blds4(live ? rz : rnull, zvo, g, bb + BTILES + BSC + (wave & 1) * 256);
     }
   };
-  constexpr int NBW = ASYM ? 3 : 2;
+  // at the barrier of buffer u + 1 (the middle of half step u), batch(u + 1 - DA) has landed and batches
+  // u + 2 - DA .. u (DA - 1 of them, (DA - 1) / 2 with a B tile) may be in flight
+  constexpr int NB = ASYM ? 3 : 2;
+  constexpr int WV = (DA - 1) * PA + (DA - 1) / 2 * NB;
+  static_assert(WV < 64, "vmcnt");
 
   const uint32_t mag = 0x64006400u;
   const h2_t s16 = splat(1.f / 16.f);
@@ -204,19 +242,19 @@ __global__ __launch_bounds__(512, 1) void woq_gemm7_kernel(GemmArgs a, const _Fl
     return splat(f);
   };
 
-  f4_t acc[16][2];
+  f4_t acc[RF][2];
 #pragma unroll
-  for (int i = 0; i < 16; i++)
+  for (int i = 0; i < RF; i++)
 #pragma unroll
     for (int j = 0; j < 2; j++) acc[i][j] = f4_t{0.f, 0.f, 0.f, 0.f};
 
-  h8_t af[16];
+  h8_t af[RF];
   h8_t bf[2];
   h2_t sc[2];
   h2_t c0[2] = {zc0, zc0}, c1[2] = {zc1, zc1};
   uint32_t bw0 = 0, bw1 = 0, sw0 = 0, sw1 = 0, zw0 = 0, zw1 = 0;
 
-  // B words (+ scale / zp at a tile start) and A fragments 0..7 of half step u
+  // B words (+ scale / zp at a tile start) and A fragments 0 .. HF - 1 of half step u
   auto read_lo = [&](auto Hc, int u) {
     constexpr int H = decltype(Hc)::value;
     const int t = u >> 1;
@@ -231,26 +269,12 @@ __global__ __launch_bounds__(512, 1) void woq_gemm7_kernel(GemmArgs a, const _Fl
         zw1 = lds_b32<64>(bl + zoff);
       }
     }
-    const uint32_t al = lds_addr(smem + (u & 3) * HBUF) + roff;
-    af[0] = lds_b128<0 * 16 * ROWB>(al);
-    af[1] = lds_b128<1 * 16 * ROWB>(al);
-    af[2] = lds_b128<2 * 16 * ROWB>(al);
-    af[3] = lds_b128<3 * 16 * ROWB>(al);
-    af[4] = lds_b128<4 * 16 * ROWB>(al);
-    af[5] = lds_b128<5 * 16 * ROWB>(al);
-    af[6] = lds_b128<6 * 16 * ROWB>(al);
-    af[7] = lds_b128<7 * 16 * ROWB>(al);
+    const uint32_t al = lds_addr(smem + (u % NA) * HBUF) + roff;
+    read_frags<0>(af, al, std::make_index_sequence<HF>{});
   };
   auto read_hi = [&](int u) {
-    const uint32_t al = lds_addr(smem + (u & 3) * HBUF) + roff;
-    af[8] = lds_b128<8 * 16 * ROWB>(al);
-    af[9] = lds_b128<9 * 16 * ROWB>(al);
-    af[10] = lds_b128<10 * 16 * ROWB>(al);
-    af[11] = lds_b128<11 * 16 * ROWB>(al);
-    af[12] = lds_b128<12 * 16 * ROWB>(al);
-    af[13] = lds_b128<13 * 16 * ROWB>(al);
-    af[14] = lds_b128<14 * 16 * ROWB>(al);
-    af[15] = lds_b128<15 * 16 * ROWB>(al);
+    const uint32_t al = lds_addr(smem + (u % NA) * HBUF) + roff;
+    read_frags<HF>(af, al, std::make_index_sequence<HF>{});
   };
   auto dequant = [&](auto Hc) {
     constexpr int H = decltype(Hc)::value;
@@ -269,109 +293,102 @@ __global__ __launch_bounds__(512, 1) void woq_gemm7_kernel(GemmArgs a, const _Fl
     bf[1] = dequant_fold(bw1, mag, s16, c0[1], c1[1], sc[1]);
   };
 
-  // prologue
-  issue(std::integral_constant<int, 1>{}, -3);
-  issue(std::integral_constant<int, 0>{}, -2);
-  if (nh > 2) {
-    issue(std::integral_constant<int, 1>{}, -1);
-    wait_vm<8 + NBW>();
-  } else {
-    wait_vm<4>();
-  }
+  // prologue: batches -DA .. -1, then the operands of half step 0
+#pragma unroll
+  for (int v = -DA; v < 0; v++) issue(v);
+  wait_vm<WV>();
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
   read_lo(std::integral_constant<int, 0>{}, 0);
   read_hi(0);
-  wait_lgk<8>(bw0, bw1, sw0, sw1, zw0, zw1);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  tie(bw0);
+  tie(bw1);
+  tie(sw0);
+  tie(sw1);
+  tie(zw0);
+  tie(zw1);
   dequant(std::integral_constant<int, 0>{});
 
-  // half step u: entering, B of u is dequantized, A fragments 0..7 of u were issued before 8..15 (both may be in
-  // flight).  The barrier of buffer u + 1 sits between the two MFMA halves.  (Waves 4-7 with that barrier after both
+  // half step u: entering, B of u is dequantized, A fragments 0 .. HF - 1 of u were issued before the rest (both may be
+  // in flight).  The barrier of buffer u + 1 sits between the two MFMA halves.  (Waves 4-7 with that barrier after both
   // halves instead -- a stagger, MI355X_MICROARCH item 9 -- measured 6-15 % slower: profiles/r05_gemm7_stagger_ab.txt.)
-  auto half = [&](auto Hc, auto IssC, auto WvC, int u) {
+  auto half = [&](auto Hc, int u) {
     constexpr int H = decltype(Hc)::value;
-    constexpr bool ISS = decltype(IssC)::value;
-    constexpr int WV = decltype(WvC)::value;
-    constexpr bool MORE = WV >= 0;
-    auto sync = [&]() {
-      wait_vm<WV>();
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-      NAD_SCHED_FENCE();
-      read_lo(std::integral_constant<int, 1 - H>{}, u + 1);
-    };
     NAD_SCHED_FENCE();
-    wait_lgk<8>(af[0], af[1], af[2], af[3], af[4], af[5], af[6], af[7]);
+    asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(HF));  // fragments 0 .. HF - 1 (HF newer reads may be in flight)
+    tie_frags<0>(af, std::make_index_sequence<HF>{});
     NAD_SCHED_FENCE();
-    if constexpr (ISS) issue(Hc, u);
+    issue(u);
 #pragma unroll
-    for (int i = 0; i < 8; i++)
+    for (int i = 0; i < HF; i++)
 #pragma unroll
       for (int j = 0; j < 2; j++) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
     NAD_SCHED_FENCE();
-    wait_lgk<0>(af[8], af[9], af[10], af[11], af[12], af[13], af[14], af[15]);
-    if constexpr (MORE) sync();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    tie_frags<HF>(af, std::make_index_sequence<HF>{});
+    wait_vm<WV>();
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    NAD_SCHED_FENCE();
+    read_lo(std::integral_constant<int, 1 - H>{}, u + 1);
     NAD_SCHED_FENCE();
 #pragma unroll
-    for (int i = 8; i < 16; i++) {
+    for (int i = HF; i < RF; i++) {
       acc[i][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bf[0], acc[i][0], 0, 0, 0);
       acc[i][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bf[1], acc[i][1], 0, 0, 0);
     }
     NAD_SCHED_FENCE();
-    if constexpr (MORE) {
-      read_hi(u + 1);
-      wait_lgk<8>(bw0, bw1, sw0, sw1, zw0, zw1);  // B words (issued before the 16 A fragments) have landed
-      dequant(std::integral_constant<int, 1 - H>{});
-    }
+    read_hi(u + 1);
+    asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(HF));  // the B words and fragments 0 .. HF - 1 have landed
+    tie(bw0);
+    tie(bw1);
+    tie(sw0);
+    tie(sw1);
+    tie(zw0);
+    tie(zw1);
+    dequant(std::integral_constant<int, 1 - H>{});
   };
-  using I0 = std::integral_constant<int, 0>;
-  using I1 = std::integral_constant<int, 1>;
-  using Yes = std::true_type;
-  using No = std::false_type;
-  using Steady = std::integral_constant<int, 8 + NBW>;
-  for (int u = 0; u + 4 < nh; u += 2) {
-    half(I0{}, Yes{}, Steady{}, u);
-    half(I1{}, Yes{}, Steady{}, u + 1);
+  for (int u = 0; u < nh; u += 2) {
+    half(std::integral_constant<int, 0>{}, u);
+    half(std::integral_constant<int, 1>{}, u + 1);
   }
-  if (nh >= 4) {
-    half(I0{}, Yes{}, Steady{}, nh - 4);
-    half(I1{}, No{}, std::integral_constant<int, 4>{}, nh - 3);
-  }
-  half(I0{}, No{}, std::integral_constant<int, 0>{}, nh - 2);
-  half(I1{}, No{}, std::integral_constant<int, -1>{}, nh - 1);
-
-  // epilogue: the two K halves of each 256 x 32 tile meet in LDS (gemm5's order: (k-half 0) + (k-half 1) for every
-  // output).  Wave (wn, wk) finishes rows wk * 128 .. + 127.
+  // drain the no-op loads past the end and the last (unused) operand reads before the rings are reused
   NAD_SCHED_FENCE();
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __syncthreads();
-  float* const tw = reinterpret_cast<float*>(smem) + wave * (128 * EPI_LD);
-  float* const tp = reinterpret_cast<float*>(smem) + (wave ^ 4) * (128 * EPI_LD);
+
+  // epilogue: the two K halves of each BMT x 32 tile meet in LDS ((k-half 0) + (k-half 1) for every output).  Wave
+  // (wn, wk) finishes rows wk * BMT / 2 .. + BMT / 2 - 1.
+  constexpr int HR = BMT / 2;
+  float* const tw = reinterpret_cast<float*>(smem) + wave * (HR * EPI_LD);
+  float* const tp = reinterpret_cast<float*>(smem) + (wave ^ 4) * (HR * EPI_LD);
 #pragma unroll
-  for (int i = 0; i < 8; i++)
+  for (int i = 0; i < HF; i++)
 #pragma unroll
     for (int j = 0; j < 2; j++)
 #pragma unroll
       for (int rr = 0; rr < 4; rr++) {
-        const float v = wk ? acc[i][j][rr] : acc[8 + i][j][rr];  // the partner's rows
+        const float v = wk ? acc[i][j][rr] : acc[HF + i][j][rr];  // the partner's rows
         tp[(i * 16 + kq * 4 + rr) * EPI_LD + j * 16 + nl] = v;
       }
   __syncthreads();
 #pragma unroll
-  for (int i = 0; i < 8; i++)
+  for (int i = 0; i < HF; i++)
 #pragma unroll
     for (int j = 0; j < 2; j++)
 #pragma unroll
       for (int rr = 0; rr < 4; rr++) {
         float* p = tw + (i * 16 + kq * 4 + rr) * EPI_LD + j * 16 + nl;
-        const float mine = wk ? acc[8 + i][j][rr] : acc[i][j][rr];
+        const float mine = wk ? acc[HF + i][j][rr] : acc[i][j][rr];
         *p = wk == 0 ? mine + *p : *p + mine;
       }
   const int col0 = (bn * NS + wn * 2) * 16;
 #pragma unroll 4
-  for (int q = 0; q < 16; q++) {
+  for (int q = 0; q < HR / 8; q++) {
     const int c = q * 64 + lane;
     const int rl = c >> 3, c4 = c & 7;
-    const int row = m0 + wk * 128 + rl;
+    const int row = m0 + wk * HR + rl;
     const int n0 = col0 + c4 * 4;
     const float4 t = *reinterpret_cast<const float4*>(tw + rl * EPI_LD + c4 * 4);
     if (row >= M || n0 >= W.n) continue;
@@ -391,29 +408,46 @@ bool gemm7_ok(int bits, int blocksize, int fold_ok) {
   return bits == 4 && fold_ok && blocksize % g7::KT == 0 && (tpg & (tpg - 1)) == 0;
 }
 
-hipError_t launch_gemm7(const GemmArgs& a, const _Float16* A16, int lda16, hipStream_t st) {
-  const int nbm = (a.M + g7::BM - 1) / g7::BM, nbn = (a.w.ns + g7::NS - 1) / g7::NS;
-  auto go = [&](auto k, bool& done) -> hipError_t {
-    if (!done) {
+hipError_t launch_gemm7(const GemmArgs& a, int bm, const _Float16* A16, int lda16, hipStream_t st) {
+  const int nbm = (a.M + bm - 1) / bm, nbn = (a.w.ns + g7::NS - 1) / g7::NS;
+  const dim3 grid(nbm * nbn * (a.ksplit > 1 ? a.ksplit : 1));
+  auto go = [&](auto k, int lds, bool& done) -> hipError_t {
+    if (!done) {  // opt in to the dynamic LDS once per instantiation
       hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                         g7::LDS_BYTES);
+                                         lds);
       if (e != hipSuccess) return e;
       done = true;
     }
-    hipLaunchKernelGGL(k, dim3(nbm * nbn * (a.ksplit > 1 ? a.ksplit : 1)), dim3(512), g7::LDS_BYTES, st, a, A16,
-                       lda16);
+    hipLaunchKernelGGL(k, grid, dim3(512), lds, st, a, A16, lda16);
     return hipGetLastError();
   };
-  static bool attr[2][3] = {};
-  const bool asym = a.w.zps != nullptr;
-  bool& d = attr[asym][a.scale_t];
-  switch (a.scale_t) {
-    case kScaleF32:
-      return asym ? go(g7::woq_gemm7_kernel<true, kScaleF32>, d) : go(g7::woq_gemm7_kernel<false, kScaleF32>, d);
-    case kScaleBF16:
-      return asym ? go(g7::woq_gemm7_kernel<true, kScaleBF16>, d) : go(g7::woq_gemm7_kernel<false, kScaleBF16>, d);
+  auto pick = [&](auto bmc) -> hipError_t {
+    constexpr int BMT = decltype(bmc)::value;
+    constexpr int L = g7::Geo<BMT>::LDS;
+    static bool attr[2][3] = {};
+    const bool asym = a.w.zps != nullptr;
+    bool& d = attr[asym][a.scale_t];
+    switch (a.scale_t) {
+      case kScaleF32:
+        return asym ? go(g7::woq_gemm7_kernel<BMT, true, kScaleF32>, L, d)
+                    : go(g7::woq_gemm7_kernel<BMT, false, kScaleF32>, L, d);
+      case kScaleBF16:
+        return asym ? go(g7::woq_gemm7_kernel<BMT, true, kScaleBF16>, L, d)
+                    : go(g7::woq_gemm7_kernel<BMT, false, kScaleBF16>, L, d);
+      default:
+        return asym ? go(g7::woq_gemm7_kernel<BMT, true, kScaleF16>, L, d)
+                    : go(g7::woq_gemm7_kernel<BMT, false, kScaleF16>, L, d);
+    }
+  };
+  switch (bm) {
+    case 32:
+      return pick(std::integral_constant<int, 32>{});
+    case 64:
+      return pick(std::integral_constant<int, 64>{});
+    case 128:
+      return pick(std::integral_constant<int, 128>{});
     default:
-      return asym ? go(g7::woq_gemm7_kernel<true, kScaleF16>, d) : go(g7::woq_gemm7_kernel<false, kScaleF16>, d);
+      return pick(std::integral_constant<int, 256>{});
   }
 }
 

@@ -199,7 +199,7 @@ hipError_t launch_gemm4(const GemmArgs& a, int bits, const _Float16* A16, int ld
 // prefill GEMM v7 (woq_gemm7.hip, the default for int4 groups of 128 * 2^j): gemm3's contract (256 x 128 tiles,
 // split-K partials, fp16 A padded to the 128-deep tile) with the group scale folded (needs DeviceWeight::fold_ok)
 bool gemm7_ok(int bits, int blocksize, int fold_ok);
-hipError_t launch_gemm7(const GemmArgs& a, const _Float16* A16, int lda16, hipStream_t stream);
+hipError_t launch_gemm7(const GemmArgs& a, int bm, const _Float16* A16, int lda16, hipStream_t stream);
 // sum a.ksplit partials of a split-K gemm3 / gemm4 launch in run order and apply a.epi into a.w.out (woq_gemm2.hip)
 hipError_t launch_splitk_reduce(const GemmArgs& a, hipStream_t stream);
 hipError_t launch_cvt_act(const void* A, int act_t, int lda, int M, int K, int Kp, const int32_t* shuffle,

@@ -333,3 +333,29 @@ def test_ffn_prefill_fp16_intermediates(oracle, knob, qt, bs):
     assert _rel_err(y32, ref) <= TOL["fp32"], _rel_err(y32, ref)
     assert _rel_err(y, y32.astype(np.float64)) <= TOL["fp32"]
     assert not np.array_equal(y, y32)   # the fp16 path really ran (different rounding of the intermediates)
+
+
+MID_M = [17, 32, 33, 64, 100, 128, 200, 256, 512]
+
+
+@pytest.mark.parametrize("m", MID_M)
+@pytest.mark.parametrize("fmt", [(S4, 128, F16, False), (S4, 128, BF16, True), (S2, 64, F16, False), (S2, 64, F16, True)])
+def test_gemm_mid_m(oracle, knob, m, fmt):
+    """The mid-M range (17 <= M <= 512): int4 g128 runs gemm7 with a tile of 32 / 64 / 128 / 256
+    rows and split-K runs (the plan reports the split), int2 g64 gemm4; fp16 activations against the oracle at the
+    fold bar, and -- for int4 -- against gemm3 (exact scale, 256-row tiles) on the same inputs."""
+    qt, bs, st, asym = fmt
+    n, k = 1024, 2048
+    blob = _blob(oracle, n, k, bs, qt, st, asym, 4, seed=m * 7 + bs)
+    w = bestla.DeviceWeight(blob)
+    x = (torch.from_numpy(np.random.default_rng(m).uniform(-0.5, 0.5, size=(m, k)).astype(np.float32))
+         .cuda().half())
+    ref = oracle.forward(x.float().cpu().numpy(), blob, n, k)
+    plan = w.plan(m, "fp16")
+    y = w.forward(x).cpu().numpy()
+    assert _rel_err(y, ref) <= (FOLD_TOL if plan["fold"] else TOL["fp16"]), (_rel_err(y, ref), plan)
+    if qt == S4:
+        assert plan["kernel"] == "woq_gemm7_kernel" and plan["ksplit"] > 1, plan
+        knob("NAD_GEMM_KERNEL", "3")
+        y3 = w.forward(x).cpu().numpy()
+        assert _rel_err(y, y3.astype(np.float64)) <= FOLD_TOL

@@ -1,5 +1,5 @@
-"""Workload for the PMC traffic pass (development tool): a few decode tokens through the per-op launches and the
-decode chain, and a few prefill GEMMs, on the bench's synthetic Llama-2-7B stack (fewer layers: the per-launch
+"""Workload for the PMC traffic pass (development tool): a few decode tokens through the per-op launches and a few
+prefill GEMMs, on the bench's synthetic Llama-2-7B stack (fewer layers: the per-launch
 counters do not depend on the layer count)."""
 import os
 import sys
@@ -14,9 +14,6 @@ stack = bench.Stack(cfg, 0, 1)
 dec = bench.Runner(stack, 1, None, "cuda")
 for _ in range(3):
     dec.step()
-ch = bench.ChainRunner(stack, "cuda", cut=True)
-for _ in range(2):
-    ch.step()
 pre = bench.Runner(stack, 2048, None, "cuda")
 pre.step()
 torch.cuda.synchronize()
@@ -26,4 +23,4 @@ if os.environ.get("PMC_ALG_OUT"):
     L1 = stack.launches(1)
     launches = sum(c for *_, c in L1)
     json.dump({"decode_bytes_per_token": sum(b * c for _, b, _, c in L1), "decode_launches_per_token": launches,
-               "decode_tokens": 3, "chain_tokens": 2}, open(os.environ["PMC_ALG_OUT"], "w"))
+               "decode_tokens": 3}, open(os.environ["PMC_ALG_OUT"], "w"))

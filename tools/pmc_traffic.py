@@ -26,7 +26,7 @@ def per_dispatch(root, ctr):
 
 
 def family(name):
-    for fam in ("woq_gemv_m1_kernel", "woq_gemv_kernel", "woq_engine_kernel"):
+    for fam in ("woq_gemv_m1_kernel", "woq_gemv_kernel"):
         if fam in name:
             return fam
     return None
@@ -44,21 +44,13 @@ def main():
         if family(name):
             fam_w[family(name)] += list(d.values())
     rec = {"method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE (separate passes) over tools/pmc_decode.py "
-                     "(4 Llama-2-7B layers + lm_head: 3 per-op tokens, 2 chain tokens); FETCH_SIZE doubled per "
+                     "(4 Llama-2-7B layers + lm_head: 3 per-op tokens); FETCH_SIZE doubled per "
                      "MI355X_MICROARCH.md (gfx950 reports half of 16 B/lane streaming reads); KB = 1024 B; "
                      "tools/pmc_traffic.py"}
     per_op_alg = alg["decode_bytes_per_token"] / alg["decode_launches_per_token"]
     for fam in fam_f:
         n = len(fam_f[fam])
-        if fam == "woq_engine_kernel":  # the cut launches of a token differ in size: per token, not per launch
-            tok = alg["chain_tokens"]
-            fb = 2 * 1024 * sum(fam_f[fam]) / tok
-            wb = 1024 * sum(fam_w[fam]) / tok
-            a = alg["decode_bytes_per_token"]
-            rec[fam] = {"fetch_bytes_per_token": fb, "write_bytes_per_token": wb, "algorithmic_bytes_per_token": a,
-                        "dispatches": n, "traffic_over_algorithmic": round((fb + wb) / a, 4),
-                        "note": "weights + the granule hand-offs (every CU reads each op's whole input vector)"}
-        else:
+        if True:
             fb = 2 * 1024 * sum(fam_f[fam]) / n
             wb = 1024 * sum(fam_w[fam]) / max(1, len(fam_w[fam]))
             rec[fam] = {"fetch_bytes_per_launch": fb, "write_bytes_per_launch": wb, "algorithmic_bytes_per_launch":
