@@ -169,7 +169,7 @@ def split_range(blob, axis, rank, world, unit=1):
 # ---------------------------------------------------------------------------------------------------- device
 KERNELS = {1: "woq_gemv_m1_kernel", 2: "woq_gemv_kernel", 3: "woq_skinny_kernel", 4: "woq_i8_kernel",
            5: "woq_gemm3_kernel", 6: "woq_gemm4_kernel", 7: "woq_gemm2_kernel", 8: "woq_gemm_kernel",
-           9: "woq_gemm7_kernel"}
+           9: "woq_gemm7_kernel", 10: "woq_mid_kernel"}
 
 
 def plan_forward(bits, n, k, group_size=128, scale_dtype="fp16", asym=False, m=1, act="fp32"):

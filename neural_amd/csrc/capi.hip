@@ -56,6 +56,7 @@ struct Knobs {
   int compute_int8;
   int gemm2_disable, gemm4_all, gemm4_disable, ffn_f32, gemm_kernel, gemm7_bm, splitk_disable;
   int gemm3_stagger, gemm4_fold_all, gemm4_fold, gemm4_ksw;
+  int mid_min_m, mid_max_m, mid_ks;
   int host_cache_mb;
 };
 static Knobs read_knobs() {
@@ -79,6 +80,9 @@ static Knobs read_knobs() {
   k.gemm4_fold_all = env_int("NAD_GEMM4_FOLD_ALL", 1);
   k.gemm4_fold = env_int("NAD_GEMM4_FOLD", 1);
   k.gemm4_ksw = env_int("NAD_GEMM4_KSW", 2);  // folded gemm4 launches with the waves split over K: 0 off, 1 on, 2 auto
+  k.mid_max_m = env_int("NAD_MID_MAX_M", 64);  // mid-M kernel (woq_gemm_mid.hip) up to this M (0: off)
+  k.mid_ks = env_int("NAD_MID_KS", 0);         // tests / tuning: its K runs (0 auto)
+  k.mid_min_m = env_int("NAD_MID_MIN_M", 17);  // ... from this M (tests / tuning: below 17 the GEMV)
   k.host_cache_mb = env_int("NAD_HOST_CACHE_MB", 64 * 1024);
   return k;
 }
@@ -1007,6 +1011,85 @@ struct Half16 {
   const _Float16* aux = nullptr;
 };
 
+// The mid-M GEMM (woq_gemm_mid.hip) for 17 <= M <= 64 (NAD_MID_MIN_M / NAD_MID_MAX_M): integer int4 / int2 weights,
+// stripe-major, no act-order gather, 16-B aligned activation rows with K % 8 == 0 (int2 and int4 g32: M <= 32).
+// Stripe groups of 4 x K runs of one chunk (8 K tiles int4, 4 int2: mid_geometry) each, so K = 4096 splits 4 ways and
+// the 256 / 688 / 768 stripes of the Llama shapes give 256 / 688 / 768 workgroups; the runs' fp32 slabs are summed by
+// the split-K reduce launch.  Returns 1 if launched, 0 if not eligible, -1 on error.
+static int run_mid(const void* act, int act_t, int lda, int m, int k, const DeviceWeight& w, float* out, int ldo,
+                   int epi, const float* bias, int bias_ld, const float* res, int ld_res, const float* aux, int ld_aux,
+                   hipStream_t st, const A16* pre, const Half16* h16) {
+  const Knobs& kn = knobs();
+  if (m > kn.mid_max_m || m < kn.mid_min_m) return 0;
+  if ((w.bits != 4 && w.bits != 2) || w.kmajor || w.f4kind >= 0 || w.shuffle) return 0;
+  if (w.bits == 2 && m > 32) return 0;  // a 256-deep int2 stage's activation fragments: 32 rows fit the registers
+  int tpg = 0;
+  const int gpt = gemv_groups_per_tile(w.bits, w.nt, w.ng, w.blocksize, &tpg);
+  if (gpt != 1 && gpt != 2 && gpt != 4) return 0;
+  if (gpt == 4 && m > 32) return 0;  // 4 groups per tile x 4 stripes of scales beside 64 rows: out of registers
+  // a fused caller's shared fp16 copy of A (pre) is not read: the kernel converts the caller's activations itself, so a
+  // fused QKV / FFN launch is bit-identical to the same weights' single launches; its split-K slabs go past where such a
+  // copy sits in the workspace (the weights after this one may still read it)
+  (void)pre;
+  if (!vec_aligned(act, lda, act_t) || k % 8 != 0) return 0;
+  const int esz = act_t == kActF32 ? 4 : 2;
+  if (uint64_t(m) * lda * esz >= (1ull << 31) || uint64_t(w.ns) * w.nt * 1024 >= (1ull << 31)) return 0;
+  const int rf = (m + 15) / 16;
+  int sps = 0, nw = 0, spw = 0;
+  mid_geometry(w.bits, gpt, act_t, rf, &sps, &nw, &spw);
+  const int chunk = nw * spw;
+  const int nsg = (w.ns + sps - 1) / sps;
+  int ks = (w.nt + chunk - 1) / chunk;
+  // slabs within nad_device_workspace_size's N-independent bound (m x 128 KiB past the fp16 copy): ks x N <= 32768,
+  // so wide weights split K less (N = 11008: 2 runs, 172 x 2 workgroups; N = 32000: none, 500 workgroups)
+  ks = std::max(1, std::min(ks, 32768 / ((w.n + 3) / 4 * 4)));
+  if (kn.mid_ks > 0) ks = std::min(kn.mid_ks, w.nt);
+  const int ktiles = (w.nt + ks - 1) / ks;
+  ks = (w.nt + ktiles - 1) / ktiles;
+  GemmArgs a{};
+  a.A = act;
+  a.lda = lda;
+  a.M = m;
+  a.K = k;
+  a.scale_t = w.scale_t;
+  a.epi = epi;
+  a.res = res;
+  a.ld_res = ld_res;
+  a.aux = aux;
+  a.ld_aux = ld_aux;
+  a.tpg_shift = tpg == 0 ? 31 : __builtin_ctz(unsigned(tpg));
+  a.w = view(w, out, ldo, bias, bias_ld);
+  if (h16) {
+    a.out16 = h16->out;
+    a.ldo16 = h16->ldo;
+    a.aux16 = h16->aux;
+  }
+  if (ks > 1) {
+    a.ksplit = ks;
+    a.ktiles = ktiles;
+    a.ldp = (w.n + 3) / 4 * 4;
+    if (uint64_t(ks) * m * a.ldp * 4 >= (1ull << 31)) return 0;
+    const size_t a16 = (size_t(m) * ((size_t(k) + 255) / 256 * 256) * 2 + 255) / 256 * 256;  // an fp16 copy's room
+    char* base = static_cast<char*>(workspace_for(a16 + size_t(ks) * m * a.ldp * 4, st));
+    if (!base) return -1;
+    a.part = reinterpret_cast<float*>(base + a16);
+  } else {
+    a.ktiles = w.nt;
+  }
+  const int grid = nsg * ks;
+  if (planned(NAD_KERNEL_MID, grid, nw * 64, ks, 0)) {
+    if (ks > 1) planned(0, 0, 0, 1, 0, false);  // the split-K reduce
+    return 1;
+  }
+  hipError_t e = launch_gemm_mid(a, w.bits, gpt, act_t, rf, grid, st);
+  if (e == hipSuccess && ks > 1) e = launch_splitk_reduce(a, st);
+  if (e != hipSuccess) {
+    set_err("mid-M GEMM launch failed: %s", hipGetErrorString(e));
+    return -1;
+  }
+  return 1;
+}
+
 static int run_gemm(const void* act, int act_t, int lda, int m, int k, const DeviceWeight& w, float* out, int ldo,
                     int epi, const float* bias, int bias_ld, const float* res, int ld_res, const float* aux,
                     int ld_aux, hipStream_t st, const A16* pre = nullptr, const Half16* h16 = nullptr) {
@@ -1015,6 +1098,10 @@ static int run_gemm(const void* act, int act_t, int lda, int m, int k, const Dev
     float* outs[1] = {out};
     const int ldos[1] = {ldo};
     return run_i8(act, act_t, lda, m, k, 1, ws, outs, ldos, false, epi, bias, bias_ld, res, ld_res, aux, ld_aux, st);
+  }
+  {
+    const int r = run_mid(act, act_t, lda, m, k, w, out, ldo, epi, bias, bias_ld, res, ld_res, aux, ld_aux, st, pre, h16);
+    if (r != 0) return r < 0 ? -1 : 0;
   }
   GemmArgs a{};
   a.A = act;
@@ -1142,6 +1229,11 @@ extern "C" int nad_device_forward(const void* act, int act_dtype, const void* de
   }
   hipStream_t st = static_cast<hipStream_t>(queue);
   if (m <= kSkinnyMaxM) {
+    if (!int8_compute(*w)) {  // the mid-M kernel where NAD_MID_MIN_M reaches below 17 (tests / tuning)
+      const int r = run_mid(act, act_dtype, lda, m, k, *w, out, ldo, epi, bias, bias_ld, res, ld_res, nullptr, 0, st,
+                            nullptr, nullptr);
+      if (r != 0) return r < 0 ? -1 : 0;
+    }
     float* outs[1] = {out};
     int ldos[1] = {ldo};
     const DeviceWeight* ws[1] = {w};

@@ -86,6 +86,7 @@ struct GemmArgs {
   _Float16* out16;
   int ldo16;
   const _Float16* aux16;
+  int tpg_shift;        // mid-M kernel, one group per K tile or more: log2(K tiles per group) (31: one group)
   SkinnyWeight w;
 };
 
@@ -200,6 +201,11 @@ hipError_t launch_gemm4(const GemmArgs& a, int bits, const _Float16* A16, int ld
 // split-K partials, fp16 A padded to the 128-deep tile) with the group scale folded (needs DeviceWeight::fold_ok)
 bool gemm7_ok(int bits, int blocksize, int fold_ok);
 hipError_t launch_gemm7(const GemmArgs& a, int bm, const _Float16* A16, int lda16, hipStream_t stream);
+// mid-M GEMM (woq_gemm_mid.hip, 17 <= M <= 64): int4 / int2, gpt groups per K tile (1, 2, 4), rf = ceil(M / 16) row
+// fragments; grid = ceil(ns / S) * a.ksplit for the S of mid_geometry; a.ksplit > 1: launch_splitk_reduce follows
+void mid_geometry(int bits, int gpt, int act_t, int rf, int* s, int* nw, int* spw);
+int mid_lds_bytes(int rf, int s, int nw);
+hipError_t launch_gemm_mid(const GemmArgs& a, int bits, int gpt, int act_t, int rf, int grid, hipStream_t stream);
 // sum a.ksplit partials of a split-K gemm3 / gemm4 launch in run order and apply a.epi into a.w.out (woq_gemm2.hip)
 hipError_t launch_splitk_reduce(const GemmArgs& a, hipStream_t stream);
 hipError_t launch_cvt_act(const void* A, int act_t, int lda, int M, int K, int Kp, const int32_t* shuffle,

@@ -186,7 +186,7 @@ def test_device_forward_uses_caller_workspace_and_capture_contract(oracle):
     nad_device_workspace_size); nad_device_forward under graph capture uses a bound workspace, and without one on a
     fresh stream it fails loudly instead of switching kernels."""
     L = _lib.lib()
-    n, k, m = 256, 1024, 64
+    n, k, m = 256, 1024, 100  # past the mid-M kernel (M <= 64 reads the activations as they are)
     blob = _wb(oracle, n, k, 5)
     w = bestla.DeviceWeight(blob)
     A = np.random.default_rng(1).uniform(-1, 1, size=(m, k)).astype(np.float32)

@@ -43,6 +43,7 @@ GEMM2_CASES = [
 @pytest.mark.parametrize("act", ["fp32", "fp16", "bf16"])
 def test_gemm_parity(oracle, knob, kernel, cfg, act):
     """gemm3 / gemm2 (held to FOLD_TOL when the launch folds the group scale, which nad_plan_weight reports)."""
+    knob("NAD_MID_MAX_M", "0")  # M <= 64 would take the mid-M kernel (tests/test_mid_gpu.py)
     knob("NAD_GEMM_KERNEL", kernel)
     m, n, k, bs, qt, st, asym, comp, shuf = cfg
     blob = _blob(oracle, n, k, bs, qt, st, asym, comp, seed=m + 3 * n + k, gidx=shuf)
@@ -65,6 +66,7 @@ def test_gemm_kernels_agree(oracle, knob):
     m, n, k = 700, 272, 1536
     blob = _blob(oracle, n, k, 128, S4, BF16, True, 4, seed=11)
     w = bestla.DeviceWeight(blob)
+    knob("NAD_GEMM_KERNEL", "3")  # the exact-scale kernels (gemm7, the default, folds: test_gemm_parity)
     x = (torch.rand((m, k), device="cuda") - 0.5).half()
     ref = oracle.forward(x.float().cpu().numpy(), blob, n, k)
     y3 = w.forward(x).cpu().numpy()
@@ -80,7 +82,7 @@ def test_gemm_kernels_agree(oracle, knob):
 
 
 def test_gemm_full_size_rows(oracle):
-    """BASELINE synthetic GEMM shape K = N = 4096 at M = 4096 (gemm3): oracle on sampled rows."""
+    """BASELINE synthetic GEMM shape K = N = 4096 at M = 4096 (gemm7, scale folded): oracle on sampled rows."""
     n = k = 4096
     blob = _blob(oracle, n, k, 128, S4, F16, False, 4, seed=42)
     w = bestla.DeviceWeight(blob)
@@ -88,7 +90,7 @@ def test_gemm_full_size_rows(oracle):
     y = w.forward(x).cpu().numpy()
     rows = np.random.default_rng(1).choice(4096, size=16, replace=False)
     ref = oracle.forward(x[rows].float().cpu().numpy(), blob, n, k)
-    assert _rel_err(y[rows], ref) <= 2e-5
+    assert _rel_err(y[rows], ref) <= (FOLD_TOL if w.plan(4096, "fp16")["fold"] else 2e-5)
 
 
 def test_gemm_strided_epilogues(oracle):
@@ -160,6 +162,7 @@ GEMM4_CASES = [
 @pytest.mark.parametrize("act", ["fp32", "fp16", "bf16"])
 def test_gemm4_parity(oracle, knob, cfg, act, ksw):
     """gemm4 against the oracle (NAD_GEMM4_KSW=1: folded launches with the waves split over K)."""
+    knob("NAD_MID_MAX_M", "0")
     knob("NAD_GEMM4_KSW", ksw)
     m, n, k, bs, qt, st, asym, comp = cfg
     blob = _blob(oracle, n, k, bs, qt, st, asym, comp, seed=m + 7 * n + k)
@@ -242,6 +245,7 @@ SPLITK_CASES = [
 @pytest.mark.parametrize("cfg", SPLITK_CASES)
 def test_gemm_splitk_parity(oracle, knob, cfg):
     """Split-K gemm3 against the oracle, and against the same GEMM without the split (fp32 sums in another order)."""
+    knob("NAD_MID_MAX_M", "0")
     m, n, k, bs, asym, act = cfg
     blob = _blob(oracle, n, k, bs, S4, F16, asym, 4, seed=m + n + k)
     w = bestla.DeviceWeight(blob)
@@ -251,10 +255,15 @@ def test_gemm_splitk_parity(oracle, knob, cfg):
         x = x.to(torch.float16 if act == "fp16" else torch.bfloat16)
     ref = oracle.forward(x.float().cpu().numpy(), blob, n, k)
     y = w.forward(x).cpu().numpy()
-    assert _rel_err(y, ref) <= TOL[act], (_rel_err(y, ref), act)
+    tol = max(TOL[act], FOLD_TOL) if w.plan(m, act)["fold"] else TOL[act]  # gemm7 folds the scale (fp16 weights)
+    assert _rel_err(y, ref) <= tol, (_rel_err(y, ref), act)
     knob("NAD_SPLITK_DISABLE", "1")
     y1 = w.forward(x).cpu().numpy()
     assert _rel_err(y, y1.astype(np.float64)) <= 2e-5
+    knob("NAD_SPLITK_DISABLE", "0")
+    knob("NAD_GEMM_KERNEL", "3")  # the exact-scale gemm3 split-K path at the exact bar
+    y3 = w.forward(x).cpu().numpy()
+    assert _rel_err(y3, ref) <= TOL[act], (_rel_err(y3, ref), act)
 
 
 def test_gemm_splitk_epilogues(oracle):
@@ -298,6 +307,7 @@ SPLITK4_CASES = [
 @pytest.mark.parametrize("cfg", SPLITK4_CASES)
 def test_gemm4_splitk_parity(oracle, knob, cfg):
     m, n, k, bs, qt, asym, act = cfg
+    knob("NAD_MID_MAX_M", "0")
     blob = _blob(oracle, n, k, bs, qt, F16, asym, 4, seed=m + 3 * n + k)
     w = bestla.DeviceWeight(blob)
     A = np.random.default_rng(m + 5).uniform(-0.5, 0.5, size=(m, k)).astype(np.float32)
@@ -354,6 +364,9 @@ def test_gemm_mid_m(oracle, knob, m, fmt):
     plan = w.plan(m, "fp16")
     y = w.forward(x).cpu().numpy()
     assert _rel_err(y, ref) <= (FOLD_TOL if plan["fold"] else TOL["fp16"]), (_rel_err(y, ref), plan)
+    if m <= (64 if qt == S4 else 32):  # the mid-M kernel (exact scales; tests/test_mid_gpu.py)
+        assert plan["kernel"] == "woq_mid_kernel", plan
+        return
     if qt == S4:
         assert plan["kernel"] == "woq_gemm7_kernel" and plan["ksplit"] > 1, plan
         knob("NAD_GEMM_KERNEL", "3")
