@@ -212,7 +212,7 @@ def test_host_cache_key_is_constant_time_at_lm_head_shape():
 
 def test_plan_forward_kernel_choice():
     """nad_plan_forward (the host side of nad_device_forward with every launch recorded, no GPU): the decode shapes take
-    the M = 1 / stripe-stream GEMVs, prefill takes gemm7 (int4 g128, the scale folded; gemm3 under NAD_GEMM_KERNEL=3)
+    the M = 1 / stripe-stream GEMVs, 17 <= M <= 64 the mid-M kernel, prefill takes gemm7 (int4 g128, the scale folded; gemm3 under NAD_GEMM_KERNEL=3)
     or gemm4 (g32 / g64 with the scale folded, int2, int8), and few output tiles split K."""
     p = bestla.plan_forward
     assert p(4, 4096, 4096, 128, m=1)["kernel"] == "woq_gemv_m1_kernel"
@@ -225,7 +225,14 @@ def test_plan_forward_kernel_choice():
     for bits, g in ((4, 32), (4, 64), (2, 64)):
         r = p(bits, 4096, 4096, g, m=2048)
         assert (r["kernel"], r["fold"]) == ("woq_gemm4_kernel", True), (bits, g, r)
-    r = p(4, 4096, 4096, 128, m=64)
+    r = p(4, 4096, 4096, 128, m=64)                 # mid-M: fp32 activations read as they are, + the split-K reduce
+    assert (r["kernel"], r["fold"], r["ksplit"], r["launches"]) == ("woq_mid_kernel", False, 4, 2), r
+    r = p(4, 4096, 4096, 128, m=17, act="fp16")
+    assert (r["kernel"], r["grid"], r["threads"]) == ("woq_mid_kernel", 256, 256), r
+    assert p(4, 11008, 4096, 128, m=32)["ksplit"] == 2      # slabs within the workspace bound: ks x N <= 32768
+    assert p(4, 32000, 4096, 128, m=32)["ksplit"] == 1
+    assert p(2, 4096, 4096, 64, m=33)["kernel"] == "woq_gemm4_kernel"   # int2 past 32 rows: the prefill GEMM
+    r = p(4, 4096, 4096, 128, m=65)
     assert r["kernel"] == "woq_gemm7_kernel" and r["ksplit"] > 1 and r["launches"] == 3   # + the split-K reduce
     # int8 / int2 at g128 fold too (NAD_GEMM4_FOLD_ALL default since round 4)
     assert p(8, 4096, 4096, 128, m=2048)["fold"] and p(2, 4096, 4096, 128, m=2048)["fold"]
