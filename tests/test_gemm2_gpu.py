@@ -372,3 +372,4 @@ def test_gemm_mid_m(oracle, knob, m, fmt):
         knob("NAD_GEMM_KERNEL", "3")
         y3 = w.forward(x).cpu().numpy()
         assert _rel_err(y, y3.astype(np.float64)) <= FOLD_TOL
+

@@ -2,7 +2,7 @@
 
 Usage: python tools/gemm_sweep.py [--m 2048,4096] [--act fp16,fp32] [--shapes o,gate,down,lm_head] [--reps 20]
        [--kernels 3,2] [--bits 4] [--group 128] [--asym]
-Kernels: 3 / 2 = the int4 pipelined kernels, suffix k = gemm4 waves split over K (j: the library's auto choice), a = int4 g128 on gemm4 too, f / u = fold at g128 on / off (default: the library's), 4 = gemm4 (int4 g32/g64, int2), 0 = generic tiled fallback.
+Kernels: 7 / 3 / 2 = the int4 pipelined kernels, suffix k = gemm4 waves split over K (j: the library's auto choice), a = int4 g128 on gemm4 too, f / u = fold at g128 on / off (default: the library's), 4 = gemm4 (int4 g32/g64, int2), 0 = generic tiled fallback.
 Each line: shape, M, activation dtype, kernel, average device time per forward (HIP events on the launch stream, back
 to back launches) and TFLOP/s (2*M*N*K / time).  fp32 activations include the one-pass fp16 conversion kernel.
 """

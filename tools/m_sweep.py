@@ -23,12 +23,13 @@ def main():
     ap.add_argument("--bits", type=int, default=4)
     ap.add_argument("--group", type=int, default=128)
     ap.add_argument("--reps", type=int, default=32)
+    ap.add_argument("--mb", type=float, default=400.0, help="MB of rotated weight copies (past 256 MB: cold)")
     args = ap.parse_args()
     import torch
     from neural_amd import bestla
     n, k, g, bits = args.n, args.k, args.group, args.bits
     wb = n * k * bits // 8 + n * math.ceil(k / g) * 2
-    copies = max(2, math.ceil(400e6 / wb))
+    copies = max(2, math.ceil(args.mb * 1e6 / wb))
     ws = [bestla.DeviceWeight.synthetic(bits, n, k, g, "fp16", False, seed=77 + i) for i in range(copies)]
     dt = {"fp16": torch.float16, "fp32": torch.float32, "bf16": torch.bfloat16}[args.act]
     esz = torch.tensor([], dtype=dt).element_size()
