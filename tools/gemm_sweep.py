@@ -26,12 +26,17 @@ def main():
     ap.add_argument("--bits", type=int, default=4)
     ap.add_argument("--group", type=int, default=128)
     ap.add_argument("--asym", action="store_true")
+    ap.add_argument("--nk", default="", help="extra N:K shapes, comma separated (named nNkK)")
     args = ap.parse_args()
     import torch
     from neural_amd import _lib, bestla
     dev = torch.device("cuda:0")
     print(torch.cuda.get_device_name(0), flush=True)
-    for name in args.shapes.split(","):
+    for nk in filter(None, args.nk.split(",")):
+        n_, k_ = (int(v) for v in nk.split(":"))
+        SHAPES[f"n{n_}k{k_}"] = (n_, k_)
+    names = args.shapes.split(",") + [f"n{n_}k{k_}" for n_, k_ in (map(int, nk.split(":")) for nk in filter(None, args.nk.split(",")))]
+    for name in filter(None, names):
         n, k = SHAPES[name]
         w = bestla.DeviceWeight.synthetic(args.bits, n, k, args.group, "fp16", args.asym, seed=3)
         for m in (int(x) for x in args.m.split(",")):
