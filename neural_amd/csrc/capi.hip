@@ -82,7 +82,7 @@ static Knobs read_knobs() {
   k.gemm4_ksw = env_int("NAD_GEMM4_KSW", 2);  // folded gemm4 launches with the waves split over K: 0 off, 1 on, 2 auto
   k.mid_max_m = env_int("NAD_MID_MAX_M", 64);  // mid-M kernel (woq_gemm_mid.hip) up to this M (0: off)
   k.mid_ks = env_int("NAD_MID_KS", 0);         // tests / tuning: its K runs (0 auto)
-  k.mid_min_m = env_int("NAD_MID_MIN_M", 17);  // ... from this M (tests / tuning: below 17 the GEMV)
+  k.mid_min_m = env_int("NAD_MID_MIN_M", 0);  // ... from this M (0 auto: 12 rows of fp16 activations, 8 of fp32 / bf16)
   k.host_cache_mb = env_int("NAD_HOST_CACHE_MB", 64 * 1024);
   return k;
 }
@@ -1020,7 +1020,11 @@ static int run_mid(const void* act, int act_t, int lda, int m, int k, const Devi
                    int epi, const float* bias, int bias_ld, const float* res, int ld_res, const float* aux, int ld_aux,
                    hipStream_t st, const A16* pre, const Half16* h16) {
   const Knobs& kn = knobs();
-  if (m > kn.mid_max_m || m < kn.mid_min_m) return 0;
+  // from 12 rows (fp16; 8 for fp32 / bf16, which the GEMV stages as two fp16 rows each) the mid-M kernel beats the
+  // stripe-stream GEMV: K = N = 4096 M = 16 8.3 vs 10.1 us (fp16), 9.0 vs 12.7 (fp32); N = 11008 fp32 M = 16 17.7 vs
+  // 36.7 (profiles/r05_mid_small_m.txt)
+  const int min_m = kn.mid_min_m > 0 ? kn.mid_min_m : (act_t == kActF16 ? 12 : 8);
+  if (m > kn.mid_max_m || m < min_m) return 0;
   if ((w.bits != 4 && w.bits != 2) || w.kmajor || w.f4kind >= 0 || w.shuffle) return 0;
   if (w.bits == 2 && m > 32) return 0;  // a 256-deep int2 stage's activation fragments: 32 rows fit the registers
   int tpg = 0;

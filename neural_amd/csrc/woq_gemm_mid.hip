@@ -99,25 +99,25 @@ __device__ __forceinline__ f4_t scale4(const u4_t& x, bool bf16) {
   }
   return r;
 }
-// 8 activations (raw 16 or 32 bytes) -> the fp16 A fragment (fp32 / bf16 rounded once to fp16, as the prefill GEMMs)
+// 8 activations (raw 16 or 32 bytes) -> the fp16 fragment; fp32 / bf16 values split as hi = fp16(a), lo = fp16(a - hi)
+// (two MFMAs: products accurate to fp32, as the decode GEMV does)
+__device__ __forceinline__ float a_val(int at, const u4_t& x0, const u4_t& x1, int e) {
+  if (at == kActF32) return __uint_as_float(e < 4 ? x0[e] : x1[e - 4]);
+  const uint32_t w = x0[e >> 1];
+  return __uint_as_float((e & 1) ? (w & 0xFFFF0000u) : (w << 16));
+}
 template <int AT>
-__device__ __forceinline__ h8_t a_frag(const u4_t& x0, const u4_t& x1) {
-  if constexpr (AT == kActF16) return __builtin_bit_cast(h8_t, x0);
-  h8_t r;
-  if constexpr (AT == kActF32) {
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-      r[j] = _Float16(__uint_as_float(x0[j]));
-      r[4 + j] = _Float16(__uint_as_float(x1[j]));
-    }
+__device__ __forceinline__ void a_frag(const u4_t& x0, const u4_t& x1, h8_t& hi, h8_t& lo) {
+  if constexpr (AT == kActF16) {
+    hi = __builtin_bit_cast(h8_t, x0);
   } else {
 #pragma unroll
-    for (int j = 0; j < 4; j++) {
-      r[2 * j] = _Float16(__uint_as_float(x0[j] << 16));
-      r[2 * j + 1] = _Float16(__uint_as_float(x0[j] & 0xFFFF0000u));
+    for (int e = 0; e < 8; e++) {
+      const float f = a_val(AT, x0, x1, e);
+      hi[e] = _Float16(f);
+      lo[e] = _Float16(f - float(hi[e]));
     }
   }
-  return r;
 }
 
 // BITS 4 / 2 (K tile 128 / 256), GPT groups per K tile (1, 2, 4), RF row fragments (M <= 16 RF), S stripes per
@@ -234,10 +234,12 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW / 4,
         }
 #pragma unroll
         for (int i = 0; i < RF; i++) {
-          const h8_t af = a_frag<AT>(av[j][i][d][0], av[j][i][d][AL - 1]);
+          h8_t af, afl;
+          a_frag<AT>(av[j][i][d][0], av[j][i][d][AL - 1], af, afl);
           // operands swapped (C^T = B^T A^T): lane l gets rows 4 (l >> 4) .. + 3 of C^T = 4 consecutive columns
           tmp[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf, af, d % SPG == 0 ? f4_t{0.f, 0.f, 0.f, 0.f} : tmp[i], 0,
                                                           0, 0);
+          if constexpr (AT != kActF16) tmp[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf, afl, tmp[i], 0, 0, 0);
         }
         if ((d + 1) % SPG == 0) {
           const f4_t scl = scale4<SF32>(sc[j][s][g], sbf16);
@@ -337,35 +339,33 @@ static hipError_t mid_go(const GemmArgs& a, int grid, hipStream_t st) {
   return hipGetLastError();
 }
 
-// Geometry per format: 4 stripes per workgroup; NW waves x SPW stages (K tiles) per wave.
-//   int4, fp16 activations: 4 x 2; fp32 / bf16: 8 x 1 (a stage's raw fp32 rows fill two waves' register budget per SIMD)
-//   int2 (256-deep tiles: 8 steps of activation fragments per stage), and int4 with 2 groups per tile at M > 32 (their
-//   scale / zero-point registers): 4 x 1.  Not taken: int2 at M > 32, int4 with 4 groups per tile (g32) at M > 32.
+// Geometry per format: 4 stripes per workgroup, 4 waves (one per SIMD: a stage's raw fp32 activation rows, hi / lo
+// fragments and 64 accumulators need more than two waves' register budget); int4 2 stages (K tiles) per wave, 1 for
+// groups finer than a tile at M > 32 (their scale / zero-point registers); int2 (256-deep tiles, 8 steps of activation
+// fragments per stage) 1.  Not taken: int2 at M > 32, int4 with 4 groups per tile (g32) at M > 32.
 void mid_geometry(int bits, int gpt, int act_t, int rf, int* s, int* nw, int* spw) {
+  (void)act_t;
   *s = 4;
-  if (bits == 4 && (rf <= 2 || gpt == 1)) {
-    *nw = act_t == kActF16 ? 4 : 8;
-    *spw = act_t == kActF16 ? 2 : 1;
-  } else {  // int2, and int4 with finer groups at M > 32 (their scale / zero-point registers): 4 waves x 1 stage
-    *nw = 4;
-    *spw = 1;
-  }
+  *nw = 4;
+  *spw = bits == 4 && (rf <= 2 || gpt == 1) ? 2 : 1;
 }
 
 template <int BITS, int GPT, bool ASYM, int AT>
 static hipError_t mid_rf(const GemmArgs& a, int rf, int grid, hipStream_t st) {
   if constexpr (BITS == 4) {
-    constexpr int NW = AT == kActF16 ? 4 : 8, SPW = AT == kActF16 ? 2 : 1;
-    constexpr int NW3 = GPT == 1 ? NW : 4, SPW3 = GPT == 1 ? SPW : 1;  // M > 32
+    constexpr int SPW3 = GPT == 1 ? 2 : 1;  // M > 32
     switch (rf) {
       case 1:
-        return mid_go<BITS, GPT, ASYM, AT, 1, 4, NW, SPW>(a, grid, st);
+        return mid_go<BITS, GPT, ASYM, AT, 1, 4, 4, 2>(a, grid, st);
       case 2:
-        return mid_go<BITS, GPT, ASYM, AT, 2, 4, NW, SPW>(a, grid, st);
-      case 3:
-        return mid_go<BITS, GPT, ASYM, AT, 3, 4, NW3, SPW3>(a, grid, st);
+        return mid_go<BITS, GPT, ASYM, AT, 2, 4, 4, 2>(a, grid, st);
       default:
-        return mid_go<BITS, GPT, ASYM, AT, 4, 4, NW3, SPW3>(a, grid, st);
+        if constexpr (GPT == 4) {
+          return hipErrorInvalidValue;  // g32 at M > 32: not taken (run_mid)
+        } else {
+          return rf == 3 ? mid_go<BITS, GPT, ASYM, AT, 3, 4, 4, SPW3>(a, grid, st)
+                         : mid_go<BITS, GPT, ASYM, AT, 4, 4, 4, SPW3>(a, grid, st);
+        }
     }
   } else {
     // int2 (8 steps of activation fragments per 256-deep stage): M <= 32 only (run_mid)

@@ -217,7 +217,10 @@ def test_plan_forward_kernel_choice():
     p = bestla.plan_forward
     assert p(4, 4096, 4096, 128, m=1)["kernel"] == "woq_gemv_m1_kernel"
     assert p(2, 14336, 4096, 64, m=1)["kernel"] == "woq_gemv_m1_kernel"
-    assert p(4, 4096, 4096, 128, m=8)["kernel"] == "woq_gemv_kernel"
+    assert p(4, 4096, 4096, 128, m=4)["kernel"] == "woq_gemv_kernel"
+    assert p(4, 4096, 4096, 128, m=8, act="fp16")["kernel"] == "woq_gemv_kernel"
+    assert p(4, 4096, 4096, 128, m=8)["kernel"] == "woq_mid_kernel"       # fp32 rows: the mid-M kernel from 8
+    assert p(4, 4096, 4096, 128, m=12, act="fp16")["kernel"] == "woq_mid_kernel"
     r = p(4, 4096, 4096, 128, m=2048)
     assert (r["kernel"], r["fold"], r["ksplit"]) == ("woq_gemm7_kernel", True, 1)
     assert r["launches"] == 2                       # fp32 activations: one fp16 conversion pass, then the GEMM

@@ -291,6 +291,7 @@ def test_gemv_stream_geometry(oracle, knob, cfg, geom):
     """The persistent stripe-stream GEMV with forced grids / wave counts: workgroups owning many stripes, wave ranges
     crossing stripe and group boundaries, single-wave workgroups.  Same bar as the default launch."""
     grid, waves = geom
+    knob("NAD_MID_MAX_M", "0")  # M >= 8 would take the mid-M kernel (tests/test_mid_gpu.py)
     if grid:
         knob("NAD_GEMV_GRID", grid)
         knob("NAD_GEMV_WAVES", waves)

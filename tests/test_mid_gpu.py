@@ -1,12 +1,12 @@
-"""The mid-M GEMM (woq_gemm_mid.hip, 17 <= M <= 64): operands straight to registers, the split-K runs' slabs summed in
-run order by the reduce launch.
+"""The mid-M GEMM (woq_gemm_mid.hip, 12 (fp16) / 8 (fp32, bf16) <= M <= 64): operands straight to registers, the
+split-K runs' slabs summed in run order by the reduce launch.
 
 Against the oracle (fp64 GEMM on the reference's dequantized weights, bestla_wrapper.h:471-542 semantics) on the
 formats the kernel takes (int4 / int2, sym / asym, groups of 32 .. per-channel, fp32 / fp16 / bf16 scales), ragged M / N,
 K tails, every activation type and the epilogues; bit-identical across repeated launches and under graph replay.
 
-Tolerances: the group scale is applied exactly in fp32 (as the decode GEMV); the activations are rounded once to fp16
-(fp32 / bf16 inputs), so the bars are the prefill GEMMs' exact-scale ones (tests/test_gemm2_gpu.py TOL).
+Tolerance: the decode GEMV's -- the group scale is applied exactly in fp32 and fp32 / bf16 activations enter as fp16
+hi + lo rows (two MFMAs), so every activation type is held to 2e-5 of max|ref|.
 """
 import numpy as np
 import pytest
@@ -21,7 +21,7 @@ if gpu_available():
     import torch
     from neural_amd import bestla
 
-TOL = {"fp32": 1e-3, "fp16": 2e-5, "bf16": 1e-4}
+TOL = {"fp32": 2e-5, "fp16": 2e-5, "bf16": 2e-5}
 
 MID_CASES = [
     # m, n, k, bs, qtype, stype, asym
@@ -137,7 +137,7 @@ def test_mid_fused_qkv_ffn(oracle):
     h1 = oracle.forward(A, b1, fmid, fin).astype(np.float64)
     h3 = oracle.forward(A, b3, fmid, fin).astype(np.float64)
     ref = oracle.forward((h1 / (1 + np.exp(-h1)) * h3).astype(np.float32), b2, fout, fmid)
-    assert _rel_err(y, ref) <= 2 * TOL["fp32"]
+    assert _rel_err(y, ref) <= 2e-3  # the FFN's intermediates (fp16 at M > 16) dominate
 
 
 def test_mid_graph_replay(oracle):
@@ -167,7 +167,7 @@ def test_mid_graph_replay(oracle):
 
 @pytest.mark.parametrize("m", [2, 5, 8, 13, 16])
 def test_mid_small_m(oracle, knob, m):
-    """Below 17 rows (NAD_MID_MIN_M lowered; the GEMV serves them by default): the one-fragment tile with zero rows."""
+    """Below the default threshold (NAD_MID_MIN_M=1): the one-fragment tile with zero rows, at the decode bar."""
     n, k = 1024, 4096
     blob = _blob(oracle, n, k, 128, S4, F16, False, 4, seed=m)
     w = bestla.DeviceWeight(blob)
