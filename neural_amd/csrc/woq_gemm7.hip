@@ -28,14 +28,23 @@ namespace g7 {
 
 constexpr int KT = 128, ROWB = 128;  // ROWB: bytes of one A row per 64-deep half step
 constexpr int NS = 8;                // stripes per tile (128 columns)
-constexpr int BTILES = NS * 1024, BSC = 512, BZP = 512;
-constexpr int BBUF = BTILES + BSC + BZP;  // one K tile of B + scale and zero-point dwords
-constexpr int EPI_LD = 36;                // epilogue transpose row stride (floats)
+constexpr int BTILES = NS * 1024;
+constexpr int EPI_LD = 36;           // epilogue transpose row stride (floats)
+
+// One K tile of B with its scale and zero-point bytes as they lie in HBM ([stripe][group][16 columns]): GPT groups per
+// tile (4 at groups of 32, 2 at 64, 1 from 128 up), each region at least one 256-byte LDS-DMA piece
+template <int GPT, int ST, bool ASYM>
+struct Bbuf {
+  static constexpr int ESZ = ST == kScaleF32 ? 4 : 2;
+  static constexpr int SCT = NS * GPT * 16 * ESZ, ZPT = NS * GPT * 16;  // bytes a tile uses
+  static constexpr int SCR = SCT > 256 ? SCT : 256, ZPR = ASYM ? (ZPT > 256 ? ZPT : 256) : 0;
+  static constexpr int BYTES = BTILES + SCR + ZPR;
+};
 
 // Geometry per tile height BMT (32, 64, 128, 256 rows; every wave covers all of them): the A ring runs DA = NA - 1 half
 // steps ahead -- deeper for the short tiles, whose K runs are split-K runs of a few tiles -- and the B ring holds a
 // tile no shorter than the two half steps after its last read.
-template <int BMT>
+template <int BMT, int BBUF>
 struct Geo {
   static constexpr int RF = BMT / 16;                  // row fragments per wave
   static constexpr int HF = RF / 2;                    // fragments per half of the register rotation
@@ -147,17 +156,19 @@ __device__ __forceinline__ h8_t dequant_fold(uint32_t w, uint32_t mag, h2_t s16,
 // every M-wave) 3-35 % slower than this one (profiles/r05_gemm8_tile_shapes_sweep.txt).  BMT < 256 serves 17 <= M <= 256
 // with split-K runs (the mid-M range): the tile's rows are what the problem has, not 256 rows of which most re-read the
 // last one.
-template <int BMT, bool ASYM, int ST>
+template <int BMT, bool ASYM, int ST, int GPT>
 __global__ __launch_bounds__(512, 1) void woq_gemm7_kernel(GemmArgs a, const _Float16* __restrict__ A16, int lda16) {
-  using G = Geo<BMT>;
+  using BB = Bbuf<GPT, ST, ASYM>;
+  using G = Geo<BMT, BB::BYTES>;
   constexpr int RF = G::RF, HF = G::HF, HBUF = G::HBUF, PA = G::PA, NA = G::NA, DA = G::DA, NBR = G::NBR;
+  constexpr int BBUF = BB::BYTES, BSC = BB::SCR, ESZ = BB::ESZ;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));
   const int wn = wave & 3, wk = wave >> 2;
   const SkinnyWeight& W = a.w;
   const int M = a.M, nt = W.nt, ng = W.ng, ns = W.ns;
-  const int tpg = W.bs / KT;
+  const int tpg = W.bs >= KT ? W.bs / KT : 1;
   const int tsh = __builtin_ctz(unsigned(tpg));
 
   // XCD-aware remap (one XCD walks the N tiles of one (M tile, K run)) and split-K runs, as gemm3
@@ -195,12 +206,22 @@ __global__ __launch_bounds__(512, 1) void woq_gemm7_kernel(GemmArgs a, const _Fl
   const auto rb = brsrc(static_cast<const char*>(W.tiles) + size_t(kt0) * 1024);
   const auto rnull = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(W.tiles), 0, 0, 0x00020000);
   const uint32_t boffd = (uint32_t(min(bn * NS + wave, ns - 1)) * nt * 64 + lane) * 16;
-  const int sstripe = min(bn * NS + (wave & 1) * 4 + (lane >> 4), ns - 1);
-  const uint32_t srow0 = uint32_t(sstripe) * ng * 16 + nl + uint32_t(kt0 >> tsh) * 16;
+  // scale / zero-point pieces: wave w copies 256-byte piece w % pieces of the tile's region; lane bytes past the tile's
+  // share (a region rounded up to one piece) re-read its start into the unused tail
   constexpr int st = ST;
   const auto rs = brsrc(W.scales);
   const auto rz = brsrc(W.zps);
-  const uint32_t svo = st == kScaleF32 ? srow0 * 4 : (srow0 >> 1) * 4, zvo = (srow0 >> 2) * 4;
+  const uint32_t g0 = GPT > 1 ? uint32_t(kt0) * GPT : uint32_t(kt0 >> tsh);  // first group of the K run
+  auto piece_off = [&](int pieces, int total, int esz, int* dst) {
+    const int p = wave % pieces;
+    *dst = p * 256;
+    const int o = (p * 256 + lane * 4) % total, chunk = GPT * 16 * esz;
+    const int s = min(bn * NS + o / chunk, ns - 1);
+    return (uint32_t(s) * ng * 16 + g0 * 16) * esz + uint32_t(o % chunk);
+  };
+  int sdst = 0, zdst = 0;
+  const uint32_t svo = piece_off(BB::SCR / 256, BB::SCT, ESZ, &sdst);
+  const uint32_t zvo = ASYM ? piece_off(BB::ZPR / 256, BB::ZPT, 1, &zdst) : 0u;
 
   // batch(u): A(u + DA) and, when u + DA is even, B tile (u + DA) / 2 with its scale / zero-point pieces
   auto issue = [&](int u) {
@@ -214,9 +235,9 @@ __global__ __launch_bounds__(512, 1) void woq_gemm7_kernel(GemmArgs a, const _Fl
       const int t = ua >> 1;
       char* bb = smem + NA * HBUF + (t % NBR) * BBUF;
       blds16(live ? rb : rnull, boffd, uint32_t(t) * 1024, bb + wave * 1024);
-      const uint32_t g = uint32_t(t >> tsh) * 16;
-      blds4(live ? rs : rnull, svo, st == kScaleF32 ? g * 4 : g * 2, bb + BTILES + (wave & 1) * 256);
-      if constexpr (ASYM) blds4(live ? rz : rnull, zvo, g, bb + BTILES + BSC + (wave & 1) * 256);
+      const uint32_t g = (GPT > 1 ? uint32_t(t) * GPT : uint32_t(t >> tsh)) * 16;
+      blds4(live ? rs : rnull, svo, g * ESZ, bb + BTILES + sdst);
+      if constexpr (ASYM) blds4(live ? rz : rnull, zvo, g, bb + BTILES + BSC + zdst);
     }
   };
   // at the barrier of buffer u + 1 (the middle of half step u), batch(u + 1 - DA) has landed and batches
@@ -230,8 +251,13 @@ __global__ __launch_bounds__(512, 1) void woq_gemm7_kernel(GemmArgs a, const _Fl
   const h2_t zc0 = splat(-(1024.f + 8.f)), zc1 = splat(-(64.f + 8.f));
   const uint32_t roff = uint32_t(nl * ROWB + (((wk * 4 + kq) ^ ((nl >> 1) & 7)) * 16));
   const int boff = (wn * 2) * 1024 + lane * 16 + wk * 4;
-  const int soff = BTILES + ((wn * 2) * 16 + nl) * 4;
-  const int zoff = BTILES + BSC + ((wn * 2) * 16 + nl) * 4;
+  // this lane's scale / zero-point dword for stripe 2 wn (+ SJ for 2 wn + 1) at its first 32-deep step of the tile; the
+  // step's group moves it by SH per half step
+  const int gw = GPT == 4 ? wk : 0;
+  const int soff = BTILES + ((((wn * 2) * GPT + gw) * 16 + nl) * ESZ & ~3);
+  const int zoff = BTILES + BSC + ((((wn * 2) * GPT + gw) * 16 + nl) & ~3);
+  constexpr int SJ = GPT * 16 * ESZ, ZJ = GPT * 16;
+  constexpr int SH = GPT == 4 ? 2 * 16 * ESZ : (GPT == 2 ? 16 * ESZ : 0), ZH = SH / ESZ;
   const int ssh = st == kScaleF32 ? 0 : (nl & 1) * 16;
   const int zsh = (nl & 3) * 8;
   auto scale_h2 = [&](uint32_t x) {
@@ -261,12 +287,12 @@ __global__ __launch_bounds__(512, 1) void woq_gemm7_kernel(GemmArgs a, const _Fl
     const uint32_t bl = lds_addr(smem + NA * HBUF + (t % NBR) * BBUF);
     bw0 = lds_b32<H * 8>(bl + boff);
     bw1 = lds_b32<1024 + H * 8>(bl + boff);
-    if constexpr (H == 0) {
-      sw0 = lds_b32<0>(bl + soff);
-      sw1 = lds_b32<64>(bl + soff);
+    if constexpr (H == 0 || GPT > 1) {
+      sw0 = lds_b32<H * SH>(bl + soff);
+      sw1 = lds_b32<H * SH + SJ>(bl + soff);
       if constexpr (ASYM) {
-        zw0 = lds_b32<0>(bl + zoff);
-        zw1 = lds_b32<64>(bl + zoff);
+        zw0 = lds_b32<H * ZH>(bl + zoff);
+        zw1 = lds_b32<H * ZH + ZJ>(bl + zoff);
       }
     }
     const uint32_t al = lds_addr(smem + (u % NA) * HBUF) + roff;
@@ -278,7 +304,7 @@ __global__ __launch_bounds__(512, 1) void woq_gemm7_kernel(GemmArgs a, const _Fl
   };
   auto dequant = [&](auto Hc) {
     constexpr int H = decltype(Hc)::value;
-    if constexpr (H == 0) {
+    if constexpr (H == 0 || GPT > 1) {
       sc[0] = scale_h2(sw0);
       sc[1] = scale_h2(sw1);
       if constexpr (ASYM) {
@@ -405,7 +431,7 @@ __global__ __launch_bounds__(512, 1) void woq_gemm7_kernel(GemmArgs a, const _Fl
 
 bool gemm7_ok(int bits, int blocksize, int fold_ok) {
   const int tpg = blocksize / g7::KT;
-  return bits == 4 && fold_ok && blocksize % g7::KT == 0 && (tpg & (tpg - 1)) == 0;
+  return bits == 4 && fold_ok && (blocksize == 32 || blocksize == 64 || (blocksize % g7::KT == 0 && (tpg & (tpg - 1)) == 0));
 }
 
 hipError_t launch_gemm7(const GemmArgs& a, int bm, const _Float16* A16, int lda16, hipStream_t st) {
@@ -421,23 +447,34 @@ hipError_t launch_gemm7(const GemmArgs& a, int bm, const _Float16* A16, int lda1
     hipLaunchKernelGGL(k, grid, dim3(512), lds, st, a, A16, lda16);
     return hipGetLastError();
   };
+  const int gpt = a.w.bs == 32 ? 4 : (a.w.bs == 64 ? 2 : 1);
   auto pick = [&](auto bmc) -> hipError_t {
     constexpr int BMT = decltype(bmc)::value;
-    constexpr int L = g7::Geo<BMT>::LDS;
-    static bool attr[2][3] = {};
+    static bool attr[3][2][3] = {};
     const bool asym = a.w.zps != nullptr;
-    bool& d = attr[asym][a.scale_t];
-    switch (a.scale_t) {
-      case kScaleF32:
-        return asym ? go(g7::woq_gemm7_kernel<BMT, true, kScaleF32>, L, d)
-                    : go(g7::woq_gemm7_kernel<BMT, false, kScaleF32>, L, d);
-      case kScaleBF16:
-        return asym ? go(g7::woq_gemm7_kernel<BMT, true, kScaleBF16>, L, d)
-                    : go(g7::woq_gemm7_kernel<BMT, false, kScaleBF16>, L, d);
-      default:
-        return asym ? go(g7::woq_gemm7_kernel<BMT, true, kScaleF16>, L, d)
-                    : go(g7::woq_gemm7_kernel<BMT, false, kScaleF16>, L, d);
-    }
+    const int gi = gpt == 4 ? 2 : gpt - 1;
+    bool& d = attr[gi][asym][a.scale_t];
+    auto sel = [&](auto asc, auto stc, auto gc) {
+      constexpr bool AS = decltype(asc)::value;
+      constexpr int STT = decltype(stc)::value, GP = decltype(gc)::value;
+      return go(g7::woq_gemm7_kernel<BMT, AS, STT, GP>, g7::Geo<BMT, g7::Bbuf<GP, STT, AS>::BYTES>::LDS, d);
+    };
+    auto by_gpt = [&](auto asc, auto stc) {
+      return gpt == 4   ? sel(asc, stc, std::integral_constant<int, 4>{})
+             : gpt == 2 ? sel(asc, stc, std::integral_constant<int, 2>{})
+                        : sel(asc, stc, std::integral_constant<int, 1>{});
+    };
+    auto by_st = [&](auto asc) {
+      switch (a.scale_t) {
+        case kScaleF32:
+          return by_gpt(asc, std::integral_constant<int, kScaleF32>{});
+        case kScaleBF16:
+          return by_gpt(asc, std::integral_constant<int, kScaleBF16>{});
+        default:
+          return by_gpt(asc, std::integral_constant<int, kScaleF16>{});
+      }
+    };
+    return asym ? by_st(std::true_type{}) : by_st(std::false_type{});
   };
   switch (bm) {
     case 32:

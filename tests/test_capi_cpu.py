@@ -213,7 +213,7 @@ def test_host_cache_key_is_constant_time_at_lm_head_shape():
 def test_plan_forward_kernel_choice():
     """nad_plan_forward (the host side of nad_device_forward with every launch recorded, no GPU): the decode shapes take
     the M = 1 / stripe-stream GEMVs, 17 <= M <= 64 the mid-M kernel, prefill takes gemm7 (int4 g128, the scale folded; gemm3 under NAD_GEMM_KERNEL=3)
-    or gemm4 (g32 / g64 with the scale folded, int2, int8), and few output tiles split K."""
+    or gemm4 (int2, int8), int4 g32 / g64 gemm7 as well, and few output tiles split K."""
     p = bestla.plan_forward
     assert p(4, 4096, 4096, 128, m=1)["kernel"] == "woq_gemv_m1_kernel"
     assert p(2, 14336, 4096, 64, m=1)["kernel"] == "woq_gemv_m1_kernel"
@@ -225,9 +225,11 @@ def test_plan_forward_kernel_choice():
     assert (r["kernel"], r["fold"], r["ksplit"]) == ("woq_gemm7_kernel", True, 1)
     assert r["launches"] == 2                       # fp32 activations: one fp16 conversion pass, then the GEMM
     assert p(4, 4096, 4096, 128, m=2048, act="fp16")["launches"] == 1
-    for bits, g in ((4, 32), (4, 64), (2, 64)):
+    for bits, g in ((4, 32), (4, 64)):              # int4 g32 / g64: gemm7 with the scale per 32-deep step
         r = p(bits, 4096, 4096, g, m=2048)
-        assert (r["kernel"], r["fold"]) == ("woq_gemm4_kernel", True), (bits, g, r)
+        assert (r["kernel"], r["fold"]) == ("woq_gemm7_kernel", True), (bits, g, r)
+    r = p(2, 4096, 4096, 64, m=2048)
+    assert (r["kernel"], r["fold"]) == ("woq_gemm4_kernel", True), r
     r = p(4, 4096, 4096, 128, m=64)                 # mid-M: fp32 activations read as they are, + the split-K reduce
     assert (r["kernel"], r["fold"], r["ksplit"], r["launches"]) == ("woq_mid_kernel", False, 4, 2), r
     r = p(4, 4096, 4096, 128, m=17, act="fp16")
@@ -243,13 +245,14 @@ def test_plan_forward_kernel_choice():
 
 def test_plan_gemm4_waves_split_over_k():
     """gemm4's K-split wave layout (NAD_GEMM4_KSW=2, auto): on for more than one round of output tiles or K >= 8192
-    (gate, down, lm_head, M = 4096), off for one round at K = 4096 (profiles/r04_gemm4_ksw_ab.txt) and under split-K."""
+    (gate, down, lm_head, M = 4096), off for one round at K = 4096 (profiles/r04_gemm4_ksw_ab.txt) and under split-K.
+    Shown on int8 g32 (int4 g32 runs gemm7)."""
     p = bestla.plan_forward
-    assert not p(4, 4096, 4096, 32, m=2048)["ksw"]          # 256 tiles: one round on 256 CUs
-    assert p(4, 4096, 4096, 32, m=4096)["ksw"]              # 512 tiles
-    assert p(4, 11008, 4096, 32, m=2048)["ksw"]             # gate: 688 tiles
-    assert p(4, 4096, 11008, 32, m=2048)["ksw"]             # down: K = 11008
-    r = p(4, 4096, 11008, 32, m=64)
+    assert not p(8, 4096, 4096, 32, m=2048)["ksw"]          # 256 tiles: one round on 256 CUs
+    assert p(8, 4096, 4096, 32, m=4096)["ksw"]              # 512 tiles
+    assert p(8, 11008, 4096, 32, m=2048)["ksw"]             # gate: 688 tiles
+    assert p(8, 4096, 11008, 32, m=2048)["ksw"]             # down: K = 11008
+    r = p(8, 4096, 11008, 32, m=64)
     assert r["ksplit"] > 1 and not r["ksw"]                 # split-K launches keep the M-split waves
     assert not p(4, 4096, 4096, 128, m=4096)["ksw"]         # int4 g128: gemm7 (its own K split, not reported as ksw)
 

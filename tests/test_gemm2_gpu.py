@@ -161,8 +161,10 @@ GEMM4_CASES = [
 @pytest.mark.parametrize("cfg", GEMM4_CASES)
 @pytest.mark.parametrize("act", ["fp32", "fp16", "bf16"])
 def test_gemm4_parity(oracle, knob, cfg, act, ksw):
-    """gemm4 against the oracle (NAD_GEMM4_KSW=1: folded launches with the waves split over K)."""
+    """gemm4 against the oracle (NAD_GEMM4_KSW=1: folded launches with the waves split over K; NAD_GEMM_KERNEL=3 keeps
+    int4 g32 / g64 on gemm4, tests/test_gemm2_gpu.py::test_gemm7_small_groups covers their default gemm7 path)."""
     knob("NAD_MID_MAX_M", "0")
+    knob("NAD_GEMM_KERNEL", "3")
     knob("NAD_GEMM4_KSW", ksw)
     m, n, k, bs, qt, st, asym, comp = cfg
     blob = _blob(oracle, n, k, bs, qt, st, asym, comp, seed=m + 7 * n + k)
@@ -187,6 +189,7 @@ FOLD_TOL = 5e-4
 def test_gemm4_g64_scale_fold(oracle, knob, cfg):
     """Groups of 64 fold the group scale into the fp16 B fragment too (int4 / int2 / int8): against the oracle and the
     exact fp32 group-end scaling (NAD_GEMM4_FOLD=0)."""
+    knob("NAD_GEMM_KERNEL", "3")
     m, n, k, bs, qt, st, asym, comp = cfg
     blob = _blob(oracle, n, k, bs, qt, st, asym, comp, seed=m + 9 * n + k)
     w = bestla.DeviceWeight(blob)
@@ -205,6 +208,7 @@ def test_gemm4_g32_scale_fold(oracle, knob, cfg):
     """Groups of 32 fold the group scale into the fp16 B fragment by default (q * s rounded once to fp16; every q * s of
     these blobs is an fp16 normal, DeviceWeight::fold_ok): against the oracle at the prefill bar, and against the exact
     fp32 per-step scaling (NAD_GEMM4_FOLD=0) within the fp16 rounding of q * s (2^-11 relative per weight)."""
+    knob("NAD_GEMM_KERNEL", "3")
     m, n, k, bs, qt, st, asym, comp = cfg
     blob = _blob(oracle, n, k, bs, qt, st, asym, comp, seed=m + 5 * n + k)
     w = bestla.DeviceWeight(blob)
@@ -216,6 +220,49 @@ def test_gemm4_g32_scale_fold(oracle, knob, cfg):
     assert _rel_err(yf, ref) <= FOLD_TOL
     assert _rel_err(ye, ref) <= TOL["fp16"]
     assert _rel_err(yf, ye) <= FOLD_TOL
+
+
+GEMM7_GROUP_CASES = [
+    # m, n, k, bs, stype, asym -- int4 groups of 32 / 64 on gemm7 (the group scale per 32-deep step)
+    (2048, 512, 1024, 32, F16, False),    # 256-row tiles
+    (300, 384, 640, 32, BF16, True),      # ragged M, 256-row tiles, 5 K tiles
+    (100, 130, 512, 32, F32, False),      # 128-row tile, ragged N (a partial stripe), f32 scales (the largest region)
+    (257, 300, 640, 32, F32, True),       # f32 asym: the 256-row tile's LDS at its largest (scales 2 KiB, zp 512 B)
+    (96, 130, 300, 64, F16, False),       # g64, K tail (zero padded), 128-row tile
+    (300, 200, 768, 64, BF16, True),      # g64 asym
+    (65, 1024, 4096, 32, F16, True),      # 128-row tile with split-K runs
+    (200, 640, 2048, 64, F32, True),      # 256-row tile with split-K runs
+]
+
+
+@pytest.mark.parametrize("cfg", GEMM7_GROUP_CASES)
+@pytest.mark.parametrize("act", ["fp32", "fp16", "bf16"])
+def test_gemm7_small_groups(oracle, knob, cfg, act):
+    """int4 g32 / g64 through gemm7 (q * s rounded once to fp16 per 32-deep group step): against the oracle at the fold
+    bar, against gemm4's folded launch (NAD_GEMM_KERNEL=3: the same fp16 weights up to the scale's own fp16 rounding)
+    and gemm4's exact fp32 group scales (NAD_GEMM4_FOLD=0); bit-repeatable."""
+    m, n, k, bs, st, asym = cfg
+    blob = _blob(oracle, n, k, bs, S4, st, asym, 4, seed=m + 11 * n + k)
+    w = bestla.DeviceWeight(blob)
+    plan = w.plan(m, act)
+    assert plan["kernel"] == "woq_gemm7_kernel" and plan["fold"], plan
+    A = np.random.default_rng(m * 5 + n).uniform(-0.5, 0.5, size=(m, k)).astype(np.float32)
+    x = torch.from_numpy(A).cuda()
+    if act != "fp32":
+        x = x.to(torch.float16 if act == "fp16" else torch.bfloat16)
+    ref = oracle.forward(x.float().cpu().numpy(), blob, n, k)
+    y = w.forward(x).cpu().numpy()
+    assert _rel_err(y, ref) <= max(TOL[act], FOLD_TOL), (_rel_err(y, ref), plan)
+    assert np.array_equal(w.forward(x).cpu().numpy(), y)
+    knob("NAD_GEMM_KERNEL", "3")
+    assert w.plan(m, act)["kernel"] == "woq_gemm4_kernel"
+    y4 = w.forward(x).cpu().numpy()
+    assert _rel_err(y, y4.astype(np.float64)) <= FOLD_TOL
+    knob("NAD_GEMM_KERNEL", "7")
+    knob("NAD_GEMM4_FOLD", "0")
+    ye = w.forward(x).cpu().numpy()
+    assert _rel_err(ye, ref) <= TOL[act]
+    assert _rel_err(y, ye.astype(np.float64)) <= FOLD_TOL
 
 
 def test_gemm4_takes_the_fallback_configs(oracle, knob):
