@@ -185,7 +185,7 @@ int nad_device_forward(const void* act, int act_dtype, const void* devstor, floa
 #define NAD_KERNEL_GEMM2 7     /* woq_gemm2_kernel (NAD_GEMM_KERNEL=2) */
 #define NAD_KERNEL_GEMM 8      /* woq_gemm_kernel: register-staged prefill fallback */
 #define NAD_KERNEL_GEMM7 9     /* woq_gemm7_kernel: prefill, int4 groups of 128 * 2^j, scale folded (default) */
-#define NAD_KERNEL_MID 10      /* woq_mid_kernel: 17 <= M <= 64, int4 / int2 */
+#define NAD_KERNEL_MID 10      /* woq_mid_kernel: 12 (fp16) / 8 (fp32, bf16) <= M <= 64, int4 / int2 */
 int nad_plan_forward(int bits, int n, int k, int blocksize, int scale_t, int asym, int m, int act_dtype, int64_t* out,
                      int nout);
 /* the same dry run for a loaded device weight (its format, act-order, fold range and compute mode included) */

@@ -947,10 +947,11 @@ static int pipelined_gemm(const DeviceWeight& w, int m) {
     return 0;
   const int tpg = w.blocksize / 128;
   if (w.bits == 4 && w.blocksize % 128 == 0 && (tpg & (tpg - 1)) == 0 && !kn.gemm4_all) return 3;
-  // int4 groups of 32 / 64 with a foldable q * s: gemm7 with the group scale per 32-deep step (profiles/r05_gemm7_g32*;
-  // NAD_GEMM4_FOLD=0, the exact fp32 group scales, or NAD_GEMM_KERNEL=3 keep gemm4)
-  if (w.bits == 4 && (w.blocksize == 32 || w.blocksize == 64) && w.fold_ok && kn.gemm_kernel == 7 &&
-      kn.gemm4_fold && !kn.gemm4_all)
+  // int4 groups of 32 / 64 and int2 / int8 with a foldable q * s: gemm7 with the group scale per 32-deep step or per
+  // half step (profiles/r05_gemm7_g32*, r05_gemm7_int2_int8*; NAD_GEMM4_FOLD=0, the exact fp32 group scales, or
+  // NAD_GEMM_KERNEL=3 keep gemm4)
+  if ((w.bits == 4 || w.bits == 2 || w.bits == 8) && gemm7_ok(w.bits, w.blocksize, w.fold_ok) &&
+      kn.gemm_kernel == 7 && kn.gemm4_fold && !kn.gemm4_all)
     return 3;
   if (!kn.gemm4_disable && gemm4_mode(w.bits, w.blocksize, w.ng, w.nt * tile_k(w.bits), w.asym)) return 4;
   return 0;
@@ -1192,7 +1193,7 @@ static int run_gemm(const void* act, int act_t, int lda, int m, int k, const Dev
     }
     hipError_t e = pg == 4 ? launch_gemm4(a, w.bits, pre->p, pre->ld, st)
                    : g2    ? launch_gemm2(a, pre->p, pre->ld, st)
-                   : g7    ? launch_gemm7(a, bm, pre->p, pre->ld, st)
+                   : g7    ? launch_gemm7(a, w.bits, bm, pre->p, pre->ld, st)
                            : launch_gemm3(a, pre->p, pre->ld, st);
     if (e == hipSuccess && ks > 1) e = launch_splitk_reduce(a, st);
     if (e != hipSuccess) {

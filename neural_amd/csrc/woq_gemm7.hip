@@ -28,23 +28,29 @@ namespace g7 {
 
 constexpr int KT = 128, ROWB = 128;  // ROWB: bytes of one A row per 64-deep half step
 constexpr int NS = 8;                // stripes per tile (128 columns)
-constexpr int BTILES = NS * 1024;
 constexpr int EPI_LD = 36;           // epilogue transpose row stride (floats)
 
-// One K tile of B with its scale and zero-point bytes as they lie in HBM ([stripe][group][16 columns]): GPT groups per
-// tile (4 at groups of 32, 2 at 64, 1 from 128 up), each region at least one 256-byte LDS-DMA piece
-template <int GPT, int ST, bool ASYM>
+// One B buffer with its scale and zero-point bytes as they lie in HBM ([stripe][group][16 columns]), each region at least
+// one 256-byte LDS-DMA piece.  int4 (tile mode): a whole 128-deep K tile, GPT groups per tile (4 at groups of 32, 2 at
+// 64, 1 from 128 up).  int2 / int8 (half-step mode, HS): the slice of the 8 stripes one 64-deep half step reads -- a
+// dword of every lane of a 256-deep int2 tile, a whole 64-deep int8 tile -- loaded every half step, so each half step
+// issues the same loads and the vmcnt arithmetic stays exact; GPT groups per half step (2 at groups of 32, else 1).
+template <int BITS, int GPT, int ST, bool ASYM>
 struct Bbuf {
+  static constexpr bool HS = BITS != 4;
   static constexpr int ESZ = ST == kScaleF32 ? 4 : 2;
-  static constexpr int SCT = NS * GPT * 16 * ESZ, ZPT = NS * GPT * 16;  // bytes a tile uses
+  static constexpr int BSL = BITS == 4 ? 1024 : (BITS == 8 ? 1024 : 256);  // bytes per stripe per buffer
+  static constexpr int SCT = NS * GPT * 16 * ESZ, ZPT = NS * GPT * 16;      // bytes a buffer uses
   static constexpr int SCR = SCT > 256 ? SCT : 256, ZPR = ASYM ? (ZPT > 256 ? ZPT : 256) : 0;
-  static constexpr int BYTES = BTILES + SCR + ZPR;
+  static constexpr int BW = NS * BSL;
+  static constexpr int BYTES = BW + SCR + ZPR;
 };
 
 // Geometry per tile height BMT (32, 64, 128, 256 rows; every wave covers all of them): the A ring runs DA = NA - 1 half
-// steps ahead -- deeper for the short tiles, whose K runs are split-K runs of a few tiles -- and the B ring holds a
-// tile no shorter than the two half steps after its last read.
-template <int BMT, int BBUF>
+// steps ahead -- deeper for the short tiles, whose K runs are split-K runs of a few tiles.  Tile mode: the B ring holds
+// a tile no shorter than the two half steps after its last read.  Half-step mode: B runs DB half steps ahead (DA, or 2
+// where DA + 1 int8 slices would not fit beside the A ring) in a ring of DB + 1 slices.
+template <int BMT, class BB>
 struct Geo {
   static constexpr int RF = BMT / 16;                  // row fragments per wave
   static constexpr int HF = RF / 2;                    // fragments per half of the register rotation
@@ -53,8 +59,9 @@ struct Geo {
   static constexpr int PA = PIECES >= 8 ? PIECES / 8 : 1;  // per wave (BMT = 32: waves 4-7 repeat pieces 0-3)
   static constexpr int NA = BMT == 256 ? 4 : (BMT == 128 ? 6 : 8);
   static constexpr int DA = NA - 1;
-  static constexpr int NBR = (DA + 3) / 2;
-  static constexpr int LDS_RING = NA * HBUF + NBR * BBUF;
+  static constexpr int DB = !BB::HS ? DA : (NA * HBUF + (DA + 1) * BB::BYTES <= 160 * 1024 ? DA : 2);
+  static constexpr int NBR = BB::HS ? DB + 1 : (DA + 3) / 2;
+  static constexpr int LDS_RING = NA * HBUF + NBR * BB::BYTES;
   static constexpr int LDS_EPI = 8 * (BMT / 2) * EPI_LD * 4;
   static constexpr int LDS = LDS_RING > LDS_EPI ? LDS_RING : LDS_EPI;
   static_assert(LDS <= 160 * 1024 && DA % 2 == 1, "geometry");
@@ -144,6 +151,40 @@ __device__ __forceinline__ h8_t dequant_fold(uint32_t w, uint32_t mag, h2_t s16,
   return r;
 }
 
+// int8: a dword pair (8 bytes q + 128) -> fp16 (q - zp) * s: byte b becomes 1024 + b by a byte permute, c = -(1152 + zp)
+__device__ __forceinline__ h8_t dequant8_fold(uint32_t w0, uint32_t w1, h2_t c, h2_t sc) {
+  const h2_t p0 = (as_h2(__builtin_amdgcn_perm(0x64646464u, w0, 0x04010400u)) + c) * sc;
+  const h2_t p1 = (as_h2(__builtin_amdgcn_perm(0x64646464u, w0, 0x04030402u)) + c) * sc;
+  const h2_t p2 = (as_h2(__builtin_amdgcn_perm(0x64646464u, w1, 0x04010400u)) + c) * sc;
+  const h2_t p3 = (as_h2(__builtin_amdgcn_perm(0x64646464u, w1, 0x04030402u)) + c) * sc;
+  h8_t r;
+  r[0] = p0[0];
+  r[1] = p0[1];
+  r[2] = p1[0];
+  r[3] = p1[1];
+  r[4] = p2[0];
+  r[5] = p2[1];
+  r[6] = p3[0];
+  r[7] = p3[1];
+  return r;
+}
+// int2: one 32-deep step (the low 8 bits of each 16-bit half of x) -> fp16 (q - 2 - zp) * s: the exact integers of the
+// scaled magic numbers (dequant2s), then one rounding
+__device__ __forceinline__ h8_t dequant2_fold(uint32_t x, const Dq2c& q, h2_t sc) {
+  const h8_t v = dequant2s(x, q);
+  h8_t r;
+#pragma unroll
+  for (int i = 0; i < 8; i += 2) {
+    h2_t p;
+    p[0] = v[i];
+    p[1] = v[i + 1];
+    p = p * sc;
+    r[i] = p[0];
+    r[i + 1] = p[1];
+  }
+  return r;
+}
+
 #define NAD_SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
 
 // 8 waves (two per SIMD) split over K: wave (wn = w & 3, wk = w >> 2) owns the BMT x 32 partial of stripes 2 wn,
@@ -156,19 +197,22 @@ __device__ __forceinline__ h8_t dequant_fold(uint32_t w, uint32_t mag, h2_t s16,
 // every M-wave) 3-35 % slower than this one (profiles/r05_gemm8_tile_shapes_sweep.txt).  BMT < 256 serves 17 <= M <= 256
 // with split-K runs (the mid-M range): the tile's rows are what the problem has, not 256 rows of which most re-read the
 // last one.
-template <int BMT, bool ASYM, int ST, int GPT>
+template <int BITS, int BMT, bool ASYM, int ST, int GPT>
 __global__ __launch_bounds__(512, 1) void woq_gemm7_kernel(GemmArgs a, const _Float16* __restrict__ A16, int lda16) {
-  using BB = Bbuf<GPT, ST, ASYM>;
-  using G = Geo<BMT, BB::BYTES>;
-  constexpr int RF = G::RF, HF = G::HF, HBUF = G::HBUF, PA = G::PA, NA = G::NA, DA = G::DA, NBR = G::NBR;
-  constexpr int BBUF = BB::BYTES, BSC = BB::SCR, ESZ = BB::ESZ;
+  using BB = Bbuf<BITS, GPT, ST, ASYM>;
+  using G = Geo<BMT, BB>;
+  constexpr int RF = G::RF, HF = G::HF, HBUF = G::HBUF, PA = G::PA, NA = G::NA, DA = G::DA, DB = G::DB, NBR = G::NBR;
+  constexpr int BBUF = BB::BYTES, BSC = BB::SCR, ESZ = BB::ESZ, BW = BB::BW;
+  constexpr bool HS = BB::HS;
+  constexpr int TK = BITS == 4 ? 128 : (BITS == 2 ? 256 : 64), HPT = TK / 64;  // K tile depth, half steps per tile
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));
   const int wn = wave & 3, wk = wave >> 2;
   const SkinnyWeight& W = a.w;
   const int M = a.M, nt = W.nt, ng = W.ng, ns = W.ns;
-  const int tpg = W.bs >= KT ? W.bs / KT : 1;
+  // tile mode: K tiles per group (2^tsh); half-step mode: half steps per group (2^tsh, groups of 64 up)
+  const int tpg = HS ? (W.bs >= 64 ? W.bs / 64 : 1) : (W.bs >= KT ? W.bs / KT : 1);
   const int tsh = __builtin_ctz(unsigned(tpg));
 
   // XCD-aware remap (one XCD walks the N tiles of one (M tile, K run)) and split-K runs, as gemm3
@@ -186,7 +230,8 @@ __global__ __launch_bounds__(512, 1) void woq_gemm7_kernel(GemmArgs a, const _Fl
   bid -= ks * ntile;
   const int kt0 = nsplit > 1 ? ks * a.ktiles : 0;
   const int ntl = nsplit > 1 ? min(a.ktiles, nt - kt0) : nt;
-  const int nh = 2 * ntl;
+  const int nh = HPT * ntl;            // half steps of the K run
+  const int nh2 = (nh + 1) & ~1;       // the loop's (int8: an odd count ends with one all-zero half step)
   const int bm = bid / nbn, bn = bid % nbn;
   const int m0 = bm * BMT;
   const int nl = lane & 15, kq = lane >> 4;
@@ -202,28 +247,47 @@ __global__ __launch_bounds__(512, 1) void woq_gemm7_kernel(GemmArgs a, const _Fl
     aoff[i] = uint32_t(grow) * uint32_t(lda16) * 2u + uint32_t(((lane & 7) ^ ((row >> 1) & 7)) * 16);
     adst[i] = smem + p * 1024;
   }
-  const auto ra = brsrc(reinterpret_cast<const char*>(A16) + size_t(kt0) * KT * 2);
+  const auto ra = brsrc(reinterpret_cast<const char*>(A16) + size_t(kt0) * TK * 2);
   const auto rb = brsrc(static_cast<const char*>(W.tiles) + size_t(kt0) * 1024);
   const auto rnull = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(W.tiles), 0, 0, 0x00020000);
   const uint32_t boffd = (uint32_t(min(bn * NS + wave, ns - 1)) * nt * 64 + lane) * 16;
   // scale / zero-point pieces: wave w copies 256-byte piece w % pieces of the tile's region; lane bytes past the tile's
   // share (a region rounded up to one piece) re-read its start into the unused tail
   constexpr int st = ST;
-  const auto rs = brsrc(W.scales);
-  const auto rz = brsrc(W.zps);
-  const uint32_t g0 = GPT > 1 ? uint32_t(kt0) * GPT : uint32_t(kt0 >> tsh);  // first group of the K run
-  auto piece_off = [&](int pieces, int total, int esz, int* dst) {
+  // scales / zero points: a lane whose group lies past the last one (the zero-padded K tail of the last tile or half
+  // step) gets an offset past the resource's end, which loads 0 without touching memory
+  constexpr uint32_t kOOB = 0x7FFF0000u;
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(W.scales), 0, int(kOOB), 0x00020000);
+  const auto rz = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(static_cast<const void*>(W.zps)), 0, int(kOOB),
+                                                    0x00020000);
+  // first group of B buffer v of the K run (a tile, or a half step)
+  auto group_of = [&](int v) -> uint32_t {
+    const uint32_t x = HS ? uint32_t(kt0 * HPT + v) : uint32_t(kt0 + v);
+    return GPT > 1 ? x * GPT : x >> tsh;
+  };
+  auto piece_off = [&](int pieces, int total, int esz, int* dst, int* gi) {
     const int p = wave % pieces;
     *dst = p * 256;
     const int o = (p * 256 + lane * 4) % total, chunk = GPT * 16 * esz;
     const int s = min(bn * NS + o / chunk, ns - 1);
-    return (uint32_t(s) * ng * 16 + g0 * 16) * esz + uint32_t(o % chunk);
+    *gi = (o % chunk) / (16 * esz);  // the lane's group within the buffer
+    return uint32_t(s) * ng * 16 * esz + uint32_t(o % chunk);
   };
-  int sdst = 0, zdst = 0;
-  const uint32_t svo = piece_off(BB::SCR / 256, BB::SCT, ESZ, &sdst);
-  const uint32_t zvo = ASYM ? piece_off(BB::ZPR / 256, BB::ZPT, 1, &zdst) : 0u;
+  int sdst = 0, zdst = 0, sgi = 0, zgi = 0;
+  const uint32_t svo = piece_off(BB::SCR / 256, BB::SCT, ESZ, &sdst, &sgi);
+  const uint32_t zvo = ASYM ? piece_off(BB::ZPR / 256, BB::ZPT, 1, &zdst, &zgi) : 0u;
+  // the scale / zero-point pieces of buffer v (first group g)
+  auto load_sz = [&](bool live, uint32_t g, char* dst) {
+    const uint32_t vs = g + uint32_t(sgi) < uint32_t(ng) ? svo + g * 16 * ESZ : kOOB;
+    blds4(live ? rs : rnull, vs, 0, dst + sdst);
+    if constexpr (ASYM) {
+      const uint32_t vz = g + uint32_t(zgi) < uint32_t(ng) ? zvo + g * 16 : kOOB;
+      blds4(live ? rz : rnull, vz, 0, dst + BSC + zdst);
+    }
+  };
 
-  // batch(u): A(u + DA) and, when u + DA is even, B tile (u + DA) / 2 with its scale / zero-point pieces
+  // batch(u): A(u + DA) and -- tile mode -- when u + DA is even, B tile (u + DA) / 2 with its scale / zero-point
+  // pieces; half-step mode: the B slice of half step u + DB (none in the prologue batches before it starts)
   auto issue = [&](int u) {
     const int ua = u + DA;
     const bool live = ua < nh;
@@ -231,33 +295,49 @@ __global__ __launch_bounds__(512, 1) void woq_gemm7_kernel(GemmArgs a, const _Fl
     const auto rA = live ? ra : rnull;
 #pragma unroll
     for (int i = 0; i < PA; i++) blds16(rA, aoff[i], uint32_t(ua) * ROWB, adst[i] + aslot * HBUF);
-    if ((ua & 1) == 0) {
+    if constexpr (HS) {
+      const int ub = u + DB;
+      if (ub >= 0) {
+        const bool lb = ub < nh;
+        char* bb = smem + NA * HBUF + (ub % NBR) * BBUF;
+        if constexpr (BITS == 8)
+          blds16(lb ? rb : rnull, boffd, uint32_t(ub) * 1024, bb + wave * 1024);
+        else  // dword ub & 3 of every lane of int2 tile ub >> 2
+          blds4(lb ? rb : rnull, boffd, uint32_t(ub >> 2) * 1024 + uint32_t(ub & 3) * 4, bb + wave * 256);
+        load_sz(lb, group_of(ub), bb + BW);
+      }
+    } else if ((ua & 1) == 0) {
       const int t = ua >> 1;
       char* bb = smem + NA * HBUF + (t % NBR) * BBUF;
       blds16(live ? rb : rnull, boffd, uint32_t(t) * 1024, bb + wave * 1024);
-      const uint32_t g = (GPT > 1 ? uint32_t(t) * GPT : uint32_t(t >> tsh)) * 16;
-      blds4(live ? rs : rnull, svo, g * ESZ, bb + BTILES + sdst);
-      if constexpr (ASYM) blds4(live ? rz : rnull, zvo, g, bb + BTILES + BSC + zdst);
+      load_sz(live, group_of(t), bb + BW);
     }
   };
   // at the barrier of buffer u + 1 (the middle of half step u), batch(u + 1 - DA) has landed and batches
-  // u + 2 - DA .. u (DA - 1 of them, (DA - 1) / 2 with a B tile) may be in flight
+  // u + 2 - DA .. u (DA - 1 of them, (DA - 1) / 2 with a B tile) may be in flight; half-step mode: B(u + 1) came with
+  // batch(u + 1 - DB), after which DB - 1 whole batches may be in flight
   constexpr int NB = ASYM ? 3 : 2;
-  constexpr int WV = (DA - 1) * PA + (DA - 1) / 2 * NB;
+  constexpr int WV = HS ? (DB - 1) * (PA + NB) : (DA - 1) * PA + (DA - 1) / 2 * NB;
   static_assert(WV < 64, "vmcnt");
 
   const uint32_t mag = 0x64006400u;
   const h2_t s16 = splat(1.f / 16.f);
   const h2_t zc0 = splat(-(1024.f + 8.f)), zc1 = splat(-(64.f + 8.f));
+  const h2_t zc8 = splat(-(1024.f + 128.f));
   const uint32_t roff = uint32_t(nl * ROWB + (((wk * 4 + kq) ^ ((nl >> 1) & 7)) * 16));
-  const int boff = (wn * 2) * 1024 + lane * 16 + wk * 4;
+  // this lane's B bytes of stripe 2 wn (+ 1 KiB / 256 B for 2 wn + 1) for its 32-deep step: int4 dword 2 H + wk of the
+  // tile, int8 the dword pair wk, int2 the half step's dword (its 16-bit half wk)
+  const int boff = BITS == 4 ? (wn * 2) * 1024 + lane * 16 + wk * 4
+                             : (BITS == 8 ? (wn * 2) * 1024 + lane * 16 + wk * 8 : (wn * 2) * 256 + lane * 4);
+  constexpr int BJ = BITS == 2 ? 256 : 1024;
   // this lane's scale / zero-point dword for stripe 2 wn (+ SJ for 2 wn + 1) at its first 32-deep step of the tile; the
   // step's group moves it by SH per half step
-  const int gw = GPT == 4 ? wk : 0;
-  const int soff = BTILES + ((((wn * 2) * GPT + gw) * 16 + nl) * ESZ & ~3);
-  const int zoff = BTILES + BSC + ((((wn * 2) * GPT + gw) * 16 + nl) & ~3);
+  const int gw = (HS ? GPT == 2 : GPT == 4) ? wk : 0;
+  const int soff = BW + ((((wn * 2) * GPT + gw) * 16 + nl) * ESZ & ~3);
+  const int zoff = BW + BSC + ((((wn * 2) * GPT + gw) * 16 + nl) & ~3);
   constexpr int SJ = GPT * 16 * ESZ, ZJ = GPT * 16;
-  constexpr int SH = GPT == 4 ? 2 * 16 * ESZ : (GPT == 2 ? 16 * ESZ : 0), ZH = SH / ESZ;
+  constexpr int SH = HS ? 0 : (GPT == 4 ? 2 * 16 * ESZ : (GPT == 2 ? 16 * ESZ : 0)), ZH = SH / ESZ;
+  constexpr bool SCALE_EVERY = HS || GPT > 1;  // the scale changes within a tile / every half step
   const int ssh = st == kScaleF32 ? 0 : (nl & 1) * 16;
   const int zsh = (nl & 3) * 8;
   auto scale_h2 = [&](uint32_t x) {
@@ -278,16 +358,27 @@ __global__ __launch_bounds__(512, 1) void woq_gemm7_kernel(GemmArgs a, const _Fl
   h8_t bf[2];
   h2_t sc[2];
   h2_t c0[2] = {zc0, zc0}, c1[2] = {zc1, zc1};
-  uint32_t bw0 = 0, bw1 = 0, sw0 = 0, sw1 = 0, zw0 = 0, zw1 = 0;
+  const Dq2c q2s = dq2_consts(2);
+  Dq2c q2[2] = {q2s, q2s};
+  if constexpr (BITS == 8) c0[0] = c0[1] = zc8;
+  uint32_t bw0 = 0, bw1 = 0, bx0 = 0, bx1 = 0, sw0 = 0, sw1 = 0, zw0 = 0, zw1 = 0;
 
   // B words (+ scale / zp at a tile start) and A fragments 0 .. HF - 1 of half step u
   auto read_lo = [&](auto Hc, int u) {
     constexpr int H = decltype(Hc)::value;
-    const int t = u >> 1;
+    const int t = HS ? u : u >> 1;
     const uint32_t bl = lds_addr(smem + NA * HBUF + (t % NBR) * BBUF);
-    bw0 = lds_b32<H * 8>(bl + boff);
-    bw1 = lds_b32<1024 + H * 8>(bl + boff);
-    if constexpr (H == 0 || GPT > 1) {
+    if constexpr (BITS == 8) {
+      const uint2 x0 = lds_b64<0>(bl + boff), x1 = lds_b64<BJ>(bl + boff);
+      bw0 = x0.x;
+      bx0 = x0.y;
+      bw1 = x1.x;
+      bx1 = x1.y;
+    } else {
+      bw0 = lds_b32<HS ? 0 : H * 8>(bl + boff);
+      bw1 = lds_b32<HS ? BJ : 1024 + H * 8>(bl + boff);
+    }
+    if constexpr (H == 0 || SCALE_EVERY) {
       sw0 = lds_b32<H * SH>(bl + soff);
       sw1 = lds_b32<H * SH + SJ>(bl + soff);
       if constexpr (ASYM) {
@@ -304,19 +395,37 @@ __global__ __launch_bounds__(512, 1) void woq_gemm7_kernel(GemmArgs a, const _Fl
   };
   auto dequant = [&](auto Hc) {
     constexpr int H = decltype(Hc)::value;
-    if constexpr (H == 0 || GPT > 1) {
+    if constexpr (H == 0 || SCALE_EVERY) {
       sc[0] = scale_h2(sw0);
       sc[1] = scale_h2(sw1);
       if constexpr (ASYM) {
-        const float z0 = float(int(int8_t((zw0 >> zsh) & 0xFFu))), z1 = float(int(int8_t((zw1 >> zsh) & 0xFFu)));
-        c0[0] = zc0 - splat(z0);
-        c1[0] = zc1 - splat(z0);
-        c0[1] = zc0 - splat(z1);
-        c1[1] = zc1 - splat(z1);
+        const int z0 = int(int8_t((zw0 >> zsh) & 0xFFu)), z1 = int(int8_t((zw1 >> zsh) & 0xFFu));
+        if constexpr (BITS == 4) {
+          c0[0] = zc0 - splat(float(z0));
+          c1[0] = zc1 - splat(float(z0));
+          c0[1] = zc0 - splat(float(z1));
+          c1[1] = zc1 - splat(float(z1));
+        } else if constexpr (BITS == 8) {
+          c0[0] = zc8 - splat(float(z0));
+          c0[1] = zc8 - splat(float(z1));
+        } else {  // the symmetric constants less zp: 4 packed subtractions per stripe
+          const h2_t y0 = splat(float(z0)), y1 = splat(float(z1));
+          q2[0] = Dq2c{q2s.c0 - y0, q2s.c1 - y0, q2s.c2 - y0, q2s.c3 - y0};
+          q2[1] = Dq2c{q2s.c0 - y1, q2s.c1 - y1, q2s.c2 - y1, q2s.c3 - y1};
+        }
       }
     }
-    bf[0] = dequant_fold(bw0, mag, s16, c0[0], c1[0], sc[0]);
-    bf[1] = dequant_fold(bw1, mag, s16, c0[1], c1[1], sc[1]);
+    if constexpr (BITS == 4) {
+      bf[0] = dequant_fold(bw0, mag, s16, c0[0], c1[0], sc[0]);
+      bf[1] = dequant_fold(bw1, mag, s16, c0[1], c1[1], sc[1]);
+    } else if constexpr (BITS == 8) {
+      bf[0] = dequant8_fold(bw0, bx0, c0[0], sc[0]);
+      bf[1] = dequant8_fold(bw1, bx1, c0[1], sc[1]);
+    } else {
+      const uint32_t sh = uint32_t(wk) * 8u;
+      bf[0] = dequant2_fold(bw0 >> sh, q2[0], sc[0]);
+      bf[1] = dequant2_fold(bw1 >> sh, q2[1], sc[1]);
+    }
   };
 
   // prologue: batches -DA .. -1, then the operands of half step 0
@@ -330,6 +439,8 @@ __global__ __launch_bounds__(512, 1) void woq_gemm7_kernel(GemmArgs a, const _Fl
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   tie(bw0);
   tie(bw1);
+  tie(bx0);
+  tie(bx1);
   tie(sw0);
   tie(sw1);
   tie(zw0);
@@ -369,13 +480,15 @@ __global__ __launch_bounds__(512, 1) void woq_gemm7_kernel(GemmArgs a, const _Fl
     asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(HF));  // the B words and fragments 0 .. HF - 1 have landed
     tie(bw0);
     tie(bw1);
+    tie(bx0);
+    tie(bx1);
     tie(sw0);
     tie(sw1);
     tie(zw0);
     tie(zw1);
     dequant(std::integral_constant<int, 1 - H>{});
   };
-  for (int u = 0; u < nh; u += 2) {
+  for (int u = 0; u < nh2; u += 2) {
     half(std::integral_constant<int, 0>{}, u);
     half(std::integral_constant<int, 1>{}, u + 1);
   }
@@ -429,12 +542,14 @@ __global__ __launch_bounds__(512, 1) void woq_gemm7_kernel(GemmArgs a, const _Fl
 
 }  // namespace g7
 
-bool gemm7_ok(int bits, int blocksize, int fold_ok) {
-  const int tpg = blocksize / g7::KT;
-  return bits == 4 && fold_ok && (blocksize == 32 || blocksize == 64 || (blocksize % g7::KT == 0 && (tpg & (tpg - 1)) == 0));
-}
+#ifndef G7_BITS
+#define G7_BITS 4  // this object's weight format: woq_gemm7.o 4, woq_gemm7_b2.o 2, woq_gemm7_b8.o 8 (Makefile)
+#endif
+#define G7_CAT2(x, y) x##y
+#define G7_CAT(x, y) G7_CAT2(x, y)
 
-hipError_t launch_gemm7(const GemmArgs& a, int bm, const _Float16* A16, int lda16, hipStream_t st) {
+hipError_t G7_CAT(launch_gemm7_b, G7_BITS)(const GemmArgs& a, int bm, const _Float16* A16, int lda16, hipStream_t st) {
+  constexpr int BITS = G7_BITS;
   const int nbm = (a.M + bm - 1) / bm, nbn = (a.w.ns + g7::NS - 1) / g7::NS;
   const dim3 grid(nbm * nbn * (a.ksplit > 1 ? a.ksplit : 1));
   auto go = [&](auto k, int lds, bool& done) -> hipError_t {
@@ -447,7 +562,8 @@ hipError_t launch_gemm7(const GemmArgs& a, int bm, const _Float16* A16, int lda1
     hipLaunchKernelGGL(k, grid, dim3(512), lds, st, a, A16, lda16);
     return hipGetLastError();
   };
-  const int gpt = a.w.bs == 32 ? 4 : (a.w.bs == 64 ? 2 : 1);
+  // groups per B buffer: per tile (int4) or per half step (int2 / int8)
+  const int gpt = BITS == 4 ? (a.w.bs == 32 ? 4 : (a.w.bs == 64 ? 2 : 1)) : (a.w.bs == 32 ? 2 : 1);
   auto pick = [&](auto bmc) -> hipError_t {
     constexpr int BMT = decltype(bmc)::value;
     static bool attr[3][2][3] = {};
@@ -457,12 +573,13 @@ hipError_t launch_gemm7(const GemmArgs& a, int bm, const _Float16* A16, int lda1
     auto sel = [&](auto asc, auto stc, auto gc) {
       constexpr bool AS = decltype(asc)::value;
       constexpr int STT = decltype(stc)::value, GP = decltype(gc)::value;
-      return go(g7::woq_gemm7_kernel<BMT, AS, STT, GP>, g7::Geo<BMT, g7::Bbuf<GP, STT, AS>::BYTES>::LDS, d);
+      return go(g7::woq_gemm7_kernel<BITS, BMT, AS, STT, GP>, g7::Geo<BMT, g7::Bbuf<BITS, GP, STT, AS>>::LDS, d);
     };
     auto by_gpt = [&](auto asc, auto stc) {
-      return gpt == 4   ? sel(asc, stc, std::integral_constant<int, 4>{})
-             : gpt == 2 ? sel(asc, stc, std::integral_constant<int, 2>{})
-                        : sel(asc, stc, std::integral_constant<int, 1>{});
+      if constexpr (BITS == 4) {
+        if (gpt == 4) return sel(asc, stc, std::integral_constant<int, 4>{});
+      }
+      return gpt == 2 ? sel(asc, stc, std::integral_constant<int, 2>{}) : sel(asc, stc, std::integral_constant<int, 1>{});
     };
     auto by_st = [&](auto asc) {
       switch (a.scale_t) {
@@ -487,5 +604,25 @@ hipError_t launch_gemm7(const GemmArgs& a, int bm, const _Float16* A16, int lda1
       return pick(std::integral_constant<int, 256>{});
   }
 }
+
+#if G7_BITS == 4
+// int4: groups of 32, 64 or 128 * 2^j; int2 / int8: 32 or 64 * 2^j (a whole number of groups per 64-deep half step, or
+// whole half steps per group)
+bool gemm7_ok(int bits, int blocksize, int fold_ok) {
+  if (!fold_ok) return false;
+  if (blocksize == 32 || blocksize == 64) return bits == 4 || bits == 2 || bits == 8;
+  const int unit = bits == 4 ? g7::KT : 64, r = blocksize / unit;
+  return (bits == 4 || bits == 2 || bits == 8) && blocksize % unit == 0 && (r & (r - 1)) == 0;
+}
+
+hipError_t launch_gemm7_b2(const GemmArgs& a, int bm, const _Float16* A16, int lda16, hipStream_t st);
+hipError_t launch_gemm7_b8(const GemmArgs& a, int bm, const _Float16* A16, int lda16, hipStream_t st);
+
+hipError_t launch_gemm7(const GemmArgs& a, int bits, int bm, const _Float16* A16, int lda16, hipStream_t st) {
+  return bits == 2   ? launch_gemm7_b2(a, bm, A16, lda16, st)
+         : bits == 8 ? launch_gemm7_b8(a, bm, A16, lda16, st)
+                     : launch_gemm7_b4(a, bm, A16, lda16, st);
+}
+#endif
 
 }  // namespace nad

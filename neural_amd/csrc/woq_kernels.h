@@ -200,7 +200,7 @@ hipError_t launch_gemm4(const GemmArgs& a, int bits, const _Float16* A16, int ld
 // prefill GEMM v7 (woq_gemm7.hip, the default for int4 groups of 128 * 2^j): gemm3's contract (256 x 128 tiles,
 // split-K partials, fp16 A padded to the 128-deep tile) with the group scale folded (needs DeviceWeight::fold_ok)
 bool gemm7_ok(int bits, int blocksize, int fold_ok);
-hipError_t launch_gemm7(const GemmArgs& a, int bm, const _Float16* A16, int lda16, hipStream_t stream);
+hipError_t launch_gemm7(const GemmArgs& a, int bits, int bm, const _Float16* A16, int lda16, hipStream_t stream);
 // mid-M GEMM (woq_gemm_mid.hip, 17 <= M <= 64): int4 / int2, gpt groups per K tile (1, 2, 4), rf = ceil(M / 16) row
 // fragments; grid = ceil(ns / S) * a.ksplit for the S of mid_geometry; a.ksplit > 1: launch_splitk_reduce follows
 void mid_geometry(int bits, int gpt, int act_t, int rf, int* s, int* nw, int* spw);

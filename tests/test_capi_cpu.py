@@ -213,7 +213,7 @@ def test_host_cache_key_is_constant_time_at_lm_head_shape():
 def test_plan_forward_kernel_choice():
     """nad_plan_forward (the host side of nad_device_forward with every launch recorded, no GPU): the decode shapes take
     the M = 1 / stripe-stream GEMVs, 17 <= M <= 64 the mid-M kernel, prefill takes gemm7 (int4 g128, the scale folded; gemm3 under NAD_GEMM_KERNEL=3)
-    or gemm4 (int2, int8), int4 g32 / g64 gemm7 as well, and few output tiles split K."""
+    -- as do int4 g32 / g64, int2 and int8 (gemm4 under NAD_GEMM_KERNEL=3) -- and few output tiles split K."""
     p = bestla.plan_forward
     assert p(4, 4096, 4096, 128, m=1)["kernel"] == "woq_gemv_m1_kernel"
     assert p(2, 14336, 4096, 64, m=1)["kernel"] == "woq_gemv_m1_kernel"
@@ -225,36 +225,35 @@ def test_plan_forward_kernel_choice():
     assert (r["kernel"], r["fold"], r["ksplit"]) == ("woq_gemm7_kernel", True, 1)
     assert r["launches"] == 2                       # fp32 activations: one fp16 conversion pass, then the GEMM
     assert p(4, 4096, 4096, 128, m=2048, act="fp16")["launches"] == 1
-    for bits, g in ((4, 32), (4, 64)):              # int4 g32 / g64: gemm7 with the scale per 32-deep step
+    for bits, g in ((4, 32), (4, 64), (2, 64), (8, 32), (8, 128)):   # gemm7: the scale per 32-deep step / half step
         r = p(bits, 4096, 4096, g, m=2048)
         assert (r["kernel"], r["fold"]) == ("woq_gemm7_kernel", True), (bits, g, r)
-    r = p(2, 4096, 4096, 64, m=2048)
-    assert (r["kernel"], r["fold"]) == ("woq_gemm4_kernel", True), r
     r = p(4, 4096, 4096, 128, m=64)                 # mid-M: fp32 activations read as they are, + the split-K reduce
     assert (r["kernel"], r["fold"], r["ksplit"], r["launches"]) == ("woq_mid_kernel", False, 4, 2), r
     r = p(4, 4096, 4096, 128, m=17, act="fp16")
     assert (r["kernel"], r["grid"], r["threads"]) == ("woq_mid_kernel", 256, 256), r
     assert p(4, 11008, 4096, 128, m=32)["ksplit"] == 2      # slabs within the workspace bound: ks x N <= 32768
     assert p(4, 32000, 4096, 128, m=32)["ksplit"] == 1
-    assert p(2, 4096, 4096, 64, m=33)["kernel"] == "woq_gemm4_kernel"   # int2 past 32 rows: the prefill GEMM
+    assert p(2, 4096, 4096, 64, m=33)["kernel"] == "woq_gemm7_kernel"   # int2 past 32 rows: the prefill GEMM
     r = p(4, 4096, 4096, 128, m=65)
     assert r["kernel"] == "woq_gemm7_kernel" and r["ksplit"] > 1 and r["launches"] == 3   # + the split-K reduce
     # int8 / int2 at g128 fold too (NAD_GEMM4_FOLD_ALL default since round 4)
     assert p(8, 4096, 4096, 128, m=2048)["fold"] and p(2, 4096, 4096, 128, m=2048)["fold"]
 
 
-def test_plan_gemm4_waves_split_over_k():
+def test_plan_gemm4_waves_split_over_k(knob):
     """gemm4's K-split wave layout (NAD_GEMM4_KSW=2, auto): on for more than one round of output tiles or K >= 8192
     (gate, down, lm_head, M = 4096), off for one round at K = 4096 (profiles/r04_gemm4_ksw_ab.txt) and under split-K.
-    Shown on int8 g32 (int4 g32 runs gemm7)."""
+    Shown on int8 g32 with gemm4 selected (NAD_GEMM_KERNEL=3; by default it runs gemm7)."""
     p = bestla.plan_forward
+    knob("NAD_GEMM_KERNEL", "3")
     assert not p(8, 4096, 4096, 32, m=2048)["ksw"]          # 256 tiles: one round on 256 CUs
     assert p(8, 4096, 4096, 32, m=4096)["ksw"]              # 512 tiles
     assert p(8, 11008, 4096, 32, m=2048)["ksw"]             # gate: 688 tiles
     assert p(8, 4096, 11008, 32, m=2048)["ksw"]             # down: K = 11008
     r = p(8, 4096, 11008, 32, m=64)
     assert r["ksplit"] > 1 and not r["ksw"]                 # split-K launches keep the M-split waves
-    assert not p(4, 4096, 4096, 128, m=4096)["ksw"]         # int4 g128: gemm7 (its own K split, not reported as ksw)
+    assert not p(4, 4096, 4096, 128, m=4096)["ksw"]         # int4 g128: gemm3 (no K-split waves; gemm7 by default)
 
 
 def test_host_cost_per_forward_under_3us():

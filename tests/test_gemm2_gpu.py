@@ -223,26 +223,38 @@ def test_gemm4_g32_scale_fold(oracle, knob, cfg):
 
 
 GEMM7_GROUP_CASES = [
-    # m, n, k, bs, stype, asym -- int4 groups of 32 / 64 on gemm7 (the group scale per 32-deep step)
-    (2048, 512, 1024, 32, F16, False),    # 256-row tiles
-    (300, 384, 640, 32, BF16, True),      # ragged M, 256-row tiles, 5 K tiles
-    (100, 130, 512, 32, F32, False),      # 128-row tile, ragged N (a partial stripe), f32 scales (the largest region)
-    (257, 300, 640, 32, F32, True),       # f32 asym: the 256-row tile's LDS at its largest (scales 2 KiB, zp 512 B)
-    (96, 130, 300, 64, F16, False),       # g64, K tail (zero padded), 128-row tile
-    (300, 200, 768, 64, BF16, True),      # g64 asym
-    (65, 1024, 4096, 32, F16, True),      # 128-row tile with split-K runs
-    (200, 640, 2048, 64, F32, True),      # 256-row tile with split-K runs
+    # m, n, k, bs, qtype, stype, asym -- gemm7 beyond int4 g128: int4 g32 / g64 (the group scale per 32-deep step), int2
+    # and int8 (half-step mode: the B slice, scales and zero points of every 64-deep half step loaded with it)
+    (2048, 512, 1024, 32, S4, F16, False),    # 256-row tiles
+    (300, 384, 640, 32, S4, BF16, True),      # ragged M, 256-row tiles, 5 K tiles
+    (100, 130, 512, 32, S4, F32, False),      # 128-row tile, ragged N (a partial stripe), f32 scales (the largest region)
+    (257, 300, 640, 32, S4, F32, True),       # f32 asym: the 256-row tile's LDS at its largest (scales 2 KiB, zp 512 B)
+    (96, 130, 300, 64, S4, F16, False),       # g64, K tail (zero padded), 128-row tile
+    (300, 200, 768, 64, S4, BF16, True),      # g64 asym
+    (65, 1024, 4096, 32, S4, F16, True),      # 128-row tile with split-K runs
+    (200, 640, 2048, 64, S4, F32, True),      # 256-row tile with split-K runs
+    (300, 256, 1024, 64, S2, F16, False),     # int2 g64 (Mistral): one group per half step
+    (257, 200, 768, 64, S2, BF16, True),      # int2 g64 asym, ragged, K = 3 int2 tiles
+    (100, 96, 640, 128, S2, F32, True),       # int2 g128, K tail inside a 256-deep tile, 128-row tile
+    (64, 1024, 4096, 256, S2, F16, False),    # int2 g256, 64-row tile with split-K runs
+    (48, 160, 1024, 1024, S2, F16, True),     # int2 per-channel (a group of 16 half steps)
+    (300, 256, 1024, 32, S8, F16, False),     # int8 g32: two groups per half step
+    (257, 300, 640, 32, S8, F32, True),       # int8 g32 f32 asym: the 256-row tile's int8 slices at their largest
+    (96, 130, 320, 128, S8, BF16, False),     # int8 g128, an odd half-step count (5 tiles: one all-zero padding step)
+    (200, 96, 1024, 256, S8, F16, True),      # int8 g256 asym
+    (33, 640, 2048, 64, S8, F16, False),      # int8, 64-row tile (M = 33) with split-K runs
 ]
 
 
 @pytest.mark.parametrize("cfg", GEMM7_GROUP_CASES)
 @pytest.mark.parametrize("act", ["fp32", "fp16", "bf16"])
 def test_gemm7_small_groups(oracle, knob, cfg, act):
-    """int4 g32 / g64 through gemm7 (q * s rounded once to fp16 per 32-deep group step): against the oracle at the fold
-    bar, against gemm4's folded launch (NAD_GEMM_KERNEL=3: the same fp16 weights up to the scale's own fp16 rounding)
-    and gemm4's exact fp32 group scales (NAD_GEMM4_FOLD=0); bit-repeatable."""
-    m, n, k, bs, st, asym = cfg
-    blob = _blob(oracle, n, k, bs, S4, st, asym, 4, seed=m + 11 * n + k)
+    """gemm7 at int4 g32 / g64, int2 and int8 (q * s rounded once to fp16): against the oracle at the fold bar, against
+    gemm4's folded launch (NAD_GEMM_KERNEL=3: the same fp16 weights up to the scale's own fp16 rounding) and gemm4's
+    exact fp32 group scales (NAD_GEMM4_FOLD=0); bit-repeatable."""
+    m, n, k, bs, qt, st, asym = cfg
+    knob("NAD_MID_MAX_M", "0")
+    blob = _blob(oracle, n, k, bs, qt, st, asym, 4, seed=m + 11 * n + k)
     w = bestla.DeviceWeight(blob)
     plan = w.plan(m, act)
     assert plan["kernel"] == "woq_gemm7_kernel" and plan["fold"], plan
@@ -267,7 +279,8 @@ def test_gemm7_small_groups(oracle, knob, cfg, act):
 
 def test_gemm4_takes_the_fallback_configs(oracle, knob):
     """With gemm4 disabled the same inputs run the register-staged kernel: both agree within fp32 accumulation noise
-    (they see identical fp16 A and exact weights)."""
+    (they see identical fp16 A and exact weights).  NAD_GEMM_KERNEL=3: int2 otherwise runs gemm7."""
+    knob("NAD_GEMM_KERNEL", "3")
     m, n, k = 200, 256, 1024
     blob = _blob(oracle, n, k, 64, S2, F16, True, 1, seed=5)
     w = bestla.DeviceWeight(blob)

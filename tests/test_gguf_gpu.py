@@ -78,6 +78,6 @@ def test_q4_0_fp_mode(oracle, m):
     w = bestla.DeviceWeight.from_q4_0(Wq, n, k)
     x = torch.from_numpy(rng.uniform(-1, 1, size=(m, k)).astype(np.float32)).half().cuda()
     ref = x.float().cpu().numpy().astype(np.float64) @ oracle.q4_0_dequant(Wq, n, k).T.astype(np.float64)
-    # M > 16 runs gemm4 at groups of 32, which folds the fp16 block scale into the fp16 weights (q * d rounded once:
+    # M > 16 runs the prefill GEMM (gemm7) at groups of 32, which folds the fp16 block scale into the fp16 weights (q * d rounded once:
     # tests/test_gemm2_gpu.py FOLD_TOL); the M = 1 GEMV keeps them exact
     assert _rel_err(w.forward(x).cpu().numpy(), ref) <= (2e-5 if m <= 16 else 5e-4)
