@@ -1100,6 +1100,35 @@ static int run_mid(const void* act, int act_t, int lda, int m, int k, const Devi
   return 1;
 }
 
+// gemm7's tile height (32 rows up to M = 32, else 64 / 128 / 256) by a cost model fitted to the K = 4096, N = 4096 /
+// 11008 sweeps (profiles/r05_gemm7_tile_height_sweep.txt): a launch takes the rounds of workgroups over the CUs, each
+// a fixed P (prologue, epilogue, output stores) plus its K run's half steps at h per half step (h grows with the tile
+// height: 0.35 / 0.55 / 0.95 us at 64 / 128 / 256 rows), plus, with split K, the reduce launch and the fp32 slabs
+// (written and read once, ~5 TB/s).  Picks within ~10 % of the best measured height at every swept M (the fixed
+// M-thresholds it replaces were up to 35 % off: N = 4096, M = 256 31.1 us against 22.7 with 64-row tiles).
+static int gemm7_pick_bm(const DeviceWeight& w, int m) {
+  if (m <= 32) return 32;
+  static const int bms[3] = {64, 128, 256};
+  static const double hs_us[3] = {0.35, 0.55, 0.95}, fixed_us[3] = {5.5, 5.0, 8.0};
+  const int cus = device_cus();
+  const int hpt = k_tile(w) / 64;
+  int best = 256;
+  double best_t = 1e30;
+  for (int i = 0; i < 3; i++) {
+    int kt = w.nt;
+    const int ks = splitk_plan(w, m, &kt, bms[i]);
+    const long tiles = long((m + bms[i] - 1) / bms[i]) * ((w.ns + 7) / 8);
+    const long rounds = (tiles * ks + cus - 1) / cus;
+    double t = double(rounds) * (fixed_us[i] + double(kt) * hpt * hs_us[i]);
+    if (ks > 1) t += 2.0 + double(m) * w.n * ks * 8.0 / 5e6;
+    if (t < best_t) {
+      best_t = t;
+      best = bms[i];
+    }
+  }
+  return best;
+}
+
 static int run_gemm(const void* act, int act_t, int lda, int m, int k, const DeviceWeight& w, float* out, int ldo,
                     int epi, const float* bias, int bias_ld, const float* res, int ld_res, const float* aux,
                     int ld_aux, hipStream_t st, const A16* pre = nullptr, const Half16* h16 = nullptr) {
@@ -1166,11 +1195,9 @@ static int run_gemm(const void* act, int act_t, int lda, int m, int k, const Dev
     // (profiles/r05_gemm7_*); a weight whose q * s leaves the fp16 normal range, or NAD_GEMM_KERNEL=3, runs gemm3
     const bool g7 = pg == 3 && kn.gemm_kernel == 7 && gemm7_ok(w.bits, w.blocksize, w.fold_ok);
     if (g7) a.fold = 1;
-    // gemm7's tile height: the problem's rows rounded up to 32 / 64 / 128, else 256 (mid-M launches split K so the
-    // output tiles fill the chip: 17 <= M <= 256 was a 256-row tile of which most rows re-read the last one)
     int bm = 256;
     if (g7) {
-      bm = kn.gemm7_bm > 0 ? kn.gemm7_bm : (m <= 32 ? 32 : (m <= 64 ? 64 : (m <= 128 ? 128 : 256)));
+      bm = kn.gemm7_bm > 0 ? kn.gemm7_bm : gemm7_pick_bm(w, m);
       if (bm != 32 && bm != 64 && bm != 128) bm = 256;
     }
     int ktiles = w.nt;
