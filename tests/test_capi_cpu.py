@@ -237,6 +237,12 @@ def test_plan_forward_kernel_choice():
     assert p(2, 4096, 4096, 64, m=33)["kernel"] == "woq_gemm7_kernel"   # int2 past 32 rows: the prefill GEMM
     r = p(4, 4096, 4096, 128, m=65)
     assert r["kernel"] == "woq_gemm7_kernel" and r["ksplit"] > 1 and r["launches"] == 3   # + the split-K reduce
+    # gemm7's tile height (cost model, profiles/r05_gemm7_tile_height_sweep.txt) as launch geometry: M = 256 at N = 4096
+    # takes 64-row tiles (128 tiles, split 2: 256 workgroups), M = 1024 128-row tiles (256, one round), M = 2048 256-row
+    # (256 tiles); N = 11008 M = 640 128-row tiles (430 over 2 rounds, not 258 256-row tiles over 2)
+    for m, n, grid, ks in ((256, 4096, 256, 2), (1024, 4096, 256, 1), (2048, 4096, 256, 1), (640, 11008, 430, 1)):
+        r = p(4, n, 4096, 128, m=m, act="fp16")
+        assert (r["kernel"], r["grid"], r["ksplit"]) == ("woq_gemm7_kernel", grid, ks), (m, n, r)
     # int8 / int2 at g128 fold too (NAD_GEMM4_FOLD_ALL default since round 4)
     assert p(8, 4096, 4096, 128, m=2048)["fold"] and p(2, 4096, 4096, 128, m=2048)["fold"]
 
