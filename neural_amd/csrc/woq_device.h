@@ -88,13 +88,20 @@ __device__ __forceinline__ Dq2c dq2_consts(int bias_plus_zp) {
   const float b = float(bias_plus_zp);
   return Dq2c{h2_splat(-(1024.f + b)), h2_splat(-(256.f + b)), h2_splat(-(64.f + b)), h2_splat(-(16.f + b))};
 }
+// (x & m) | c as ONE v_and_or_b32 (hipcc emits v_and_b32 + v_or_b32 for the C form: the literal mask and magic cannot
+// share a VOP3 on gfx9; here the mask sits in an SGPR and the magic in a VGPR)
+__device__ __forceinline__ uint32_t dq_and_or(uint32_t x, uint32_t m, uint32_t c) {
+  uint32_t r;
+  asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "s"(m), "v"(c));
+  return r;
+}
 // x: the dword already shifted right by 8 for the odd step (b[d >> 1] >> ((d & 1) * 8))
 __device__ __forceinline__ h8_t dequant2s(uint32_t x, const Dq2c& c) {
   const uint32_t mag = 0x64006400u;
-  const h2_t p0 = as_h2((x & 0x00030003u) | mag) + c.c0;
-  const h2_t p1 = __builtin_elementwise_fma(as_h2((x & 0x000C000Cu) | mag), h2_splat(0.25f), c.c1);
-  const h2_t p2 = __builtin_elementwise_fma(as_h2((x & 0x00300030u) | mag), h2_splat(0.0625f), c.c2);
-  const h2_t p3 = __builtin_elementwise_fma(as_h2((x & 0x00C000C0u) | mag), h2_splat(0.015625f), c.c3);
+  const h2_t p0 = as_h2(dq_and_or(x, 0x00030003u, mag)) + c.c0;
+  const h2_t p1 = __builtin_elementwise_fma(as_h2(dq_and_or(x, 0x000C000Cu, mag)), h2_splat(0.25f), c.c1);
+  const h2_t p2 = __builtin_elementwise_fma(as_h2(dq_and_or(x, 0x00300030u, mag)), h2_splat(0.0625f), c.c2);
+  const h2_t p3 = __builtin_elementwise_fma(as_h2(dq_and_or(x, 0x00C000C0u, mag)), h2_splat(0.015625f), c.c3);
   h8_t r;
   r[0] = p0[0];
   r[1] = p0[1];
