@@ -1,4 +1,4 @@
-"""Mistral-7B int2-g64 policy decode token (bench.decode_workload, no prefill): development tool for A/B builds
+"""Decode token (Mistral-7B int2-g64 policy; `llama` / `llama_asym` for the Llama-2-7B stacks) (bench.decode_workload, no prefill): development tool for A/B builds
 (NAD_LIB_PATH)."""
 import json
 import os
@@ -10,5 +10,6 @@ import torch  # noqa: E402
 
 import bench  # noqa: E402
 
-cfg = bench.MISTRAL if (len(sys.argv) < 2 or sys.argv[1] == "mistral") else bench.LLAMA_ASYM
+which = sys.argv[1] if len(sys.argv) > 1 else "mistral"
+cfg = {"mistral": bench.MISTRAL, "llama": bench.LLAMA, "llama_asym": bench.LLAMA_ASYM}[which]
 print(json.dumps(bench.decode_workload(cfg, torch, reps=20, prefill=False)), flush=True)
