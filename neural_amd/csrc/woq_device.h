@@ -29,6 +29,14 @@ __device__ __forceinline__ float load_scale(const void* p, size_t i, int st) {
 
 __device__ __forceinline__ h2_t as_h2(uint32_t v) { return __builtin_bit_cast(h2_t, v); }
 
+// (x & m) | c as ONE v_and_or_b32 (hipcc emits v_and_b32 + v_or_b32 for the C form: the literal mask and magic cannot
+// share a VOP3 on gfx9; here the mask sits in an SGPR and the magic in a VGPR)
+__device__ __forceinline__ uint32_t dq_and_or(uint32_t x, uint32_t m, uint32_t c) {
+  uint32_t r;
+  asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "s"(m), "v"(c));
+  return r;
+}
+
 // One MFMA step's B fragment (8 fp16 = exact integers q - zp) from the packed dwords.
 //   c2 = (-(1024 + bias + zp)) broadcast as half2.
 template <int BITS>
@@ -36,17 +44,17 @@ __device__ __forceinline__ h8_t dequant_step(const u4_t& b, int d, h2_t c2) {
   h2_t p0, p1, p2, p3;
   if constexpr (BITS == 4) {
     uint32_t w = b[d];
-    p0 = as_h2(((w >> 0) & 0x000F000Fu) | 0x64006400u);
-    p1 = as_h2(((w >> 4) & 0x000F000Fu) | 0x64006400u);
-    p2 = as_h2(((w >> 8) & 0x000F000Fu) | 0x64006400u);
-    p3 = as_h2(((w >> 12) & 0x000F000Fu) | 0x64006400u);
+    p0 = as_h2(dq_and_or(w, 0x000F000Fu, 0x64006400u));
+    p1 = as_h2(dq_and_or(w >> 4, 0x000F000Fu, 0x64006400u));
+    p2 = as_h2(dq_and_or(w >> 8, 0x000F000Fu, 0x64006400u));
+    p3 = as_h2(dq_and_or(w >> 12, 0x000F000Fu, 0x64006400u));
   } else if constexpr (BITS == 2) {
     uint32_t w = b[d >> 1];
     int sh = (d & 1) * 8;
-    p0 = as_h2(((w >> (sh + 0)) & 0x00030003u) | 0x64006400u);
-    p1 = as_h2(((w >> (sh + 2)) & 0x00030003u) | 0x64006400u);
-    p2 = as_h2(((w >> (sh + 4)) & 0x00030003u) | 0x64006400u);
-    p3 = as_h2(((w >> (sh + 6)) & 0x00030003u) | 0x64006400u);
+    p0 = as_h2(dq_and_or(w >> (sh + 0), 0x00030003u, 0x64006400u));
+    p1 = as_h2(dq_and_or(w >> (sh + 2), 0x00030003u, 0x64006400u));
+    p2 = as_h2(dq_and_or(w >> (sh + 4), 0x00030003u, 0x64006400u));
+    p3 = as_h2(dq_and_or(w >> (sh + 6), 0x00030003u, 0x64006400u));
   } else {
     uint32_t w0 = b[2 * d], w1 = b[2 * d + 1];
     p0 = as_h2(__builtin_amdgcn_perm(0x64646464u, w0, 0x04010400u));
@@ -87,13 +95,6 @@ __device__ __forceinline__ h2_t h2_splat(float v) {
 __device__ __forceinline__ Dq2c dq2_consts(int bias_plus_zp) {
   const float b = float(bias_plus_zp);
   return Dq2c{h2_splat(-(1024.f + b)), h2_splat(-(256.f + b)), h2_splat(-(64.f + b)), h2_splat(-(16.f + b))};
-}
-// (x & m) | c as ONE v_and_or_b32 (hipcc emits v_and_b32 + v_or_b32 for the C form: the literal mask and magic cannot
-// share a VOP3 on gfx9; here the mask sits in an SGPR and the magic in a VGPR)
-__device__ __forceinline__ uint32_t dq_and_or(uint32_t x, uint32_t m, uint32_t c) {
-  uint32_t r;
-  asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "s"(m), "v"(c));
-  return r;
 }
 // x: the dword already shifted right by 8 for the odd step (b[d >> 1] >> ((d & 1) * 8))
 __device__ __forceinline__ h8_t dequant2s(uint32_t x, const Dq2c& c) {
