@@ -238,7 +238,10 @@ GEMM7_GROUP_CASES = [
     (100, 96, 640, 128, S2, F32, True),       # int2 g128, K tail inside a 256-deep tile, 128-row tile
     (64, 1024, 4096, 256, S2, F16, False),    # int2 g256, 64-row tile with split-K runs
     (48, 160, 1024, 1024, S2, F16, True),     # int2 per-channel (a group of 16 half steps)
+    (200, 256, 1024, 32, S2, F16, False),     # int2 g32: two groups per half step
+    (100, 130, 768, 32, S2, F32, True),       # int2 g32 f32 asym, ragged N, 3 int2 tiles
     (300, 256, 1024, 32, S8, F16, False),     # int8 g32: two groups per half step
+    (96, 200, 512, 512, S8, BF16, True),      # int8 per-channel asym (one group of 8 half steps)
     (257, 300, 640, 32, S8, F32, True),       # int8 g32 f32 asym: the 256-row tile's int8 slices at their largest
     (96, 130, 320, 128, S8, BF16, False),     # int8 g128, an odd half-step count (5 tiles: one all-zero padding step)
     (200, 96, 1024, 256, S8, F16, True),      # int8 g256 asym
@@ -250,8 +253,8 @@ GEMM7_GROUP_CASES = [
 @pytest.mark.parametrize("act", ["fp32", "fp16", "bf16"])
 def test_gemm7_small_groups(oracle, knob, cfg, act):
     """gemm7 at int4 g32 / g64, int2 and int8 (q * s rounded once to fp16): against the oracle at the fold bar, against
-    gemm4's folded launch (NAD_GEMM_KERNEL=3: the same fp16 weights up to the scale's own fp16 rounding) and gemm4's
-    exact fp32 group scales (NAD_GEMM4_FOLD=0); bit-repeatable."""
+    gemm4's folded launch (NAD_GEMM_KERNEL=3: the same fp16 weights up to the scale's own fp16 rounding; int2 g32, which
+    gemm4 does not take, the generic tiled GEMM) and gemm4's exact fp32 group scales (NAD_GEMM4_FOLD=0); bit-repeatable."""
     m, n, k, bs, qt, st, asym = cfg
     knob("NAD_MID_MAX_M", "0")
     blob = _blob(oracle, n, k, bs, qt, st, asym, 4, seed=m + 11 * n + k)
@@ -267,7 +270,7 @@ def test_gemm7_small_groups(oracle, knob, cfg, act):
     assert _rel_err(y, ref) <= max(TOL[act], FOLD_TOL), (_rel_err(y, ref), plan)
     assert np.array_equal(w.forward(x).cpu().numpy(), y)
     knob("NAD_GEMM_KERNEL", "3")
-    assert w.plan(m, act)["kernel"] == "woq_gemm4_kernel"
+    assert w.plan(m, act)["kernel"] in ("woq_gemm4_kernel", "woq_gemm_kernel")  # int2 g32: the generic tiled GEMM
     y4 = w.forward(x).cpu().numpy()
     assert _rel_err(y, y4.astype(np.float64)) <= FOLD_TOL
     knob("NAD_GEMM_KERNEL", "7")
