@@ -1053,7 +1053,7 @@ static int run_mid(const void* act, int act_t, int lda, int m, int k, const Devi
   // slabs within nad_device_workspace_size's N-independent bound (m x 128 KiB past the fp16 copy): ks x N <= 32768,
   // so wide weights split K less (N = 11008: 2 runs, 172 x 2 workgroups; N = 32000: none, 500 workgroups)
   ks = std::max(1, std::min(ks, 32768 / ((w.n + 3) / 4 * 4)));
-  if (kn.mid_ks > 0) ks = std::min(kn.mid_ks, w.nt);
+  if (kn.mid_ks > 0) ks = std::max(1, std::min({kn.mid_ks, w.nt, 32768 / ((w.n + 3) / 4 * 4)}));
   const int ktiles = (w.nt + ks - 1) / ks;
   ks = (w.nt + ktiles - 1) / ktiles;
   GemmArgs a{};
@@ -1193,7 +1193,8 @@ static int run_gemm(const void* act, int act_t, int lda, int m, int k, const Dev
     const bool g2 = pg == 3 && kn.gemm_kernel == 2;
     // gemm7 (group scale folded, waves split over K) is the default for int4 groups of 128 * 2^j: +5-10 % over gemm3
     // (profiles/r05_gemm7_*); a weight whose q * s leaves the fp16 normal range, or NAD_GEMM_KERNEL=3, runs gemm3
-    const bool g7 = pg == 3 && kn.gemm_kernel == 7 && gemm7_ok(w.bits, w.blocksize, w.fold_ok);
+    // (as for gemm4, NAD_GEMM4_FOLD=0 turns the fold off: int4 g128 then runs gemm3's exact fp32 group scale)
+    const bool g7 = pg == 3 && kn.gemm_kernel == 7 && kn.gemm4_fold && gemm7_ok(w.bits, w.blocksize, w.fold_ok);
     if (g7) a.fold = 1;
     int bm = 256;
     if (g7) {
@@ -1266,7 +1267,9 @@ extern "C" int nad_device_forward(const void* act, int act_dtype, const void* de
   }
   hipStream_t st = static_cast<hipStream_t>(queue);
   if (m <= kSkinnyMaxM) {
-    if (!int8_compute(*w)) {  // the mid-M kernel where NAD_MID_MIN_M reaches below 17 (tests / tuning)
+    // the mid-M kernel from 12 rows of fp16 activations / 8 of fp32 / bf16 (NAD_MID_MIN_M); below that, and for the
+    // fused QKV / FFN entries at any M <= 16, the skinny GEMV.  Its split-K slabs fit nad_device_workspace_size(m, k).
+    if (!int8_compute(*w)) {
       const int r = run_mid(act, act_dtype, lda, m, k, *w, out, ldo, epi, bias, bias_ld, res, ld_res, nullptr, 0, st,
                             nullptr, nullptr);
       if (r != 0) return r < 0 ? -1 : 0;

@@ -474,12 +474,15 @@ extern "C" size_t nad_device_workspace_size(int m, int k) {
   // K padded to the largest device K tile (256: int2), so the bound holds for every weight format
   const size_t kp = (size_t(k) + 255) / 256 * 256;
   auto a256 = [](size_t x) { return (x + 255) / 256 * 256; };
-  // m <= 16: the fp decode GEMV stages its activations in LDS; a weight in the int8-compute mode quantizes them into
-  // u8 codes [m][kp] + per-(row, block) {scale, zp} (block >= 32)
-  if (m <= 16) return a256(size_t(m) * kp) + a256(size_t(m) * (kp / 32) * 8) + 256;
-  // fp16 copy of A (tile padded), then the split-K partials of a GEMM with few output tiles (bound for any N)
+  // fp16 copy of A (tile padded), then the split-K partials of a GEMM with few output tiles (bound for any N); the
+  // mid-M kernel's K-run slabs (ks x N <= 32768 fp32 per row, capi.hip run_mid) fit the same m x 128 KiB
   const size_t nbm = (size_t(m) + 255) / 256;
-  return a256(size_t(m) * kp * 2) + size_t(m) * 4 * 256 * 128 / nbm + 256;
+  const size_t gemm = a256(size_t(m) * kp * 2) + size_t(m) * 4 * 256 * 128 / nbm + 256;
+  // m <= 16: the fp decode GEMV stages its activations in LDS; a weight in the int8-compute mode quantizes them into
+  // u8 codes [m][kp] + per-(row, block) {scale, zp} (block >= 32); the mid-M kernel runs from 8 / 12 rows by default
+  // (from any m with NAD_MID_MIN_M), so its split-K slabs are covered here too
+  if (m <= 16) return std::max(a256(size_t(m) * kp) + a256(size_t(m) * (kp / 32) * 8) + 256, gemm);
+  return gemm;
 }
 
 // ne_bestla.cpp:205-249 + the device workspace of this backend's prefill GEMM (the reference's SYCL path reports 0)

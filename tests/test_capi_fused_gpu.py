@@ -227,6 +227,37 @@ def test_device_forward_uses_caller_workspace_and_capture_contract(oracle):
     L.nad_bind_workspace(C.c_void_p(st2.cuda_stream), None, 0)
 
 
+@pytest.mark.parametrize("m", [8, 16])
+def test_mid_m_capture_with_bound_workspace(oracle, m):
+    """at M = 8..16 fp32 rows take the mid-M kernel with split-K slabs; nad_device_workspace_size(m, k)
+    covers them, so graph capture with a workspace of exactly that size replays correctly (no 'needs N bytes')."""
+    L = _lib.lib()
+    n, k = 512, 4096
+    blob = _wb(oracle, n, k, 11)
+    w = bestla.DeviceWeight(blob)
+    p = w.plan(m, "fp32")
+    assert p["kernel"] == "woq_mid_kernel" and p["ksplit"] > 1, p
+    A = np.random.default_rng(m).uniform(-1, 1, size=(m, k)).astype(np.float32)
+    ref = oracle.forward(A, blob, n, k)
+    x = torch.from_numpy(A).cuda()
+    ws_bytes = L.nad_device_workspace_size(m, k)
+    st = torch.cuda.Stream()
+    st.wait_stream(torch.cuda.current_stream())
+    ws = torch.zeros(ws_bytes, dtype=torch.uint8, device="cuda")
+    assert L.nad_bind_workspace(C.c_void_p(st.cuda_stream), C.c_void_p(ws.data_ptr()), ws_bytes) == 0
+    y = torch.zeros(m, n, device="cuda")
+    g = torch.cuda.CUDAGraph()
+    try:
+        with torch.cuda.stream(st):
+            with torch.cuda.graph(g, stream=st):
+                w.forward(x, out=y, stream=st)
+        g.replay()
+        torch.cuda.synchronize()
+    finally:
+        L.nad_bind_workspace(C.c_void_p(st.cuda_stream), None, 0)
+    assert _rel_err(y.cpu().numpy(), ref) <= 2e-5
+
+
 def test_host_cache_code_only_rewrite_and_lru_bound(oracle):
     """(1) a rewrite that changes only the CODES and keeps every scale, through the pack API
     (BTLAGemmPackB into the same buffer) or by another writer followed by nad_host_cache_evict, is seen by the next

@@ -88,6 +88,8 @@ def test_mid_matches_prefill_and_gemv(oracle, knob):
     w = bestla.DeviceWeight(blob)
     x = _x(m, k, "fp16", 8)
     y = w.forward(x).cpu().numpy()
+    knob("NAD_MID_MIN_M", "17")  # fp16 rows take the mid-M kernel from 12: force the GEMV for the M = 16 cross-check
+    assert w.plan(16, "fp16")["kernel"] == "woq_gemv_kernel"
     y16 = w.forward(x[:16].contiguous()).cpu().numpy()
     assert _rel_err(y[:16], y16.astype(np.float64)) <= 2e-5
     knob("NAD_MID_MAX_M", "0")

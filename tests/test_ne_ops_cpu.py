@@ -51,6 +51,9 @@ def test_workspace_bound_covers_every_k_tile():
             kp = -(-k // 256) * 256
             need = _a256(m * kp) + _a256(m * (kp // 32) * 8)          # i8_act_bytes at the smallest group (32)
             assert L.nad_device_workspace_size(m, k) >= need, (m, k)
+        for m in (1, 8, 12, 16):  # the mid-M kernel (from 8 / 12 rows by default): fp16 room + ks x N <= 32768 slabs
+            a16 = _a256(m * (-(-k // 256) * 256) * 2)
+            assert L.nad_device_workspace_size(m, k) >= a16 + m * 32768 * 4, (m, k)
         for m in (17, 300, 2048):
             for ktile in (64, 128, 256):
                 kp = -(-k // ktile) * ktile
