@@ -65,6 +65,16 @@ __device__ unsigned long long nad_trace_buf[kTraceSlots][kTraceMaxWg];
   } while (0)
 #endif
 
+// M = 1 kernel tail: partial-sum slots laid out per column so a 16-wave launch reduces with four 16-B LDS reads per
+// output and no per-slot clamps (the general form's 16 clamped offsets + masks are ~100 scalar instructions executed
+// once per launch, cold in the instruction cache: ~0.4 us per KB).  Measured (profiles/r06_gemv_tail_ab.txt, same
+// box, alternating): O 4.80 -> 4.55 us, decode 946-951 -> 969-972 tok/s; bit-identical sums (same order).  A
+// branch-free first weight stage (the two-armed load_stage makes hipcc wait vmcnt(0) for the activation loads before
+// the first weight load) measured neutral (943-947 tok/s) and was not kept.
+#ifndef NAD_GEMV_LEAN_TAIL
+#define NAD_GEMV_LEAN_TAIL 1
+#endif
+
 constexpr int kOOB = 0x7FFF0000;  // a buffer offset past every resource: the load returns 0 and touches no memory
 
 // virtual stripe -> (weight index, stripe within that weight); all wave-uniform
@@ -737,7 +747,11 @@ __device__ __forceinline__ void m1_body(GemvArgs& a, int bid) {
       if constexpr (HL) {
         r += __shfl_down(r, 32, 64);
       }
+#if NAD_GEMV_LEAN_TAIL
+      if (lane < 16) part[(size_t(cj) * 16 + lane) * NW + wave] = r;  // [nv][16 columns][NW]: a column's slots together
+#else
       if (lane < 16) part[(size_t(cj) * NW + wave) * 16 + lane] = r;
+#endif
       acc = f4_t{0.f, 0.f, 0.f, 0.f};
       cq = wave;
       cs = 0;
@@ -758,37 +772,13 @@ __device__ __forceinline__ void m1_body(GemvArgs& a, int bid) {
   // 4) sum each stripe's wave slots in wave order and apply the epilogue
   const int nout = (u1 - u0) * 16;
   const int nwl = min(NW, nsl);
-  for (int o = threadIdx.x; o < nout; o += blockDim.x) {
-    const int p = o >> 4, nn = o & 15;
-    float y[2] = {0.f, 0.f};
-#pragma unroll
-    for (int h = 0; h < 2; h++) {
-      if (h < vpu) {  // all slots read at once (one LDS round trip), summed in the general kernel's order
-        const float* ps = part + size_t(p * vpu + h) * NW * 16 + nn;
-        float t[16];
-#pragma unroll
-        for (int w = 0; w < 16; w++) t[w] = ps[min(w, nwl - 1) * 16];
-        const int full = nwl & ~3;
-        float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-#pragma unroll
-        for (int w = 0; w < 16; w += 4)
-          if (w < full) {
-            s0 += t[w];
-            s1 += t[w + 1];
-            s2 += t[w + 2];
-            s3 += t[w + 3];
-          }
-#pragma unroll
-        for (int w = 0; w < 16; w++)
-          if (w >= full && w < nwl) s0 += t[w];
-        y[h] = (s0 + s1) + (s2 + s3);
-      }
-    }
+  // the fused epilogue of output o = (local stripe p, column nn) from its stripe sum(s) y
+  auto emit = [&](int p, int nn, const float (&y)[2]) {
     int wsel, s;
     vstripe(a, v0 + p * vpu, wsel, s);
     if (a.dual) wsel = 0;
     const int n = s * 16 + nn;
-    if (n >= sel3(wsel, a.w[0].n, a.w[1].n, a.w[2].n)) continue;
+    if (n >= sel3(wsel, a.w[0].n, a.w[1].n, a.w[2].n)) return;
     float* out = sel3(wsel, a.w[0].out, a.w[1].out, a.w[2].out);
     float v = y[0];
     switch (a.epi) {
@@ -823,6 +813,63 @@ __device__ __forceinline__ void m1_body(GemvArgs& a, int bid) {
         break;
     }
     out[n] = v;
+  };
+#if NAD_GEMV_LEAN_TAIL
+  if (nwl == 16 && NW == 16) {  // 16 waves with a slice each: four 16-B reads per column, no clamps or masks
+    for (int o = threadIdx.x; o < nout; o += blockDim.x) {
+      const int p = o >> 4, nn = o & 15;
+      float y[2] = {0.f, 0.f};
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        if (h < vpu) {
+          const float4* ps = reinterpret_cast<const float4*>(part + (size_t(p * vpu + h) * 16 + nn) * 16);
+          const float4 t0 = ps[0], t1 = ps[1], t2 = ps[2], t3 = ps[3];
+          // the general order below at nwl = 16: s_i sums slots i, i + 4, i + 8, i + 12
+          const float s0 = ((t0.x + t1.x) + t2.x) + t3.x, s1 = ((t0.y + t1.y) + t2.y) + t3.y;
+          const float s2 = ((t0.z + t1.z) + t2.z) + t3.z, s3 = ((t0.w + t1.w) + t2.w) + t3.w;
+          y[h] = (s0 + s1) + (s2 + s3);
+        }
+      }
+      emit(p, nn, y);
+    }
+    NAD_TRACE(3);
+    return;
+  }
+#endif
+  for (int o = threadIdx.x; o < nout; o += blockDim.x) {
+    const int p = o >> 4, nn = o & 15;
+    float y[2] = {0.f, 0.f};
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      if (h < vpu) {  // all slots read at once (one LDS round trip), summed in the general kernel's order
+#if NAD_GEMV_LEAN_TAIL
+        const float* ps = part + (size_t(p * vpu + h) * 16 + nn) * NW;
+#define NAD_SLOT(w) ps[w]
+#else
+        const float* ps = part + size_t(p * vpu + h) * NW * 16 + nn;
+#define NAD_SLOT(w) ps[(w) * 16]
+#endif
+        float t[16];
+#pragma unroll
+        for (int w = 0; w < 16; w++) t[w] = NAD_SLOT(min(w, nwl - 1));
+#undef NAD_SLOT
+        const int full = nwl & ~3;
+        float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+#pragma unroll
+        for (int w = 0; w < 16; w += 4)
+          if (w < full) {
+            s0 += t[w];
+            s1 += t[w + 1];
+            s2 += t[w + 2];
+            s3 += t[w + 3];
+          }
+#pragma unroll
+        for (int w = 0; w < 16; w++)
+          if (w >= full && w < nwl) s0 += t[w];
+        y[h] = (s0 + s1) + (s2 + s3);
+      }
+    }
+    emit(p, nn, y);
   }
   NAD_TRACE(3);
 }

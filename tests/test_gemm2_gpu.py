@@ -436,3 +436,31 @@ def test_gemm_mid_m(oracle, knob, m, fmt):
         y3 = w.forward(x).cpu().numpy()
         assert _rel_err(y, y3.astype(np.float64)) <= FOLD_TOL
 
+
+
+@pytest.mark.parametrize("edge,folds", [
+    (2.0 ** -14, True),                  # the smallest scale whose q * s is an fp16 normal for every |q| >= 1
+    (2.0 ** -14 * (1 - 2.0 ** -20), False),
+    (65504.0 / 8, True),                 # int4 sym: qmax * s = 8 * 8188 = 65504, the largest fp16
+    (65504.0 / 8 * (1 + 2.0 ** -20), False),
+])
+def test_fold_range_edge_scales(oracle, edge, folds):
+    """the load-time fold check (capi.hip scale_in_fold_range) at the edges of the fp16 range.  A
+    blob whose group scales sit exactly on an edge folds q * s into fp16 (gemm7) and is held to FOLD_TOL; one just past
+    it runs the exact fp32 group-scale path (gemm3) and is held to the fp16-activation bar, both against the oracle."""
+    m, n, k, g = 128, 256, 1024, 128
+    rng = np.random.default_rng(17)
+    q = rng.integers(-8, 8, size=(k, n)).astype(np.int8)
+    s = rng.uniform(0.001, 0.01, size=(k // g, n)).astype(np.float32)
+    s[::3, ::5] = np.float32(edge)       # a sprinkling of edge scales over groups and columns
+    s[1, 7] = -np.float32(edge)          # the check takes |s|
+    blob = bestla.qpack(q, s, weight_dtype="int4", group_size=g, alg="sym", scale_dtype="fp32", compute_dtype="fp32")
+    w = bestla.DeviceWeight(blob)
+    p = w.plan(m, "fp16")
+    assert p["fold"] == folds, p
+    assert p["kernel"] == ("woq_gemm7_kernel" if folds else "woq_gemm3_kernel"), p
+    x = torch.from_numpy(rng.uniform(-0.5, 0.5, size=(m, k)).astype(np.float32)).cuda().half()
+    ref = oracle.forward(x.float().cpu().numpy(), blob, n, k)
+    y = w.forward(x).cpu().numpy()
+    assert np.isfinite(y).all()
+    assert _rel_err(y, ref) <= (FOLD_TOL if folds else TOL["fp16"]), _rel_err(y, ref)

@@ -53,7 +53,7 @@ def _block(x, wq, wo, w1, w3, w2, ctx, world):
     return w2(t)
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, big=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", NAD_TP_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
     torch.set_num_threads(1)
@@ -64,7 +64,8 @@ def _worker(rank, world, port, q):
         o = Oracle.get()
         ctx = ParallelContext("tcp")
         assert ctx.get_tp_size() == world and ctx.get_tp_rank() == rank
-        d, f, gs = 128, 320, 32  # hidden, ffn (10 groups of 32: uneven K shards at world 4)
+        # hidden, ffn: 10 groups of 32 give uneven K shards at world 4; world 8 takes 8 / 11 groups (2,2,2,1,...)
+        d, f, gs = (256, 352, 32) if big else (128, 320, 32)
         names = {"wq": (".attention.wq.weight", d, d), "wo": (".attention.wo.weight", d, d),
                  "w1": (".feed_forward.w1.weight", f, d), "w3": (".feed_forward.w3.weight", f, d),
                  "w2": (".feed_forward.w2.weight", d, f)}
@@ -104,11 +105,11 @@ def _worker(rank, world, port, q):
         q.put((rank, "ERR", traceback.format_exc() + str(e)))
 
 
-def _run(world):
+def _run(world, big=False):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    ps = [ctx.Process(target=_worker, args=(r, world, port, q, big)) for r in range(world)]
     for p in ps:
         p.start()
     res = [q.get(timeout=240) for _ in range(world)]
@@ -119,10 +120,10 @@ def _run(world):
     return sorted(res, key=lambda r: r[0])
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_tp_block_matches_single_rank(world):
-    single = _run(1)[0]
-    multi = _run(world)
+    single = _run(1, world == 8)[0]
+    multi = _run(world, world == 8)
     for _, y, fq in multi:
         scale = np.abs(single[1]).max()
         assert np.abs(y - single[1]).max() <= 1e-5 * scale   # only the all-reduce order differs
