@@ -1414,3 +1414,95 @@ void orc_quantize_f8_rowblock(const float* src, int8_t* dst, int row, int col, i
     }
   }
 }
+
+/* The CPU baseline's GEMV with AVX-512 (test infrastructure: bench.py cpu_baseline only): the arithmetic of
+ * orc_blob_gemv_ref for int4 weights at m = 1 on an NTILE-48 PACK_ROW-1 blob, reassociated the way a SIMD kernel does
+ * it -- per quantization block t[col] = sum_k a_k * nibble_k by FMA chains (16 columns per zmm, the columns of a byte's
+ * low and high nibbles in separate accumulators, one interleave per block), then acc += (t - (8 + zp) sum_k a_k) s with
+ * the block's scales converted 16 at a time (F16C / bf16 shift) -- within
+ * fp32 reassociation of the scalar restatement (tests/test_oracle_golden.py::test_avx512_gemv_matches_scalar).  The
+ * reference's own AVX512F / AMX cores (kernel_avx512f.h, bestla_gemm.h) need xbyak and are unbuildable here.
+ * Returns -7 when the host has no AVX-512 (the caller falls back to orc_blob_gemv_par). */
+#include <immintrin.h>
+
+__attribute__((target("avx512f,avx512bw,avx2,fma,f16c"))) static __m512 scales16(const uint8_t* sp, size_t ci,
+                                                                                  uint32_t scat) {
+  if (scat == ORC_F32) return _mm512_loadu_ps((const float*)(sp + ci * 4));
+  const __m256i h = _mm256_loadu_si256((const __m256i*)(sp + ci * 2));
+  if (scat == ORC_BF16) return _mm512_castsi512_ps(_mm512_slli_epi32(_mm512_cvtepu16_epi32(h), 16));
+  return _mm512_cvtph_ps(h);
+}
+
+__attribute__((target("avx512f,avx512bw,avx2,fma,f16c"))) static void gemv4_nt48_avx512(const float* A,
+                                                                                        const uint8_t* bp,
+                                                                                        const uint8_t* sp,
+                                                                                        const int8_t* zp,
+                                                                                        const blob_t* b, int n0,
+                                                                                        float* out) {
+  const int nt = 48, blks = b->k / b->bs;
+  /* accumulator lanes: L0 = low nibbles of bytes 0-15 (columns 0, 2, .., 30), H0 = their high nibbles (1, 3, .., 31),
+     L1 / H1 the same for bytes 16-23 (columns 32 .. 47); one interleave per block restores column order */
+  const __m512i ia = _mm512_setr_epi32(0, 16, 1, 17, 2, 18, 3, 19, 4, 20, 5, 21, 6, 22, 7, 23);
+  const __m512i ib_ = _mm512_setr_epi32(8, 24, 9, 25, 10, 26, 11, 27, 12, 28, 13, 29, 14, 30, 15, 31);
+  const __m512i m15 = _mm512_set1_epi32(15);
+  const __m256i m15y = _mm256_set1_epi32(15);
+  const __m512 c8 = _mm512_set1_ps(8.f);
+  __m512 acc0 = _mm512_setzero_ps(), acc1 = _mm512_setzero_ps(), acc2 = _mm512_setzero_ps();
+  for (int ib = 0; ib < blks; ib++) {
+    __m512 tl0 = _mm512_setzero_ps(), th0 = _mm512_setzero_ps();
+    __m256 tl1 = _mm256_setzero_ps(), th1 = _mm256_setzero_ps();
+    float asum = 0.f;
+    const uint8_t* p = bp + (size_t)ib * b->bs * nt / 2;
+    const float* ak = A + (size_t)ib * b->bs;
+    for (int ik = 0; ik < b->bs; ik++, p += nt / 2) {
+      const float av = ak[ik];
+      asum += av;
+      const __m512 a = _mm512_set1_ps(av);
+      const __m512i x0 = _mm512_cvtepu8_epi32(_mm_loadu_si128((const __m128i*)p));
+      const __m256i x1 = _mm256_cvtepu8_epi32(_mm_loadl_epi64((const __m128i*)(p + 16)));
+      tl0 = _mm512_fmadd_ps(a, _mm512_cvtepi32_ps(_mm512_and_si512(x0, m15)), tl0);
+      th0 = _mm512_fmadd_ps(a, _mm512_cvtepi32_ps(_mm512_srli_epi32(x0, 4)), th0);
+      tl1 = _mm256_fmadd_ps(_mm512_castps512_ps256(a), _mm256_cvtepi32_ps(_mm256_and_si256(x1, m15y)), tl1);
+      th1 = _mm256_fmadd_ps(_mm512_castps512_ps256(a), _mm256_cvtepi32_ps(_mm256_srli_epi32(x1, 4)), th1);
+    }
+    const __m512 t0 = _mm512_permutex2var_ps(tl0, ia, th0), t1 = _mm512_permutex2var_ps(tl0, ib_, th0);
+    const __m512 t2 = _mm512_permutex2var_ps(_mm512_castps256_ps512(tl1), ia, _mm512_castps256_ps512(th1));
+    const size_t ci = (size_t)ib * b->cstep + n0;
+    __m512 z0 = c8, z1 = c8, z2 = c8;
+    if (zp) {
+      z0 = _mm512_add_ps(c8, _mm512_cvtepi32_ps(_mm512_cvtepi8_epi32(_mm_loadu_si128((const __m128i*)(zp + ci)))));
+      z1 = _mm512_add_ps(c8, _mm512_cvtepi32_ps(_mm512_cvtepi8_epi32(_mm_loadu_si128((const __m128i*)(zp + ci + 16)))));
+      z2 = _mm512_add_ps(c8, _mm512_cvtepi32_ps(_mm512_cvtepi8_epi32(_mm_loadu_si128((const __m128i*)(zp + ci + 32)))));
+    }
+    const __m512 as = _mm512_set1_ps(asum);
+    acc0 = _mm512_fmadd_ps(_mm512_fnmadd_ps(z0, as, t0), scales16(sp, ci, b->scat), acc0);
+    acc1 = _mm512_fmadd_ps(_mm512_fnmadd_ps(z1, as, t1), scales16(sp, ci + 16, b->scat), acc1);
+    acc2 = _mm512_fmadd_ps(_mm512_fnmadd_ps(z2, as, t2), scales16(sp, ci + 32, b->scat), acc2);
+  }
+  _mm512_storeu_ps(out, acc0);
+  _mm512_storeu_ps(out + 16, acc1);
+  _mm512_storeu_ps(out + 32, acc2);
+}
+
+int orc_blob_gemv_avx512(const float* A, const void* blob, float* C, int k_ld, int threads) {
+  (void)k_ld;
+  if (!__builtin_cpu_supports("avx512f") || !__builtin_cpu_supports("avx512bw")) return -7;
+  blob_t b;
+  int r = blob_parse(&b, blob);
+  if (r) return r;
+  if (orc_core_ntile(b.coreid) != 48 || orc_core_packrow(b.coreid) != 1 || b.has_shf || b.has_dq) return -5;
+  if (dtype_bits(b.dtype) != 4) return -6;
+  if (b.scat != ORC_F32 && b.scat != ORC_BF16 && b.scat != ORC_F16) return -6;
+  const uint8_t* q = (const uint8_t*)((const int8_t*)blob + b.q_off);
+  const uint8_t* sp = (const uint8_t*)((const int8_t*)blob + b.s_off);
+  const int8_t* zp = b.asym ? (const int8_t*)blob + b.z_off : NULL;
+  const int nblk = (b.n + 47) / 48;
+#pragma omp parallel for schedule(static) num_threads(threads)
+  for (int blk = 0; blk < nblk; blk++) {
+    const int n0 = blk * 48;
+    float acc[48];
+    gemv4_nt48_avx512(A, q + (size_t)n0 * b.kpad / 2, sp, zp, &b, n0, acc);
+    for (int in = 0; in < 48 && n0 + in < b.n; in++) C[n0 + in] = acc[in];
+  }
+  return 0;
+}

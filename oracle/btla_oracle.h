@@ -102,6 +102,7 @@ int orc_blob_forward(const float* A, const void* blob, float* C, int m, int n, i
 int orc_blob_gemv_ref(const float* A, const void* blob, float* C, int m, int lda, int ldc);
 /* single-threaded CPU WOQ GEMV in the reference algorithm's float order, used as the timed cpu_baseline */
 int orc_blob_gemv_par(const float* A, const void* blob, float* C, int m, int lda, int ldc, int threads);
+int orc_blob_gemv_avx512(const float* A, const void* blob, float* C, int k_ld, int threads);
 int orc_blob_gemv_timed(const float* A, const void* blob, float* C, int m, int lda, int ldc, int iters);
 
 

@@ -56,6 +56,7 @@ class Oracle:
         L.orc_blob_gemv_ref.argtypes = [_p, _p, _p, C.c_int, C.c_int, C.c_int]
         L.orc_blob_gemv_timed.argtypes = [_p, _p, _p, C.c_int, C.c_int, C.c_int, C.c_int]
         L.orc_blob_gemv_par.argtypes = [_p, _p, _p, C.c_int, C.c_int, C.c_int, C.c_int]
+        L.orc_blob_gemv_avx512.argtypes = [_p, _p, _p, C.c_int, C.c_int]
         L.orc_quantize_rowblock.argtypes = [_p, _p, C.c_int, C.c_int, C.c_int, C.c_int, _p, _p, C.c_int, C.c_int]
         L.orc_padding_interleave.argtypes = [_p, _p] + [C.c_int] * 8
         L.orc_revert_padding_interleave.argtypes = [_p, _p] + [C.c_int] * 8

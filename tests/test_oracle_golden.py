@@ -293,3 +293,28 @@ def test_layernorm_golden_is_the_stated_formula():
         ref = x / ms if rms else (x - mean) / ms
         d = g["dst"].reshape(rows, size).astype(np.float64)
         assert np.abs(d - ref).max() / np.abs(ref).max() <= 2e-5, case
+
+
+@pytest.mark.parametrize("stype,asym,n", [("F16", False, 200), ("BF16", True, 96), ("F32", False, 4096),
+                                          ("F16", True, 1000)])
+def test_avx512_gemv_matches_scalar(oracle, stype, asym, n):
+    """the AVX-512 + OpenMP GEMV that bench.py's cpu_baseline times (int4, NTILE-48 blobs; per-block
+    FMA chains over the raw nibbles, zero point and scale applied once per block) equals the scalar oracle within fp32
+    reassociation: 1e-5 of the largest output, ragged N."""
+    from tests import oracle_lib as ol
+    rng = np.random.default_rng(n)
+    k = 1024
+    Q = rng.integers(-8, 8, size=(k, n), dtype=np.int8)
+    S = rng.uniform(0.001, 0.01, size=(k // 128, n)).astype(np.float32)
+    Z = rng.integers(-3, 4, size=(k // 128, n), dtype=np.int8) if asym else None
+    blob = oracle.pack_q(Q, S, Z, n, k, 128, ol.S4, getattr(ol, stype), asym, oracle.core("avx512f"))
+    A = rng.uniform(-0.5, 0.5, size=(1, k)).astype(np.float32)
+    c1 = np.zeros((1, n), np.float32)
+    c2 = np.full((1, n), np.nan, np.float32)
+    assert oracle.lib.orc_blob_gemv_ref(A.ctypes.data, blob.ctypes.data, c1.ctypes.data, 1, k, n) == 0
+    r = oracle.lib.orc_blob_gemv_avx512(A.ctypes.data, blob.ctypes.data, c2.ctypes.data, k, 4)
+    if r == -7:
+        pytest.skip("host without AVX-512")
+    assert r == 0
+    assert np.isfinite(c2).all()
+    assert np.abs(c2 - c1).max() <= 1e-5 * np.abs(c1).max(), np.abs(c2 - c1).max() / np.abs(c1).max()
