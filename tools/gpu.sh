@@ -5,10 +5,12 @@
 #   tests      pytest -m gpu (PYTEST_K filters)              smoke    __graft_entry__.smoke()
 #   bench      bench.py (STEPS, BENCH_ARGS)                  prof     rocprofv3 --kernel-trace --stats over a short bench
 #   traffic    PMC FETCH_SIZE / WRITE_SIZE passes of the decode token (tools/pmc_decode.py -> tools/pmc_traffic.py)
-#   sq         SQ counter passes (3 runs) over PMC_CMD (default: the lm_head decode GEMV sweep)
+#   sq         SQ counter passes (PMC_SETS: ';'-separated, one run each) over PMC_CMD (default: the lm_head decode GEMV sweep),
+#              summarised per kernel with derived ratios (tools/pmc_derive.py)
 #   trace      decode GEMV phase trace (needs neural_amd/libneural_amd_trace.so: make -C neural_amd trace)
 #   ab         library A/B on the decode shapes (LIBS="old main", ROUNDS; tools/ab_libs.sh)
 #   abbench    bench.py decode tok/s per library (LIBS, ROUNDS), alternating
+#   abgemm     prefill GEMM TF/s per library (LIBS, ROUNDS, GEMM_ARGS), alternating
 #   sweep      tools/gemv_sweep.py over the decode shapes (SWEEP_* env)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
@@ -44,15 +46,15 @@ for task in "$@"; do
       python tools/pmc_traffic.py gpurun_out/pmc_$TAG gpurun_out/pmc_traffic_$TAG.json ;;
     sq)
       d=gpurun_out/sq_$TAG; rm -rf $d; mkdir -p $d; i=0
-      for set in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_BUSY_CYCLES SQ_WAVES" \
-                 "SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_VMEM SQ_INSTS_SALU SQ_INSTS_SMEM" \
-                 "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_MFMA SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_WAIT_INST_LDS SQ_INST_CYCLES_VMEM" \
-                 ${PMC_EXTRA:+"$PMC_EXTRA"}; do
+      SETS=${PMC_SETS:-"SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_BUSY_CYCLES SQ_WAVES GRBM_GUI_ACTIVE;SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_VMEM SQ_INSTS_SALU SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE;SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_MFMA SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE"}
+      IFS=';' read -ra SETA <<< "$SETS"
+      for set in "${SETA[@]}"; do
         i=$((i+1))
         timeout -s KILL 120 rocprofv3 --pmc $set -d $d/p$i -o run --output-format csv -- \
           ${PMC_CMD:-python tools/gemv_sweep.py --shapes lm_head --reps 8 base} > $d/p$i.log 2>&1 || exit 124
       done
-      python tools/pmc_summarize.py $d | tee gpurun_out/sq_$TAG.txt | head -40 ;;
+      python tools/pmc_summarize.py $d gpurun_out/sq_$TAG.json > gpurun_out/sq_$TAG.txt
+      python tools/pmc_derive.py gpurun_out/sq_$TAG.json | tee gpurun_out/sq_derived_$TAG.txt ;;
     trace)
       timeout -k 10 300 python -u tools/gemv_sweep.py --trace ${SHAPES:+--shapes $SHAPES} base 2>&1 | grep -v amdgpu.ids \
         > gpurun_out/trace_$TAG.txt || exit 124
@@ -67,6 +69,14 @@ for task in "$@"; do
           --no-extra --no-synthetic > gpurun_out/abbench_$l.json 2>/dev/null || exit 124
         python -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], d['value'], d.get('decode_eager_tokens_per_s'), d['roofline']['avg_launch_us'], d.get('prefill_tflops'))" gpurun_out/abbench_$l.json $l | tee -a $f
       done; done ;;
+    abgemm)  # prefill GEMM TF/s per library (LIBS, ROUNDS, GEMM_ARGS), alternating
+      f=gpurun_out/abgemm_$TAG.txt; : > $f
+      for r in $(seq ${ROUNDS:-2}); do for l in ${LIBS:-main}; do
+        if [ "$l" = main ]; then p=neural_amd/libneural_amd.so; else p=neural_amd/libneural_amd_x$l.so; fi
+        echo "#### lib $l round $r" >> $f
+        NAD_LIB_PATH=$PWD/$p timeout -k 10 300 python tools/gemm_sweep.py ${GEMM_ARGS:---m 2048,4096 --act fp16 --shapes o,gate,down --kernels 7 --reps 10} 2>&1 | grep -v amdgpu.ids >> $f || exit 124
+      done; done
+      cat $f ;;
     sweep)
       timeout -k 10 300 python -u tools/gemv_sweep.py ${SHAPES:+--shapes $SHAPES} base 2>&1 | grep -v amdgpu.ids \
         > gpurun_out/sweep_$TAG.txt || exit 124
