@@ -38,8 +38,11 @@ def _blob(seed, n, k):  # noqa: D103
 
 
 def _worker(rank, world, port, q, dims=(D, F), ms=(1, 48)):
+    # one hardware queue per rank: W ranks share the one GPU, and with HIP's default of 4 queues per process world 8
+    # oversubscribes the hardware queue slots -- a rank whose queue is not mapped cannot start its all-reduce while the
+    # mapped ranks' all-reduces spin for it (bounded: they give up and report status 1)
     os.environ.update(MASTER_ADDR="127.0.0.1", NAD_TP_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
-                      LOCAL_RANK="0", NAD_PC_NO_RCCL="1")
+                      LOCAL_RANK="0", NAD_PC_NO_RCCL="1", GPU_MAX_HW_QUEUES="1")
     try:
         import torch
         torch.cuda.set_device(0)
