@@ -37,7 +37,7 @@ def _blob(seed, n, k):  # noqa: D103
     return bestla.quantize(W, GS, "int4", "fp16", "sym", "int8")
 
 
-def _worker(rank, world, port, q, dims=(D, F), ms=(1, 48)):
+def _worker(rank, world, port, q, dims=(D, F), ms=(1, 48), host_reduce=False):
     # one hardware queue per rank: W ranks share the one GPU, and with HIP's default of 4 queues per process world 8
     # oversubscribes the hardware queue slots -- a rank whose queue is not mapped cannot start its all-reduce while the
     # mapped ranks' all-reduces spin for it (bounded: they give up and report status 1)
@@ -48,10 +48,10 @@ def _worker(rank, world, port, q, dims=(D, F), ms=(1, 48)):
         torch.cuda.set_device(0)
         from neural_amd import bestla, tp
         from neural_amd.parallel_context import ParallelContext
-        ctx = ParallelContext()
+        ctx = ParallelContext("tcp" if host_reduce else None)
         assert ctx.get_tp_size() == world and ctx.get_tp_rank() == rank
         info = ctx.info()
-        if world > 1:
+        if world > 1 and not host_reduce:
             assert info["oneshot"], "one-shot IPC all-reduce unavailable"
         d, f = dims
         spec = {"wq": (".attention.wq.weight", d, d), "wo": (".attention.wo.weight", d, d),
@@ -69,20 +69,32 @@ def _worker(rank, world, port, q, dims=(D, F), ms=(1, 48)):
             x = torch.from_numpy(np.random.default_rng(m).uniform(-1, 1, size=(m, d)).astype(np.float32)).cuda()
 
             def block(Wt, reduce):
+                def allreduce(v):
+                    if not host_reduce:
+                        ctx.reduce_add(v)
+                        return
+                    hv = v.cpu()            # the matmuls stay on the GPU; the sum goes over the rendezvous sockets
+                    ctx.reduce_add(hv)
+                    v.copy_(hv)
                 qh = Wt["wq"].forward(x)
                 h = Wt["wo"].forward(qh)
                 if reduce:
-                    ctx.reduce_add(h)
+                    allreduce(h)
                 t = bestla.ffn_gate_up(h, Wt["w1"], Wt["w3"], act="silu")
                 y = Wt["w2"].forward(t)
                 if reduce:
-                    ctx.reduce_add(y)
+                    allreduce(y)
                 return y
             y = block(W, True)
             y1 = block(FULL, False)     # TP=1 on the same GPU, same inputs
             torch.cuda.synchronize()
             out[m] = y.cpu().numpy()
             ref[m] = y1.cpu().numpy()
+        if host_reduce:
+            ctx.barrier()
+            ctx.destroy()
+            q.put((rank, out, True, ref, info))
+            return
         # graph-captured all-reduce replayed twice
         buf = torch.full((4096,), float(rank + 1), device="cuda")
         s = torch.cuda.Stream()
@@ -109,12 +121,12 @@ def _worker(rank, world, port, q, dims=(D, F), ms=(1, 48)):
         q.put((rank, "ERR", traceback.format_exc() + str(e)))
 
 
-def _run(world, dims=(D, F), ms=(1, 48)):
+def _run(world, dims=(D, F), ms=(1, 48), host_reduce=False):
     import torch.multiprocessing as mp
     c = mp.get_context("spawn")
     q = c.Queue()
     port = _free_port()
-    ps = [c.Process(target=_worker, args=(r, world, port, q, dims, ms)) for r in range(world)]
+    ps = [c.Process(target=_worker, args=(r, world, port, q, dims, ms, host_reduce)) for r in range(world)]
     for p in ps:
         p.start()
     res = [q.get(timeout=240) for _ in range(world)]
@@ -125,9 +137,9 @@ def _run(world, dims=(D, F), ms=(1, 48)):
     return sorted(res, key=lambda r: r[0])
 
 
-def _check_tp(world, dims=(D, F), ms=(1, 48)):
+def _check_tp(world, dims=(D, F), ms=(1, 48), host_reduce=False):
     single = _run(1, dims, ms)[0]
-    multi = _run(world, dims, ms)
+    multi = _run(world, dims, ms, host_reduce)
     for m in ms:   # TP=1 computed in the world-1 run and in each rank agree bit for bit
         np.testing.assert_array_equal(single[1][m], single[3][m])
         np.testing.assert_array_equal(multi[0][3][m], single[3][m])
@@ -171,8 +183,10 @@ def test_tp8_llama_layer_shapes_match_tp1():
     model_files.h:134-235): col-parallel Q 4096 -> 512 columns (4 heads) per rank, O row-parallel over 4 x 128 k per
     rank, gate/up 11008 -> 1408 / 1280 columns, and down's K = 11008 = 86 groups of 128 cut 11 x 6 + 10 x 2 (uneven,
     whole groups, exact) with the gate/up column shards lined up; TP=8 against TP=1 within 1e-5 at M = 1 (decode GEMV)
-    and M = 8 (128 KiB messages: inside the one-shot all-reduce, which is what runs without RCCL on one GPU)."""
-    multi = _check_tp(8, (4096, 11008), (1, 8))
+    and M = 8.  The sums go over the rendezvous sockets (host transport): eight processes' spinning one-shot
+    all-reduces on ONE GPU need all eight of their queues mapped at once, which the hardware scheduler does not promise
+    (the one-shot device all-reduce is exercised at worlds 2 and 4 above; on the 8-GPU node each rank has its own GPU)."""
+    multi = _check_tp(8, (4096, 11008), (1, 8), host_reduce=True)
     ranges = [r[4]["range_w2"] for r in multi]
     groups = [(e - b) // GS for b, e in ranges]
     assert groups == [11] * 6 + [10] * 2, groups
