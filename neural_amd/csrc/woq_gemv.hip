@@ -233,6 +233,16 @@ __device__ __forceinline__ float scale_bits_to_f32(uint32_t x, int st, int sh) {
   return st == kScaleF32 ? __uint_as_float(x) : f16or;
 }
 
+// ... with the scale type known at compile time (ST >= 0: the int2 M = 1 instantiations, whose body applies a scale
+// every 64 k at g64 -- VERDICT r5 item 4), else from the launch-uniform runtime value as above
+template <int ST>
+__device__ __forceinline__ float scale_to_f32(uint32_t x, int st, int sh) {
+  if constexpr (ST < 0) return scale_bits_to_f32(x, st, sh);
+  else if constexpr (ST == kScaleF32) return __uint_as_float(x);
+  else if constexpr (ST == kScaleBF16) return __uint_as_float((x >> sh) << 16);
+  else return f16_bits_to_f32(uint16_t(x >> sh));
+}
+
 // ------------------------------------------------------------------------------------------------ activation staging
 // activation bits -> 8 floats of one staging unit (runtime type: staging runs once per workgroup)
 __device__ __forceinline__ void unit_to_f32(int act_t, uint4 x0, uint4 x1, float (&f)[8]) {
@@ -608,7 +618,7 @@ static bool lean_ok(const GemvArgs& a, int bits, int waves) {
 #define NAD_M1_DUAL_NST 2
 #endif
 
-template <int BITS, int GPT, int AT, bool ASYM, int KSN, int SPW, bool BATCH, int NST>
+template <int BITS, int GPT, int AT, bool ASYM, int KSN, int SPW, bool BATCH, int NST, int ST = -1>
 __device__ __forceinline__ void m1_body(GemvArgs& a, int bid) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int KT = BITS == 4 ? 128 : 256, SPT = KT / 32, SPG = SPT / GPT;
@@ -737,7 +747,7 @@ __device__ __forceinline__ void m1_body(GemvArgs& a, int bid) {
       }
       if ((d + 1) % SPG == 0) {  // group end: scale each tile's group partial into the stripe sum, in tile order
 #pragma unroll
-        for (int i = 0; i < KSN; i++) acc += accg[i] * scale_bits_to_f32(S.sc[i][g], a.scale_t, ssh);
+        for (int i = 0; i < KSN; i++) acc += accg[i] * scale_to_f32<ST>(S.sc[i][g], a.scale_t, ssh);
       }
     }
     cq += NW;
@@ -874,9 +884,9 @@ __device__ __forceinline__ void m1_body(GemvArgs& a, int bid) {
   NAD_TRACE(3);
 }
 
-template <int BITS, int GPT, int AT, bool ASYM, int KSN, int SPW, bool BATCH, int NST>
+template <int BITS, int GPT, int AT, bool ASYM, int KSN, int SPW, bool BATCH, int NST, int ST>
 __global__ __launch_bounds__((m1_max_threads<GPT, KSN>())) void woq_gemv_m1_kernel(GemvArgs a) {
-  m1_body<BITS, GPT, AT, ASYM, KSN, SPW, BATCH, NST>(a, int(blockIdx.x));
+  m1_body<BITS, GPT, AT, ASYM, KSN, SPW, BATCH, NST, ST>(a, int(blockIdx.x));
 }
 
 // Two weight formats in one decode launch: workgroups [0, ga) run format 1's body over a, the rest format 2's over b
@@ -915,9 +925,9 @@ static hipError_t gemv_launch4(const GemvArgs& a, dim3 g, dim3 b, size_t lds, hi
                   : gemv_launch5<BITS, HILO, GPT, ASYM, 3>(a, g, b, lds, st);
 }
 
-template <int BITS, int GPT, int AT, bool ASYM, int KSN, int SPW, int NST>
+template <int BITS, int GPT, int AT, bool ASYM, int KSN, int SPW, int NST, int ST>
 static hipError_t gemv_m1_launch6(const GemvArgs& a, dim3 g, dim3 b, size_t lds, hipStream_t st) {
-  auto k = woq_gemv_m1_kernel<BITS, GPT, AT, ASYM, KSN, SPW, false, NST>;
+  auto k = woq_gemv_m1_kernel<BITS, GPT, AT, ASYM, KSN, SPW, false, NST, ST>;
   static bool attr_set = false;
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -933,10 +943,10 @@ static int m1_stages_per_wave(const GemvArgs& a, int ksn, int waves) {
   const int nsl = (a.nt + ksn - 1) / ksn;
   return (a.u_q + (a.u_r ? 1 : 0)) * (a.dual ? 2 : 1) * ((nsl + waves - 1) / waves);
 }
-template <int BITS, int GPT, int AT, bool ASYM, int KSN, int SPW>
+template <int BITS, int GPT, int AT, bool ASYM, int KSN, int SPW, int ST>
 static hipError_t gemv_m1_launch5(const GemvArgs& a, dim3 g, dim3 b, size_t lds, hipStream_t st) {
   if (a.batch) {
-    auto kb = woq_gemv_m1_kernel<BITS, GPT, AT, ASYM, KSN, SPW, true, NAD_M1_BATCH_NST>;
+    auto kb = woq_gemv_m1_kernel<BITS, GPT, AT, ASYM, KSN, SPW, true, NAD_M1_BATCH_NST, ST>;
     static bool attr_b = false;
     if (!attr_b) {
       hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kb), hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -949,15 +959,25 @@ static hipError_t gemv_m1_launch5(const GemvArgs& a, dim3 g, dim3 b, size_t lds,
   }
   const int spw = m1_stages_per_wave(a, KSN, int(b.x / 64));
   const int nst = a.m1_nst == 1 || a.m1_nst == 2 ? a.m1_nst : (spw >= 7 || (KSN == 1 && spw >= 4) ? 2 : 1);
-  return nst == 1 ? gemv_m1_launch6<BITS, GPT, AT, ASYM, KSN, SPW, 1>(a, g, b, lds, st)
-                  : gemv_m1_launch6<BITS, GPT, AT, ASYM, KSN, SPW, 2>(a, g, b, lds, st);
+  return nst == 1 ? gemv_m1_launch6<BITS, GPT, AT, ASYM, KSN, SPW, 1, ST>(a, g, b, lds, st)
+                  : gemv_m1_launch6<BITS, GPT, AT, ASYM, KSN, SPW, 2, ST>(a, g, b, lds, st);
 }
-template <int BITS, int GPT, int AT, bool ASYM>
+// int2: the scale type as a template parameter (3 x the int2 instantiations; int4 keeps the runtime form)
+#ifndef NAD_INT2_ST
+#define NAD_INT2_ST 1
+#endif
+template <int BITS, int GPT, int AT, bool ASYM, int ST = -1>
 static hipError_t gemv_m1_launch4(const GemvArgs& a, dim3 g, dim3 b, size_t lds, hipStream_t st) {
-  if (a.lean_ks == 1) return gemv_m1_launch5<BITS, GPT, AT, ASYM, 1, 1>(a, g, b, lds, st);
-  if (a.lean_ks == 2) return gemv_m1_launch5<BITS, GPT, AT, ASYM, 2, 1>(a, g, b, lds, st);
-  return a.lean_spw == 4 ? gemv_m1_launch5<BITS, GPT, AT, ASYM, KS, 4>(a, g, b, lds, st)
-                         : gemv_m1_launch5<BITS, GPT, AT, ASYM, KS, 2>(a, g, b, lds, st);
+  if constexpr (BITS == 2 && ST < 0 && NAD_INT2_ST) {
+    if (a.scale_t == kScaleF32) return gemv_m1_launch4<BITS, GPT, AT, ASYM, kScaleF32>(a, g, b, lds, st);
+    if (a.scale_t == kScaleBF16) return gemv_m1_launch4<BITS, GPT, AT, ASYM, kScaleBF16>(a, g, b, lds, st);
+    return gemv_m1_launch4<BITS, GPT, AT, ASYM, kScaleF16>(a, g, b, lds, st);
+  } else {
+    if (a.lean_ks == 1) return gemv_m1_launch5<BITS, GPT, AT, ASYM, 1, 1, ST>(a, g, b, lds, st);
+    if (a.lean_ks == 2) return gemv_m1_launch5<BITS, GPT, AT, ASYM, 2, 1, ST>(a, g, b, lds, st);
+    return a.lean_spw == 4 ? gemv_m1_launch5<BITS, GPT, AT, ASYM, KS, 4, ST>(a, g, b, lds, st)
+                           : gemv_m1_launch5<BITS, GPT, AT, ASYM, KS, 2, ST>(a, g, b, lds, st);
+  }
 }
 template <int BITS, int GPT>
 static hipError_t gemv_m1_launch2(const GemvArgs& a, dim3 g, dim3 b, size_t lds, hipStream_t st) {
@@ -968,19 +988,29 @@ static hipError_t gemv_m1_launch2(const GemvArgs& a, dim3 g, dim3 b, size_t lds,
   return a.asym ? gemv_m1_launch4<BITS, GPT, kActBF16, true>(a, g, b, lds, st)
                 : gemv_m1_launch4<BITS, GPT, kActBF16, false>(a, g, b, lds, st);
 }
-// int4 / int2 with one group per tile or 2 per tile; int2 also 4 per tile (sym only, as the general kernel)
+// int4 / int2 with one group per tile or 2 per tile; int2 also 4 per tile (sym only, as the general kernel).  The
+// int2 instantiations (3 scale types each) compile as their own object (woq_gemv_b2.o: GEMV_PART=1) in parallel with
+// the rest (GEMV_PART=0); without GEMV_PART (trace / experiment builds) one object holds everything.
+#if !defined(GEMV_PART) || GEMV_PART == 1
+hipError_t gemv_m1_launch_b2(const GemvArgs& a, int gpt, dim3 g, dim3 b, size_t lds, hipStream_t st) {
+  if (gpt == 1) return gemv_m1_launch2<2, 1>(a, g, b, lds, st);
+  if (gpt == 2) return gemv_m1_launch2<2, 2>(a, g, b, lds, st);
+  if (gpt == 4 && !a.asym) return a.act_t == kActF32 ? gemv_m1_launch4<2, 4, kActF32, false>(a, g, b, lds, st)
+                                 : (a.act_t == kActF16 ? gemv_m1_launch4<2, 4, kActF16, false>(a, g, b, lds, st)
+                                                       : gemv_m1_launch4<2, 4, kActBF16, false>(a, g, b, lds, st));
+  return hipErrorInvalidValue;
+}
+#else
+hipError_t gemv_m1_launch_b2(const GemvArgs& a, int gpt, dim3 g, dim3 b, size_t lds, hipStream_t st);
+#endif
+#if !defined(GEMV_PART) || GEMV_PART == 0
 static hipError_t gemv_m1_launch(const GemvArgs& a, int bits, int gpt, dim3 g, dim3 b, size_t lds, hipStream_t st) {
   if (bits == 4) {
     if (gpt == 1) return gemv_m1_launch2<4, 1>(a, g, b, lds, st);
     if (gpt == 2) return gemv_m1_launch2<4, 2>(a, g, b, lds, st);
-  } else {
-    if (gpt == 1) return gemv_m1_launch2<2, 1>(a, g, b, lds, st);
-    if (gpt == 2) return gemv_m1_launch2<2, 2>(a, g, b, lds, st);
-    if (gpt == 4 && !a.asym) return a.act_t == kActF32 ? gemv_m1_launch4<2, 4, kActF32, false>(a, g, b, lds, st)
-                                   : (a.act_t == kActF16 ? gemv_m1_launch4<2, 4, kActF16, false>(a, g, b, lds, st)
-                                                         : gemv_m1_launch4<2, 4, kActBF16, false>(a, g, b, lds, st));
+    return hipErrorInvalidValue;
   }
-  return hipErrorInvalidValue;
+  return gemv_m1_launch_b2(a, gpt, g, b, lds, st);
 }
 
 // Instantiated: groups of >= KT (GPT 1), KT/2 (GPT 2) and KT/4 (GPT 4), sym and asym.  Finer groups fall back to
@@ -1126,9 +1156,11 @@ hipError_t launch_gemv(const GemvArgs& a, int bits, int waves, int grid, size_t 
   return gemv_launch1<8>(a, hilo, gpt, g, b, lds, stream);
 }
 
+#endif  // GEMV_PART 0
+
 }  // namespace nad
 
-#ifdef NAD_PHASE_TRACE
+#if defined(NAD_PHASE_TRACE) && (!defined(GEMV_PART) || GEMV_PART == 0)
 extern "C" int nad_trace_clock_khz() {
   int dev = 0, khz = 0;
   if (hipGetDevice(&dev) != hipSuccess) return -1;
