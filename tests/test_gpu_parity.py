@@ -396,3 +396,28 @@ def test_qkv_mixed_formats(oracle, m, kinds):
     for y, w, b, (n, *_) in zip(bestla.qkv_forward(x, *ws), ws, blobs, spec):
         assert _rel_err(y.cpu().numpy(), oracle.forward(A, b, n, k)) <= (TOL_DECODE if m <= 16 else TOL_PREFILL)
         assert torch.equal(y, w.forward(x))    # fusion does not change a single bit
+
+
+@pytest.mark.parametrize("st", [F32, BF16, F16])
+@pytest.mark.parametrize("cfg", [(1024, 4096, 64, False, "f32"), (528, 2048, 128, True, "f16"),
+                                 (300, 1024, 256, False, "bf16"), (4096, 4096, 64, False, "f16")])
+def test_gemv_m1_int2_every_scale_type(oracle, st, cfg):
+    """Round 6: the int2 M = 1 instantiations take the scale type as a template parameter (woq_gemv.hip
+    gemv_m1_launch4, compiled as woq_gemv_b2.o).  Every scale type x group layout (4 / 2 / 1 groups per 256-deep tile)
+    against the oracle, and the batched form of the same kernel bit-identical to single launches."""
+    n, k, bs, asym, adt = cfg
+    blob = _blob(oracle, n, k, bs, S2, st, asym, 4, seed=n + bs + st)
+    w = bestla.DeviceWeight(blob)
+    assert w.plan(1, {"f32": "fp32", "f16": "fp16", "bf16": "bf16"}[adt])["kernel"] == "woq_gemv_m1_kernel"
+    A = np.random.default_rng(n + k).uniform(-0.5, 0.5, size=(1, k)).astype(np.float32)
+    xa = torch.from_numpy(A).cuda().to(dict(f32=torch.float32, f16=torch.float16, bf16=torch.bfloat16)[adt])
+    ref = oracle.forward(xa.float().cpu().numpy(), blob, n, k)
+    y = w.forward(xa).cpu().numpy()
+    assert _rel_err(y, ref) <= TOL_DECODE
+    if adt == "f32":
+        xs = [torch.from_numpy(np.random.default_rng(i).uniform(-1, 1, size=(k,)).astype(np.float32)).cuda()
+              for i in range(3)]
+        ys = [torch.empty(n, device="cuda") for _ in xs]
+        bestla.Batch([(w, x, yy) for x, yy in zip(xs, ys)]).run()
+        for x, yy in zip(xs, ys):
+            assert torch.equal(yy, w.forward(x.view(1, k)).view(n))
