@@ -56,7 +56,7 @@ struct Knobs {
   int compute_int8;
   int gemm2_disable, gemm4_all, gemm4_disable, ffn_f32, gemm_kernel, gemm7_bm, splitk_disable;
   int gemm3_stagger, gemm4_fold_all, gemm4_fold, gemm4_ksw;
-  int mid_min_m, mid_max_m, mid_ks;
+  int mid_min_m, mid_max_m, mid_ks, mid_xcd;
   int host_cache_mb;
 };
 static Knobs read_knobs() {
@@ -82,6 +82,7 @@ static Knobs read_knobs() {
   k.gemm4_ksw = env_int("NAD_GEMM4_KSW", 2);  // folded gemm4 launches with the waves split over K: 0 off, 1 on, 2 auto
   k.mid_max_m = env_int("NAD_MID_MAX_M", 64);  // mid-M kernel (woq_gemm_mid.hip) up to this M (0: off)
   k.mid_ks = env_int("NAD_MID_KS", 0);         // tests / tuning: its K runs (0 auto)
+  k.mid_xcd = env_int("NAD_MID_XCD", 1);       // the runs of a stripe group and their reduce on one XCD (0: off)
   k.mid_min_m = env_int("NAD_MID_MIN_M", 0);  // ... from this M (0 auto: 12 rows of fp16 activations, 8 of fp32 / bf16)
   k.host_cache_mb = env_int("NAD_HOST_CACHE_MB", 64 * 1024);
   return k;
@@ -1086,6 +1087,9 @@ static int run_mid(const void* act, int act_t, int lda, int m, int k, const Devi
   } else {
     a.ktiles = w.nt;
   }
+  // a stripe group's runs and the reduce of their slabs on one XCD: the reduce reads the slabs from that XCD's L2
+  // instead of memory (K = N = 4096: M = 64 14.3 -> 12.7 us, M = 32 10.3 -> 9.5; profiles/r06_mid_xcd_ab.txt)
+  if (ks > 1 && kn.mid_xcd && sps == 4) a.xcd_sg = nsg;
   const int grid = nsg * ks;
   if (planned(NAD_KERNEL_MID, grid, nw * 64, ks, 0)) {
     if (ks > 1) planned(0, 0, 0, 1, 0, false);  // the split-K reduce

@@ -658,9 +658,28 @@ __global__ __launch_bounds__(512, 1) void woq_gemm3_kernel(GemmArgs a, const _Fl
 __global__ __launch_bounds__(256) void nad_splitk_reduce_kernel(GemmArgs a) {
   const SkinnyWeight& W = a.w;
   const int nq = (W.n + 3) >> 2;
-  const size_t q = size_t(blockIdx.x) * 256 + threadIdx.x;
-  if (q >= size_t(a.M) * nq) return;
-  const int row = int(q / nq), n0 = int(q - size_t(row) * nq) * 4;
+  int row, n0;
+  if (a.xcd_sg) {
+    // the mid-M kernel's stripe groups (64 columns): group sg's slabs were written on XCD sg % 8, read them there
+    // (the last incomplete round of 8 groups in order, as the mid-M kernel places them)
+    const int per = (a.M * 16 + 255) >> 8, x8 = (a.xcd_sg >> 3) << 3, full = x8 * per, b = int(blockIdx.x);
+    int sg, u;
+    if (b < full) {
+      sg = ((b >> 3) / per) * 8 + (b & 7);
+      u = ((b >> 3) % per) * 256 + int(threadIdx.x);
+    } else {
+      sg = x8 + (b - full) / per;
+      u = ((b - full) % per) * 256 + int(threadIdx.x);
+    }
+    row = u >> 4;
+    n0 = sg * 64 + (u & 15) * 4;
+    if (row >= a.M || n0 >= W.n) return;
+  } else {
+    const size_t q = size_t(blockIdx.x) * 256 + threadIdx.x;
+    if (q >= size_t(a.M) * nq) return;
+    row = int(q / nq);
+    n0 = int(q - size_t(row) * nq) * 4;
+  }
   const size_t rs = size_t(a.M) * a.ldp;
   const float* p = a.part + size_t(row) * a.ldp + n0;
   // the loads of up to 8 runs in flight at once (a loop over the runs serialised their latencies: 4.7 us for 1 MB)
@@ -689,7 +708,7 @@ __global__ __launch_bounds__(256) void nad_splitk_reduce_kernel(GemmArgs a) {
 }
 
 hipError_t launch_splitk_reduce(const GemmArgs& a, hipStream_t st) {
-  const size_t work = size_t(a.M) * ((a.w.n + 3) / 4);
+  const size_t work = a.xcd_sg ? size_t(a.xcd_sg) * ((a.M * 16 + 255) / 256) * 256 : size_t(a.M) * ((a.w.n + 3) / 4);
   hipLaunchKernelGGL(nad_splitk_reduce_kernel, dim3(unsigned((work + 255) / 256)), dim3(256), 0, st, a);
   return hipGetLastError();
 }

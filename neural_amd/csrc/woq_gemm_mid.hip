@@ -136,7 +136,17 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW / 4,
   const int M = a.M, nt = W.nt, ng = W.ng, ns = W.ns;
   const int ks = a.ksplit > 1 ? a.ksplit : 1;
   const int bid = blockIdx.x;
-  const int r = bid % ks, sg = bid / ks;
+  // round-robin placement puts workgroup b on XCD b % 8: with xcd_sg the runs of stripe group sg all go to XCD sg % 8
+  // (the groups of the last incomplete round of 8 as before), so the reduce finds their slabs in that XCD's L2
+  const int x8 = (a.xcd_sg >> 3) << 3, full = x8 * ks;
+  int r, sg;
+  if (bid < full) {
+    r = (bid >> 3) % ks;
+    sg = ((bid >> 3) / ks) * 8 + (bid & 7);
+  } else {
+    r = (bid - full) % ks;
+    sg = x8 + (bid - full) / ks;
+  }
   const int t0 = r * a.ktiles;
   const int t1 = min(nt, t0 + a.ktiles);
   const int tsh = a.tpg_shift;

@@ -87,6 +87,8 @@ struct GemmArgs {
   int ldo16;
   const _Float16* aux16;
   int tpg_shift;        // mid-M kernel, one group per K tile or more: log2(K tiles per group) (31: one group)
+  int xcd_sg;           // mid-M kernel + its reduce: > 0 = the stripe-group count; the runs of stripe group sg on XCD
+                        // sg % 8 (whole rounds of 8 groups), and the reduce workgroups that sum them there too
   SkinnyWeight w;
 };
 
