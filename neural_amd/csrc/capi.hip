@@ -56,7 +56,7 @@ struct Knobs {
   int compute_int8;
   int gemm2_disable, gemm4_all, gemm4_disable, ffn_f32, gemm_kernel, gemm7_bm, splitk_disable;
   int gemm3_stagger, gemm4_fold_all, gemm4_fold, gemm4_ksw;
-  int mid_min_m, mid_max_m, mid_ks, mid_xcd;
+  int mid_min_m, mid_max_m, mid_ks, mid_xcd, gemm_xcd;
   int host_cache_mb;
 };
 static Knobs read_knobs() {
@@ -83,6 +83,7 @@ static Knobs read_knobs() {
   k.mid_max_m = env_int("NAD_MID_MAX_M", 64);  // mid-M kernel (woq_gemm_mid.hip) up to this M (0: off)
   k.mid_ks = env_int("NAD_MID_KS", 0);         // tests / tuning: its K runs (0 auto)
   k.mid_xcd = env_int("NAD_MID_XCD", 1);       // the runs of a stripe group and their reduce on one XCD (0: off)
+  k.gemm_xcd = env_int("NAD_GEMM_XCD", 1);     // gemm7 split-K: the runs of a tile and their reduce on one XCD (0: off)
   k.mid_min_m = env_int("NAD_MID_MIN_M", 0);  // ... from this M (0 auto: 12 rows of fp16 activations, 8 of fp32 / bf16)
   k.host_cache_mb = env_int("NAD_HOST_CACHE_MB", 64 * 1024);
   return k;
@@ -1218,6 +1219,9 @@ static int run_gemm(const void* act, int act_t, int lda, int m, int k, const Dev
       a.part = reinterpret_cast<float*>(base + a16);
     }
     const int tiles = ((m + bm - 1) / bm) * ((w.n + 127) / 128);
+    // split K: every run of a tile and the reduce of its slabs on one XCD (slabs read back from that XCD's L2): K = N =
+    // 4096 M = 128 18.6 -> 15.9 us, M = 96 17.2 -> 14.8 (profiles/r06_gemm7_xcd_splitk_ab.txt)
+    if (g7 && ks > 1 && kn.gemm_xcd && (((m + bm - 1) / bm) * ((w.ns + 7) / 8)) % 8 == 0) a.xcd_tile = bm;
     if (planned(pg == 4 ? NAD_KERNEL_GEMM4 : (g2 ? NAD_KERNEL_GEMM2 : (g7 ? NAD_KERNEL_GEMM7 : NAD_KERNEL_GEMM3)),
                 tiles * ks, 512, ks, a.fold | (a.ksw << 1))) {
       if (ks > 1) planned(0, 0, 0, 1, 0, false);  // the split-K reduce

@@ -674,6 +674,13 @@ __global__ __launch_bounds__(256) void nad_splitk_reduce_kernel(GemmArgs a) {
     row = u >> 4;
     n0 = sg * 64 + (u & 15) * 4;
     if (row >= a.M || n0 >= W.n) return;
+  } else if (a.xcd_tile) {
+    // gemm7's tiles (xcd_tile rows x 128 columns): XCD x summed tiles [x T/8, (x+1) T/8), 8 rows per workgroup
+    const int bmt = a.xcd_tile, per = bmt >> 3, nbn = (W.ns + 7) >> 3, ntile = ((a.M + bmt - 1) / bmt) * nbn;
+    const int b = int(blockIdx.x), o = b >> 3, tile = (b & 7) * (ntile >> 3) + o / per;
+    row = (tile / nbn) * bmt + (o % per) * 8 + int(threadIdx.x >> 5);
+    n0 = (tile % nbn) * 128 + int(threadIdx.x & 31) * 4;
+    if (row >= a.M || n0 >= W.n) return;
   } else {
     const size_t q = size_t(blockIdx.x) * 256 + threadIdx.x;
     if (q >= size_t(a.M) * nq) return;
@@ -708,7 +715,9 @@ __global__ __launch_bounds__(256) void nad_splitk_reduce_kernel(GemmArgs a) {
 }
 
 hipError_t launch_splitk_reduce(const GemmArgs& a, hipStream_t st) {
-  const size_t work = a.xcd_sg ? size_t(a.xcd_sg) * ((a.M * 16 + 255) / 256) * 256 : size_t(a.M) * ((a.w.n + 3) / 4);
+  const size_t work = a.xcd_sg     ? size_t(a.xcd_sg) * ((a.M * 16 + 255) / 256) * 256
+                      : a.xcd_tile ? size_t((a.M + a.xcd_tile - 1) / a.xcd_tile) * ((a.w.ns + 7) / 8) * a.xcd_tile * 32
+                                   : size_t(a.M) * ((a.w.n + 3) / 4);
   hipLaunchKernelGGL(nad_splitk_reduce_kernel, dim3(unsigned((work + 255) / 256)), dim3(256), 0, st, a);
   return hipGetLastError();
 }

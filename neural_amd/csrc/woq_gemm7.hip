@@ -221,13 +221,17 @@ __global__ __launch_bounds__(512, 1) void woq_gemm7_kernel(GemmArgs a, const _Fl
   const int ntile = nbm * nbn;
   const int nsplit = a.ksplit > 1 ? a.ksplit : 1;
   const int nwg = ntile * nsplit;
-  int bid = blockIdx.x;
-  {
+  int bid = blockIdx.x, ks;
+  if (a.xcd_tile) {  // every run of a tile on one XCD: the reduce reads the slabs from that XCD's L2
+    const int o = bid >> 3;
+    ks = o % nsplit;
+    bid = (bid & 7) * (ntile >> 3) + o / nsplit;
+  } else {
     const int q = nwg / 8, r = nwg % 8, x = bid % 8, o = bid / 8;
     bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + o;
+    ks = bid / ntile;
+    bid -= ks * ntile;
   }
-  const int ks = bid / ntile;
-  bid -= ks * ntile;
   const int kt0 = nsplit > 1 ? ks * a.ktiles : 0;
   const int ntl = nsplit > 1 ? min(a.ktiles, nt - kt0) : nt;
   const int nh = HPT * ntl;            // half steps of the K run

@@ -89,6 +89,8 @@ struct GemmArgs {
   int tpg_shift;        // mid-M kernel, one group per K tile or more: log2(K tiles per group) (31: one group)
   int xcd_sg;           // mid-M kernel + its reduce: > 0 = the stripe-group count; the runs of stripe group sg on XCD
                         // sg % 8 (whole rounds of 8 groups), and the reduce workgroups that sum them there too
+  int xcd_tile;         // gemm7 split-K: > 0 = its tile height; XCD x runs every K run of tiles [x T/8, (x+1) T/8) (T tiles,
+                        // a multiple of 8), and the reduce workgroups of those tiles run there too
   SkinnyWeight w;
 };
 
