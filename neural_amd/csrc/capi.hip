@@ -56,7 +56,7 @@ struct Knobs {
   int compute_int8;
   int gemm2_disable, gemm4_all, gemm4_disable, ffn_f32, gemm_kernel, gemm7_bm, splitk_disable;
   int gemm3_stagger, gemm4_fold_all, gemm4_fold, gemm4_ksw;
-  int mid_min_m, mid_max_m, mid_ks, mid_xcd, gemm_xcd;
+  int mid_min_m, mid_max_m, mid_ks, mid_xcd, mid_wide, gemm_xcd;
   int host_cache_mb;
 };
 static Knobs read_knobs() {
@@ -83,6 +83,7 @@ static Knobs read_knobs() {
   k.mid_max_m = env_int("NAD_MID_MAX_M", 64);  // mid-M kernel (woq_gemm_mid.hip) up to this M (0: off)
   k.mid_ks = env_int("NAD_MID_KS", 0);         // tests / tuning: its K runs (0 auto)
   k.mid_xcd = env_int("NAD_MID_XCD", 1);       // the runs of a stripe group and their reduce on one XCD (0: off)
+  k.mid_wide = env_int("NAD_MID_WIDE", 2);     // mid-M 8-stripe workgroups (M <= 32): 0 never, 1 always, 2 auto
   k.gemm_xcd = env_int("NAD_GEMM_XCD", 1);     // gemm7 split-K: the runs of a tile and their reduce on one XCD (0: off)
   k.mid_min_m = env_int("NAD_MID_MIN_M", 0);  // ... from this M (0 auto: 12 rows of fp16 activations, 8 of fp32 / bf16)
   k.host_cache_mb = env_int("NAD_HOST_CACHE_MB", 64 * 1024);
@@ -1047,15 +1048,30 @@ static int run_mid(const void* act, int act_t, int lda, int m, int k, const Devi
   const int esz = act_t == kActF32 ? 4 : 2;
   if (uint64_t(m) * lda * esz >= (1ull << 31) || uint64_t(w.ns) * w.nt * 1024 >= (1ull << 31)) return 0;
   const int rf = (m + 15) / 16;
-  int sps = 0, nw = 0, spw = 0;
-  mid_geometry(w.bits, gpt, act_t, rf, &sps, &nw, &spw);
-  const int chunk = nw * spw;
-  const int nsg = (w.ns + sps - 1) / sps;
-  int ks = (w.nt + chunk - 1) / chunk;
-  // slabs within nad_device_workspace_size's N-independent bound (m x 128 KiB past the fp16 copy): ks x N <= 32768,
-  // so wide weights split K less (N = 11008: 2 runs, 172 x 2 workgroups; N = 32000: none, 500 workgroups)
-  ks = std::max(1, std::min(ks, 32768 / ((w.n + 3) / 4 * 4)));
-  if (kn.mid_ks > 0) ks = std::max(1, std::min({kn.mid_ks, w.nt, 32768 / ((w.n + 3) / 4 * 4)}));
+  int sps = 0, nw = 0, spw = 0, nsg = 0, ks = 0;
+  // runs per stripe group: one chunk each, the slabs within nad_device_workspace_size's N-independent bound (m x 128 KiB
+  // past the fp16 copy): ks x N <= 32768, so wide weights split K less (N = 11008: 2 runs; N = 32000: none)
+  auto plan = [&](int wide) {
+    mid_geometry(w.bits, gpt, act_t, rf, wide, &sps, &nw, &spw);
+    const int chunk = nw * spw;
+    nsg = (w.ns + sps - 1) / sps;
+    ks = std::max(1, std::min((w.nt + chunk - 1) / chunk, 32768 / ((w.n + 3) / 4 * 4)));
+    if (kn.mid_ks > 0) ks = std::max(1, std::min({kn.mid_ks, w.nt, 32768 / ((w.n + 3) / 4 * 4)}));
+  };
+  plan(kn.mid_wide == 1);
+  // 8-stripe workgroups (where mid_geometry has them) when the 4-stripe grid takes more than one workgroup per CU and
+  // theirs does not: N = 11008, M = 16 / 32: 344 -> 172 workgroups, 16.3 -> 14.3-14.9 us, 21.1 -> 18.8
+  // (profiles/r06_mid_wide_ab.txt); at N = 4096 (256 either way) the 8-stripe form's doubled slabs cost 0.7-1 us
+  if (kn.mid_wide == 2 && sps == 4 && nsg * ks > device_cus()) {
+    const int s4 = sps, n4 = nsg, k4 = ks, w4 = spw;
+    plan(1);
+    if (sps == 4 || nsg * ks > device_cus()) {
+      sps = s4;
+      nsg = n4;
+      ks = k4;
+      spw = w4;
+    }
+  }
   const int ktiles = (w.nt + ks - 1) / ks;
   ks = (w.nt + ktiles - 1) / ktiles;
   GemmArgs a{};
@@ -1090,13 +1106,16 @@ static int run_mid(const void* act, int act_t, int lda, int m, int k, const Devi
   }
   // a stripe group's runs and the reduce of their slabs on one XCD: the reduce reads the slabs from that XCD's L2
   // instead of memory (K = N = 4096: M = 64 14.3 -> 12.7 us, M = 32 10.3 -> 9.5; profiles/r06_mid_xcd_ab.txt)
-  if (ks > 1 && kn.mid_xcd && sps == 4) a.xcd_sg = nsg;
+  if (ks > 1 && kn.mid_xcd) {
+    a.xcd_sg = nsg;
+    a.xcd_w = sps * 4;
+  }
   const int grid = nsg * ks;
   if (planned(NAD_KERNEL_MID, grid, nw * 64, ks, 0)) {
     if (ks > 1) planned(0, 0, 0, 1, 0, false);  // the split-K reduce
     return 1;
   }
-  hipError_t e = launch_gemm_mid(a, w.bits, gpt, act_t, rf, grid, st);
+  hipError_t e = launch_gemm_mid(a, w.bits, gpt, act_t, rf, sps, grid, st);
   if (e == hipSuccess && ks > 1) e = launch_splitk_reduce(a, st);
   if (e != hipSuccess) {
     set_err("mid-M GEMM launch failed: %s", hipGetErrorString(e));

@@ -660,9 +660,9 @@ __global__ __launch_bounds__(256) void nad_splitk_reduce_kernel(GemmArgs a) {
   const int nq = (W.n + 3) >> 2;
   int row, n0;
   if (a.xcd_sg) {
-    // the mid-M kernel's stripe groups (64 columns): group sg's slabs were written on XCD sg % 8, read them there
+    // the mid-M kernel's stripe groups (4 xcd_w columns): group sg's slabs were written on XCD sg % 8, read them there
     // (the last incomplete round of 8 groups in order, as the mid-M kernel places them)
-    const int per = (a.M * 16 + 255) >> 8, x8 = (a.xcd_sg >> 3) << 3, full = x8 * per, b = int(blockIdx.x);
+    const int xw = a.xcd_w, per = (a.M * xw + 255) >> 8, x8 = (a.xcd_sg >> 3) << 3, full = x8 * per, b = int(blockIdx.x);
     int sg, u;
     if (b < full) {
       sg = ((b >> 3) / per) * 8 + (b & 7);
@@ -671,8 +671,8 @@ __global__ __launch_bounds__(256) void nad_splitk_reduce_kernel(GemmArgs a) {
       sg = x8 + (b - full) / per;
       u = ((b - full) % per) * 256 + int(threadIdx.x);
     }
-    row = u >> 4;
-    n0 = sg * 64 + (u & 15) * 4;
+    row = u / xw;
+    n0 = (sg * xw + (u - row * xw)) * 4;
     if (row >= a.M || n0 >= W.n) return;
   } else if (a.xcd_tile) {
     // gemm7's tiles (xcd_tile rows x 128 columns): XCD x summed tiles [x T/8, (x+1) T/8), 8 rows per workgroup
@@ -715,7 +715,7 @@ __global__ __launch_bounds__(256) void nad_splitk_reduce_kernel(GemmArgs a) {
 }
 
 hipError_t launch_splitk_reduce(const GemmArgs& a, hipStream_t st) {
-  const size_t work = a.xcd_sg     ? size_t(a.xcd_sg) * ((a.M * 16 + 255) / 256) * 256
+  const size_t work = a.xcd_sg     ? size_t(a.xcd_sg) * ((a.M * a.xcd_w + 255) / 256) * 256
                       : a.xcd_tile ? size_t((a.M + a.xcd_tile - 1) / a.xcd_tile) * ((a.w.ns + 7) / 8) * a.xcd_tile * 32
                                    : size_t(a.M) * ((a.w.n + 3) / 4);
   hipLaunchKernelGGL(nad_splitk_reduce_kernel, dim3(unsigned((work + 255) / 256)), dim3(256), 0, st, a);

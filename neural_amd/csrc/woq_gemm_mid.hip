@@ -353,17 +353,28 @@ static hipError_t mid_go(const GemmArgs& a, int grid, hipStream_t st) {
 // fragments and 64 accumulators need more than two waves' register budget); int4 2 stages (K tiles) per wave, 1 for
 // groups finer than a tile at M > 32 (their scale / zero-point registers); int2 (256-deep tiles, 8 steps of activation
 // fragments per stage) 1.  Not taken: int2 at M > 32, int4 with 4 groups per tile (g32) at M > 32.
-void mid_geometry(int bits, int gpt, int act_t, int rf, int* s, int* nw, int* spw) {
+void mid_geometry(int bits, int gpt, int act_t, int rf, int wide, int* s, int* nw, int* spw) {
   (void)act_t;
-  *s = 4;
   *nw = 4;
+  if (wide && bits == 4 && rf <= 2 && gpt <= 2) {  // 8 stripes x a 512-deep run: half the activation bytes per column
+    *s = 8;
+    *spw = 1;
+    return;
+  }
+  *s = 4;
   *spw = bits == 4 && (rf <= 2 || gpt == 1) ? 2 : 1;
 }
 
 template <int BITS, int GPT, bool ASYM, int AT>
-static hipError_t mid_rf(const GemmArgs& a, int rf, int grid, hipStream_t st) {
+static hipError_t mid_rf(const GemmArgs& a, int rf, int s, int grid, hipStream_t st) {
   if constexpr (BITS == 4) {
     constexpr int SPW3 = GPT == 1 ? 2 : 1;  // M > 32
+    if constexpr (GPT <= 2) {
+      if (s == 8 && rf <= 2)
+        return rf == 1 ? mid_go<BITS, GPT, ASYM, AT, 1, 8, 4, 1>(a, grid, st)
+                       : mid_go<BITS, GPT, ASYM, AT, 2, 8, 4, 1>(a, grid, st);
+    }
+    if (s != 4) return hipErrorInvalidValue;
     switch (rf) {
       case 1:
         return mid_go<BITS, GPT, ASYM, AT, 1, 4, 4, 2>(a, grid, st);
@@ -379,28 +390,31 @@ static hipError_t mid_rf(const GemmArgs& a, int rf, int grid, hipStream_t st) {
     }
   } else {
     // int2 (8 steps of activation fragments per 256-deep stage): M <= 32 only (run_mid)
+    if (s != 4) return hipErrorInvalidValue;
     return rf == 1 ? mid_go<BITS, GPT, ASYM, AT, 1, 4, 4, 1>(a, grid, st)
                    : mid_go<BITS, GPT, ASYM, AT, 2, 4, 4, 1>(a, grid, st);
   }
 }
 
 template <int BITS, int GPT, bool ASYM>
-static hipError_t mid_at(const GemmArgs& a, int act_t, int rf, int grid, hipStream_t st) {
-  if (act_t == kActF16) return mid_rf<BITS, GPT, ASYM, kActF16>(a, rf, grid, st);
-  if (act_t == kActBF16) return mid_rf<BITS, GPT, ASYM, kActBF16>(a, rf, grid, st);
-  return mid_rf<BITS, GPT, ASYM, kActF32>(a, rf, grid, st);
+static hipError_t mid_at(const GemmArgs& a, int act_t, int rf, int s, int grid, hipStream_t st) {
+  if (act_t == kActF16) return mid_rf<BITS, GPT, ASYM, kActF16>(a, rf, s, grid, st);
+  if (act_t == kActBF16) return mid_rf<BITS, GPT, ASYM, kActBF16>(a, rf, s, grid, st);
+  return mid_rf<BITS, GPT, ASYM, kActF32>(a, rf, s, grid, st);
 }
 
-hipError_t launch_gemm_mid(const GemmArgs& a, int bits, int gpt, int act_t, int rf, int grid, hipStream_t st) {
+hipError_t launch_gemm_mid(const GemmArgs& a, int bits, int gpt, int act_t, int rf, int s, int grid, hipStream_t st) {
   const bool asym = a.w.zps != nullptr;
   if (bits == 4) {
-    if (gpt == 1) return asym ? mid_at<4, 1, true>(a, act_t, rf, grid, st) : mid_at<4, 1, false>(a, act_t, rf, grid, st);
-    if (gpt == 2) return asym ? mid_at<4, 2, true>(a, act_t, rf, grid, st) : mid_at<4, 2, false>(a, act_t, rf, grid, st);
-    return asym ? mid_at<4, 4, true>(a, act_t, rf, grid, st) : mid_at<4, 4, false>(a, act_t, rf, grid, st);
+    if (gpt == 1)
+      return asym ? mid_at<4, 1, true>(a, act_t, rf, s, grid, st) : mid_at<4, 1, false>(a, act_t, rf, s, grid, st);
+    if (gpt == 2)
+      return asym ? mid_at<4, 2, true>(a, act_t, rf, s, grid, st) : mid_at<4, 2, false>(a, act_t, rf, s, grid, st);
+    return asym ? mid_at<4, 4, true>(a, act_t, rf, s, grid, st) : mid_at<4, 4, false>(a, act_t, rf, s, grid, st);
   }
-  if (gpt == 1) return asym ? mid_at<2, 1, true>(a, act_t, rf, grid, st) : mid_at<2, 1, false>(a, act_t, rf, grid, st);
-  if (gpt == 2) return asym ? mid_at<2, 2, true>(a, act_t, rf, grid, st) : mid_at<2, 2, false>(a, act_t, rf, grid, st);
-  return asym ? mid_at<2, 4, true>(a, act_t, rf, grid, st) : mid_at<2, 4, false>(a, act_t, rf, grid, st);
+  if (gpt == 1) return asym ? mid_at<2, 1, true>(a, act_t, rf, s, grid, st) : mid_at<2, 1, false>(a, act_t, rf, s, grid, st);
+  if (gpt == 2) return asym ? mid_at<2, 2, true>(a, act_t, rf, s, grid, st) : mid_at<2, 2, false>(a, act_t, rf, s, grid, st);
+  return asym ? mid_at<2, 4, true>(a, act_t, rf, s, grid, st) : mid_at<2, 4, false>(a, act_t, rf, s, grid, st);
 }
 
 }  // namespace nad

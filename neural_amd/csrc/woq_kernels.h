@@ -89,6 +89,7 @@ struct GemmArgs {
   int tpg_shift;        // mid-M kernel, one group per K tile or more: log2(K tiles per group) (31: one group)
   int xcd_sg;           // mid-M kernel + its reduce: > 0 = the stripe-group count; the runs of stripe group sg on XCD
                         // sg % 8 (whole rounds of 8 groups), and the reduce workgroups that sum them there too
+  int xcd_w;            // ... the stripe group's width in float4 (S stripes x 4)
   int xcd_tile;         // gemm7 split-K: > 0 = its tile height; XCD x runs every K run of tiles [x T/8, (x+1) T/8) (T tiles,
                         // a multiple of 8), and the reduce workgroups of those tiles run there too
   SkinnyWeight w;
@@ -207,9 +208,9 @@ bool gemm7_ok(int bits, int blocksize, int fold_ok);
 hipError_t launch_gemm7(const GemmArgs& a, int bits, int bm, const _Float16* A16, int lda16, hipStream_t stream);
 // mid-M GEMM (woq_gemm_mid.hip, 17 <= M <= 64): int4 / int2, gpt groups per K tile (1, 2, 4), rf = ceil(M / 16) row
 // fragments; grid = ceil(ns / S) * a.ksplit for the S of mid_geometry; a.ksplit > 1: launch_splitk_reduce follows
-void mid_geometry(int bits, int gpt, int act_t, int rf, int* s, int* nw, int* spw);
+void mid_geometry(int bits, int gpt, int act_t, int rf, int wide, int* s, int* nw, int* spw);
 int mid_lds_bytes(int rf, int s, int nw);
-hipError_t launch_gemm_mid(const GemmArgs& a, int bits, int gpt, int act_t, int rf, int grid, hipStream_t stream);
+hipError_t launch_gemm_mid(const GemmArgs& a, int bits, int gpt, int act_t, int rf, int s, int grid, hipStream_t stream);
 // sum a.ksplit partials of a split-K gemm3 / gemm4 launch in run order and apply a.epi into a.w.out (woq_gemm2.hip)
 hipError_t launch_splitk_reduce(const GemmArgs& a, hipStream_t stream);
 hipError_t launch_cvt_act(const void* A, int act_t, int lda, int M, int K, int Kp, const int32_t* shuffle,

@@ -233,6 +233,10 @@ def test_plan_forward_kernel_choice():
     r = p(4, 4096, 4096, 128, m=17, act="fp16")
     assert (r["kernel"], r["grid"], r["threads"]) == ("woq_mid_kernel", 256, 256), r
     assert p(4, 11008, 4096, 128, m=32)["ksplit"] == 2      # slabs within the workspace bound: ks x N <= 32768
+    # 8-stripe workgroups where 4-stripe ones would take more than one per CU (M <= 32): 86 x 2 instead of 172 x 2
+    assert p(4, 11008, 4096, 128, m=32)["grid"] == 172
+    assert p(4, 11008, 4096, 128, m=48)["grid"] == 344     # 4 row fragments: 4 stripes only
+    assert p(4, 4096, 4096, 128, m=32)["grid"] == 256
     assert p(4, 32000, 4096, 128, m=32)["ksplit"] == 1
     assert p(2, 4096, 4096, 64, m=33)["kernel"] == "woq_gemm7_kernel"   # int2 past 32 rows: the prefill GEMM
     r = p(4, 4096, 4096, 128, m=65)

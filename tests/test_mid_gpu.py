@@ -38,6 +38,9 @@ MID_CASES = [
     (28, 448, 1280, 128, S2, F32, False),      # int2 g128, K tail inside a 256-deep tile
     (30, 256, 2048, 256, S2, F16, True),       # int2 g256 asym
     (64, 4096, 11008, 128, S4, F16, False),    # the Llama down shape: 86 K tiles, 11 runs
+    (32, 11008, 4096, 128, S4, F16, False),    # the Llama gate shape: 8-stripe workgroups (172 instead of 344)
+    (24, 9000, 4096, 128, S4, F32, False),     # 8-stripe workgroups, ragged last group (563 stripes), 3 runs
+    (20, 12288, 2048, 64, S4, BF16, True),     # 8-stripe workgroups at g64 asym (2 groups per tile)
 ]
 
 
