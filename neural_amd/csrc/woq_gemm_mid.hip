@@ -356,7 +356,10 @@ static hipError_t mid_go(const GemmArgs& a, int grid, hipStream_t st) {
 void mid_geometry(int bits, int gpt, int act_t, int rf, int wide, int* s, int* nw, int* spw) {
   (void)act_t;
   *nw = 4;
-  if (wide && bits == 4 && rf <= 2 && gpt <= 2) {  // 8 stripes x a 512-deep run: half the activation bytes per column
+  // 8 stripes x a 512-deep run: half the activation bytes per column.  Not at 3 / 4 row fragments: measured 1.1-1.3 us
+  // SLOWER than 4 stripes at M = 33 .. 64, N = 4096 (no spills; the doubled slabs outweigh the halved activation bytes;
+  // profiles/r06_mid_wide_ab.txt)
+  if (wide && bits == 4 && rf <= 2 && gpt <= 2) {
     *s = 8;
     *spw = 1;
     return;
