@@ -302,6 +302,7 @@ SPLITK_CASES = [
     (100, 1024, 11008, 128, True, "bf16"),    # down-like K = 86 tiles: runs of 3, the last one shorter
     (256, 2048, 4096, 256, False, "fp16"),    # 2 K tiles per group: runs of whole groups
     (512, 1536, 4096, 128, True, "fp16"),     # a TP-8 QKV shard width at a 512-token prefill chunk
+    (96, 1000, 4096, 128, False, "fp16"),     # ragged N (63 stripes, 16 tiles): a tile's runs + their reduce on one XCD
 ]
 
 
@@ -329,8 +330,12 @@ def test_gemm_splitk_parity(oracle, knob, cfg):
     assert _rel_err(y3, ref) <= TOL[act], (_rel_err(y3, ref), act)
 
 
-def test_gemm_splitk_epilogues(oracle):
-    """The split-K reduce applies bias, residual and the FFN's SiLU*mul after summing the runs."""
+@pytest.mark.parametrize("mid", [True, False])
+def test_gemm_splitk_epilogues(oracle, knob, mid):
+    """The split-K reduce applies bias, residual and the FFN's SiLU*mul after summing the runs: the mid-M kernel's
+    (stripe groups on one XCD) and gemm7's (NAD_MID_MAX_M=0: a tile's runs on one XCD, the scale folded)."""
+    if not mid:
+        knob("NAD_MID_MAX_M", "0")
     m, n, k = 48, 1024, 2048
     blob = _blob(oracle, n, k, 128, S4, F16, False, 4, seed=91)
     w = bestla.DeviceWeight(blob)
@@ -338,12 +343,15 @@ def test_gemm_splitk_epilogues(oracle):
     A = rng.uniform(-0.5, 0.5, size=(m, k)).astype(np.float32)
     x = torch.from_numpy(A).cuda()
     ref = oracle.forward(A, blob, n, k).astype(np.float64)
+    plan = w.plan(m, "fp32")
+    assert plan["kernel"] == ("woq_mid_kernel" if mid else "woq_gemm7_kernel") and plan["ksplit"] > 1, plan
+    tol = TOL["fp32"] if mid else FOLD_TOL
     b = rng.uniform(-1, 1, size=(n,)).astype(np.float32)
     r = rng.uniform(-1, 1, size=(m, n)).astype(np.float32)
     y = w.forward(x, epilogue=bestla.EPI_BIAS, bias=torch.from_numpy(b).cuda()).cpu().numpy()
-    assert _rel_err(y, ref + b) <= TOL["fp32"]
+    assert _rel_err(y, ref + b) <= tol
     y = w.forward(x, epilogue=bestla.EPI_RES_ADD, residual=torch.from_numpy(r).cuda()).cpu().numpy()
-    assert _rel_err(y, ref + r) <= TOL["fp32"]
+    assert _rel_err(y, ref + r) <= tol
     fin, fmid, fout = 2048, 1024, 2048
     b1, b3, b2 = (_blob(oracle, nn, kk, 128, S4, F16, False, 4, seed=s)
                   for nn, kk, s in ((fmid, fin, 61), (fmid, fin, 63), (fout, fmid, 62)))
@@ -352,7 +360,7 @@ def test_gemm_splitk_epilogues(oracle):
     h1 = oracle.forward(A, b1, fmid, fin).astype(np.float64)
     h3 = oracle.forward(A, b3, fmid, fin).astype(np.float64)
     ref = oracle.forward((h1 / (1 + np.exp(-h1)) * h3).astype(np.float32), b2, fout, fmid)
-    assert _rel_err(y, ref) <= 2 * TOL["fp32"]
+    assert _rel_err(y, ref) <= 2 * tol
 
 
 SPLITK4_CASES = [

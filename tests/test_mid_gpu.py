@@ -181,3 +181,22 @@ def test_mid_small_m(oracle, knob, m):
     x = _x(m, k, "fp32", m)
     y = w.forward(x).cpu().numpy()
     assert _rel_err(y, oracle.forward(x.cpu().numpy(), blob, n, k)) <= TOL["fp32"]
+
+
+@pytest.mark.parametrize("m,n,mid", [(32, 4096, True), (64, 1000, True), (128, 4096, False), (65, 1000, False)])
+def test_xcd_placement_is_speed_only(oracle, knob, m, n, mid):
+    """The split-K runs of a stripe group (mid-M, NAD_MID_XCD) or of a gemm7 tile (NAD_GEMM_XCD) and the reduce
+    workgroups that sum them placed on one XCD: which workgroup computes which run changes, the run order of the sums
+    does not -- results bit-identical to the round-5 placement, ragged N included."""
+    k = 4096
+    blob = _blob(oracle, n, k, 128, S4, F16, False, 4, seed=m + n)
+    w = bestla.DeviceWeight(blob)
+    plan = w.plan(m, "fp16")
+    assert plan["kernel"] == ("woq_mid_kernel" if mid else "woq_gemm7_kernel") and plan["ksplit"] > 1, plan
+    x = _x(m, k, "fp16", m)
+    y = w.forward(x).cpu().numpy()
+    knob("NAD_MID_XCD", "0")
+    knob("NAD_GEMM_XCD", "0")
+    y0 = w.forward(x).cpu().numpy()
+    assert np.array_equal(y, y0)
+    assert _rel_err(y, oracle.forward(x.float().cpu().numpy(), blob, n, k)) <= (2e-5 if mid else 5e-4)
