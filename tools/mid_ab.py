@@ -1,7 +1,7 @@
 """Mid-M A/B (development tool): bench.py's synthetic cold-rotation graph timing (K = N = 4096 int4 g128, fp16
 activations) per M, alternating runtime knob settings inside one process.
 
-Usage: python tools/mid_ab.py [--m 17,32,48,64] [--rounds 3] [--knob NAD_MID_XCD] [--values 0,1] [--n 4096]
+Usage: python tools/mid_ab.py [--m 17,32,48,64] [--rounds 3] [--knob NAD_MID_XCD] [--values 0,1] [--n 4096] [--act fp16]
 Each line: round, knob value, M, median / min us per launch over the graph replays.
 """
 import argparse
@@ -20,6 +20,7 @@ def main():
     ap.add_argument("--values", default="0,1")
     ap.add_argument("--n", type=int, default=4096)
     ap.add_argument("--copies", type=int, default=128)
+    ap.add_argument("--act", default="fp16", help="activation dtype: fp16, bf16 or fp32")
     args = ap.parse_args()
     import torch
     import bench
@@ -27,7 +28,8 @@ def main():
     K, N = 4096, args.n
     ws = [bestla.DeviceWeight.synthetic(4, N, K, 128, "fp16", False, seed=9000 + i) for i in range(args.copies)]
     gen = torch.Generator(device="cpu").manual_seed(11)
-    xs = {m: (torch.rand((m, K), generator=gen) - 0.5).half().cuda() for m in map(int, args.m.split(","))}
+    dt = {"fp16": torch.float16, "bf16": torch.bfloat16, "fp32": torch.float32}[args.act]
+    xs = {m: (torch.rand((m, K), generator=gen) - 0.5).to(dt).cuda() for m in map(int, args.m.split(","))}
     for r in range(args.rounds):
         for v in args.values.split(","):
             os.environ[args.knob] = v
