@@ -1029,11 +1029,7 @@ static int run_mid(const void* act, int act_t, int lda, int m, int k, const Devi
                    int epi, const float* bias, int bias_ld, const float* res, int ld_res, const float* aux, int ld_aux,
                    hipStream_t st, const A16* pre, const Half16* h16) {
   const Knobs& kn = knobs();
-  // from 12 rows (fp16; 8 for fp32 / bf16, which the GEMV stages as two fp16 rows each) the mid-M kernel beats the
-  // stripe-stream GEMV: K = N = 4096 M = 16 8.3 vs 10.1 us (fp16), 9.0 vs 12.7 (fp32); N = 11008 fp32 M = 16 17.7 vs
-  // 36.7 (profiles/r05_mid_small_m.txt)
-  const int min_m = kn.mid_min_m > 0 ? kn.mid_min_m : (act_t == kActF16 ? 12 : 8);
-  if (m > kn.mid_max_m || m < min_m) return 0;
+  if (m > kn.mid_max_m || m < (kn.mid_min_m > 0 ? kn.mid_min_m : 8)) return 0;
   if ((w.bits != 4 && w.bits != 2) || w.kmajor || w.f4kind >= 0 || w.shuffle) return 0;
   if (w.bits == 2 && m > 32) return 0;  // a 256-deep int2 stage's activation fragments: 32 rows fit the registers
   int tpg = 0;
@@ -1059,6 +1055,11 @@ static int run_mid(const void* act, int act_t, int lda, int m, int k, const Devi
     if (kn.mid_ks > 0) ks = std::max(1, std::min({kn.mid_ks, w.nt, 32768 / ((w.n + 3) / 4 * 4)}));
   };
   plan(kn.mid_wide == 1);
+  // from 8 rows of fp32 / bf16 activations (the GEMV stages them as two fp16 rows each) the mid-M kernel beats the
+  // stripe-stream GEMV: K = N = 4096 M = 16 8.3 vs 10.1 us (fp16), 9.0 vs 12.7 (fp32); N = 11008 fp32 M = 16 17.7 vs
+  // 36.7 (profiles/r05_mid_small_m.txt).  fp16 rows: from 9 where the stripe groups x K runs fit the CUs in one round
+  // (K = N = 4096 M = 10: 7.7 vs 8.7 us), else from 12 (N = 11008 M = 8: GEMV 12.1 vs 14.2; profiles/r06_mid_min_m_ab.txt)
+  if (kn.mid_min_m <= 0 && act_t == kActF16 && m < (nsg * ks <= device_cus() ? 9 : 12)) return 0;
   // 8-stripe workgroups (where mid_geometry has them) when the 4-stripe grid takes more than one workgroup per CU and
   // theirs does not: N = 11008, M = 16 / 32: 344 -> 172 workgroups, 16.3 -> 14.3-14.9 us, 21.1 -> 18.8
   // (profiles/r06_mid_wide_ab.txt); at N = 4096 (256 either way) the 8-stripe form's doubled slabs cost 0.7-1 us

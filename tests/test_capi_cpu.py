@@ -221,6 +221,8 @@ def test_plan_forward_kernel_choice():
     assert p(4, 4096, 4096, 128, m=8, act="fp16")["kernel"] == "woq_gemv_kernel"
     assert p(4, 4096, 4096, 128, m=8)["kernel"] == "woq_mid_kernel"       # fp32 rows: the mid-M kernel from 8
     assert p(4, 4096, 4096, 128, m=12, act="fp16")["kernel"] == "woq_mid_kernel"
+    assert p(4, 4096, 4096, 128, m=9, act="fp16")["kernel"] == "woq_mid_kernel"      # one round of workgroups: from 9
+    assert p(4, 11008, 4096, 128, m=10, act="fp16")["kernel"] == "woq_gemv_kernel"   # 344 workgroups: from 12
     r = p(4, 4096, 4096, 128, m=2048)
     assert (r["kernel"], r["fold"], r["ksplit"]) == ("woq_gemm7_kernel", True, 1)
     assert r["launches"] == 2                       # fp32 activations: one fp16 conversion pass, then the GEMM
