@@ -56,7 +56,7 @@ struct Knobs {
   int compute_int8;
   int gemm2_disable, gemm4_all, gemm4_disable, ffn_f32, gemm_kernel, gemm7_bm, splitk_disable;
   int gemm3_stagger, gemm4_fold_all, gemm4_fold, gemm4_ksw;
-  int mid_min_m, mid_max_m, mid_ks, mid_xcd, mid_wide, gemm_xcd;
+  int mid_min_m, mid_max_m, mid_ks, mid_xcd, mid_wide, gemm_xcd, gemm7_model;
   int host_cache_mb;
 };
 static Knobs read_knobs() {
@@ -84,7 +84,8 @@ static Knobs read_knobs() {
   k.mid_ks = env_int("NAD_MID_KS", 0);         // tests / tuning: its K runs (0 auto)
   k.mid_xcd = env_int("NAD_MID_XCD", 1);       // the runs of a stripe group and their reduce on one XCD (0: off)
   k.mid_wide = env_int("NAD_MID_WIDE", 2);     // mid-M 8-stripe workgroups (M <= 32): 0 never, 1 always, 2 auto
-  k.gemm_xcd = env_int("NAD_GEMM_XCD", 1);     // gemm7 split-K: the runs of a tile and their reduce on one XCD (0: off)
+  k.gemm_xcd = env_int("NAD_GEMM_XCD", 1);
+  k.gemm7_model = env_int("NAD_GEMM7_MODEL", 2);  // gemm7 tile-height model: 2 (round 6 refit), 1 (round 5)     // gemm7 split-K: the runs of a tile and their reduce on one XCD (0: off)
   k.mid_min_m = env_int("NAD_MID_MIN_M", 0);  // ... from this M (0 auto: 12 rows of fp16 activations, 8 of fp32 / bf16)
   k.host_cache_mb = env_int("NAD_HOST_CACHE_MB", 64 * 1024);
   return k;
@@ -1144,7 +1145,11 @@ static int gemm7_pick_bm(const DeviceWeight& w, int m) {
     const int ks = splitk_plan(w, m, &kt, bms[i]);
     const long tiles = long((m + bms[i] - 1) / bms[i]) * ((w.ns + 7) / 8);
     const long rounds = (tiles * ks + cus - 1) / cus;
-    double t = double(rounds) * (fixed_us[i] + double(kt) * hpt * hs_us[i]);
+    // 64-row tiles over the whole K (no split): 7.9 us fixed, refitted on the split-K XCD placement's sweep (K = N =
+    // 4096, M = 320 / 384: 64-row tiles 30.0 / 30.3 us, 128-row tiles with 2 runs 27.3 / 28.2;
+    // profiles/r06_gemm7_tile_height_xcd.txt)
+    const double fx = bms[i] == 64 && ks == 1 && knobs().gemm7_model != 1 ? 7.9 : fixed_us[i];
+    double t = double(rounds) * (fx + double(kt) * hpt * hs_us[i]);
     if (ks > 1) t += 2.0 + double(m) * w.n * ks * 8.0 / 5e6;
     if (t < best_t) {
       best_t = t;
