@@ -353,8 +353,10 @@ REFERENCE_PUBLISHED = {
 
 def cpu_baseline(budget_s=12.0):
     """The oracle's restatement of the reference GEMV (kernel_ref.h:2489-2531, gemv_4bit_fp32_fp32 order), its
-    independent NTILE column blocks spread over the host cores with OpenMP (bit-identical to the scalar oracle), on one
-    decoder layer's shapes + lm_head (int4 g128), repeated for ~budget_s seconds, extrapolated to a 32-layer token."""
+    independent NTILE column blocks spread over the host cores with OpenMP -- AVX-512 where the host has it (within
+    fp32 reassociation, 1e-5 of max|C|, of the scalar oracle; tests/test_oracle_golden.py), else the scalar blocks
+    (bit-identical) -- on one decoder layer's shapes + lm_head (int4 g128), repeated for ~budget_s seconds,
+    extrapolated to a 32-layer token."""
     from tests.oracle_lib import Oracle, S4, F16
     orc = Oracle.get()
     # every host core this process may use: its affinity set, capped by the box's CPU share when the launcher sets
@@ -403,8 +405,8 @@ def cpu_baseline(budget_s=12.0):
             "cores_note": "all CPUs this process may use (affinity), capped by the launcher's CPU share "
                           "(OMP_NUM_THREADS) when set",
             "sample": f"oracle GEMV (kernel_ref.h gemv_4bit_fp32_fp32 order; "
-                      f"{'AVX-512, 16 columns per zmm' if vec else 'scalar code'}, bit-identical to the scalar "
-                      f"restatement; NTILE-48 column blocks over {threads} OpenMP threads) on one decoder layer (QKV "
+                      f"{'AVX-512, 16 columns per zmm, within fp32 reassociation of' if vec else 'scalar code, bit-identical to'} "
+                      f"the scalar restatement; NTILE-48 column blocks over {threads} OpenMP threads) on one decoder layer (QKV "
                       f"12288x4096, O 4096x4096, gate+up 22016x4096, down 4096x11008) + lm_head 32000x4096 int4 g128, "
                       f"{len(times[0])} rounds ({spent:.1f} s of CPU work), median per shape extrapolated to 32 layers "
                       f"+ lm_head per token",
