@@ -56,7 +56,7 @@ struct Knobs {
   int compute_int8;
   int gemm2_disable, gemm4_all, gemm4_disable, ffn_f32, gemm_kernel, gemm7_bm, splitk_disable;
   int gemm3_stagger, gemm4_fold_all, gemm4_fold, gemm4_ksw;
-  int mid_min_m, mid_max_m, mid_ks, mid_xcd, mid_wide, gemm_xcd, gemm7_model;
+  int mid_min_m, mid_max_m, mid_ks, mid_xcd, mid_wide, gemm_xcd, gemm7_model, gemm7_fuse;
   int host_cache_mb;
 };
 static Knobs read_knobs() {
@@ -85,6 +85,7 @@ static Knobs read_knobs() {
   k.mid_xcd = env_int("NAD_MID_XCD", 1);       // the runs of a stripe group and their reduce on one XCD (0: off)
   k.mid_wide = env_int("NAD_MID_WIDE", 2);     // mid-M 8-stripe workgroups (M <= 32): 0 never, 1 always, 2 auto
   k.gemm_xcd = env_int("NAD_GEMM_XCD", 1);
+  k.gemm7_fuse = env_int("NAD_GEMM7_FUSE", 1);    // fused QKV prefill as one gemm7 launch (0: one per weight)
   k.gemm7_model = env_int("NAD_GEMM7_MODEL", 2);  // gemm7 tile-height model: 2 (round 6 refit), 1 (round 5)     // gemm7 split-K: the runs of a tile and their reduce on one XCD (0: off)
   k.mid_min_m = env_int("NAD_MID_MIN_M", 0);  // ... from this M (0 auto: 12 rows of fp16 activations, 8 of fp32 / bf16)
   k.host_cache_mb = env_int("NAD_HOST_CACHE_MB", 64 * 1024);
@@ -1369,6 +1370,60 @@ static bool same_kind(const DeviceWeight& a, const DeviceWeight& b) {
          a.ng == b.ng && (a.shuffle == nullptr) == (b.shuffle == nullptr);
 }
 
+// Fused QKV prefill on gemm7: the weights' column tiles in ONE launch where each weight would run whole-K gemm7 at the
+// same tile height on its own -- the same tiles and arithmetic as the separate launches (bit-identical outputs), one
+// kernel boundary and one tail of output stores instead of n: Llama-2-7B at M = 2048 runs 3 x 256 tiles as 3 rounds of
+// one launch (profiles/r06_gemm7_fused_qkv_ab.txt).  Returns 1 if launched, 0 if not eligible, -1 on error.
+static int run_gemm7_fused(const void* act, int act_t, int lda, int m, int k, const DeviceWeight* const* ws, int n,
+                           float* const* outs, const int* ldos, hipStream_t st, const A16* pre) {
+  const Knobs& kn = knobs();
+  if (n < 2 || n > 3 || !kn.gemm7_fuse || m <= kn.mid_max_m) return 0;
+  int bm0 = 0;
+  for (int i = 0; i < n; i++) {
+    const DeviceWeight& w = *ws[i];
+    if (int8_compute(w) || w.shuffle || pipelined_gemm(w, m) != 3) return 0;
+    if (kn.gemm_kernel != 7 || !kn.gemm4_fold || !gemm7_ok(w.bits, w.blocksize, w.fold_ok)) return 0;
+    if (i > 0 && (!same_kind(w, *ws[0]) || (w.zps == nullptr) != (ws[0]->zps == nullptr))) return 0;
+    int bm = kn.gemm7_bm > 0 ? kn.gemm7_bm : gemm7_pick_bm(w, m);
+    if (bm != 32 && bm != 64 && bm != 128) bm = 256;
+    int kt = w.nt;
+    if (splitk_plan(w, m, &kt, bm) != 1) return 0;  // that weight's own launch splits K: other sums
+    if (i > 0 && bm != bm0) return 0;
+    bm0 = bm;
+  }
+  GemmArgs a{};
+  a.A = act;
+  a.lda = lda;
+  a.M = m;
+  a.K = k;
+  a.scale_t = ws[0]->scale_t;
+  a.epi = kEpiNone;
+  a.vec_ok = vec_aligned(act, lda, act_t) ? 1 : 0;
+  a.fold = 1;
+  a.w = view(*ws[0], outs[0], ldos[0], nullptr, 0);
+  int cut = (ws[0]->ns + 7) / 8;
+  a.nbn_cut[0] = a.nbn_cut[1] = cut;
+  for (int i = 1; i < n; i++) {
+    a.wf[i - 1] = view(*ws[i], outs[i], ldos[i], nullptr, 0);
+    cut += (ws[i]->ns + 7) / 8;
+    if (i == 1) a.nbn_cut[1] = cut;
+  }
+  a.nbn_all = cut;
+  a.nwt = n;
+  if (planned(NAD_KERNEL_GEMM7, ((m + bm0 - 1) / bm0) * cut, 512, 1, 1)) return 1;
+  A16 own;
+  if (!pre || pre->kp != ws[0]->nt * k_tile(*ws[0])) {
+    if (prepare_a16(own, act, act_t, lda, m, k, *ws[0], st) < 0) return -1;
+    pre = &own;
+  }
+  const hipError_t e = launch_gemm7(a, ws[0]->bits, bm0, pre->p, pre->ld, st);
+  if (e != hipSuccess) {
+    set_err("fused gemm7 launch failed: %s", hipGetErrorString(e));
+    return -1;
+  }
+  return 1;
+}
+
 extern "C" int nad_device_qkv_forward(const void* act, int act_dtype, const void* wq, const void* wk, const void* wv,
                                       float* oq, float* okk, float* ov, int m, int k, int lda, int ldo_q, int ldo_k,
                                       int ldo_v, void* queue) {
@@ -1430,6 +1485,10 @@ extern "C" int nad_device_qkv_forward(const void* act, int act_dtype, const void
   if (gemm2_ok(*ws[0], m) && !ws[0]->shuffle && !int8_compute(*ws[0])) {
     if (prepare_a16(pre, act, act_dtype, lda, m, k, *ws[0], st) < 0) return -1;
     pp = &pre;
+  }
+  {
+    const int r = run_gemm7_fused(act, act_dtype, lda, m, k, ws, 3, outs, ldos, st, pp);
+    if (r != 0) return r < 0 ? -1 : 0;
   }
   for (int i = 0; i < 3; i++) {
     const DeviceWeight& w = *ws[i];

@@ -287,8 +287,8 @@ __device__ __forceinline__ float gelu_f(float x) {
 
 // Prefill epilogue of four consecutive outputs (row, n0 .. n0 + 3) of a gemm3 / gemm4 / split-K reduce: the fused op,
 // then the store -- fp32 into w.out, or fp16 (RNE) into out16 when the FFN keeps its intermediates in fp16.
-__device__ __forceinline__ void gemm_epilogue4(const GemmArgs& a, int row, int n0, float (&v)[4]) {
-  const SkinnyWeight& W = a.w;
+// W: the weight whose output this is (a.w, or one of gemm7's fused weights)
+__device__ __forceinline__ void gemm_epilogue4(const GemmArgs& a, const SkinnyWeight& W, int row, int n0, float (&v)[4]) {
 #pragma unroll
   for (int e = 0; e < 4; e++) {
     const int n = n0 + e;
@@ -337,6 +337,9 @@ __device__ __forceinline__ void gemm_epilogue4(const GemmArgs& a, int row, int n
     for (int e = 0; e < 4; e++)
       if (n0 + e < W.n) o[e] = v[e];
   }
+}
+__device__ __forceinline__ void gemm_epilogue4(const GemmArgs& a, int row, int n0, float (&v)[4]) {
+  gemm_epilogue4(a, a.w, row, n0, v);
 }
 
 }  // namespace nad

@@ -209,15 +209,14 @@ __global__ __launch_bounds__(512, 1) void woq_gemm7_kernel(GemmArgs a, const _Fl
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));
   const int wn = wave & 3, wk = wave >> 2;
-  const SkinnyWeight& W = a.w;
-  const int M = a.M, nt = W.nt, ng = W.ng, ns = W.ns;
+  const int M = a.M, nt = a.w.nt, ng = a.w.ng;  // the K side: shared by fused weights
   // tile mode: K tiles per group (2^tsh); half-step mode: half steps per group (2^tsh, groups of 64 up)
-  const int tpg = HS ? (W.bs >= 64 ? W.bs / 64 : 1) : (W.bs >= KT ? W.bs / KT : 1);
+  const int tpg = HS ? (a.w.bs >= 64 ? a.w.bs / 64 : 1) : (a.w.bs >= KT ? a.w.bs / KT : 1);
   const int tsh = __builtin_ctz(unsigned(tpg));
 
   // XCD-aware remap (one XCD walks the N tiles of one (M tile, K run)) and split-K runs, as gemm3
   const int nbm = (M + BMT - 1) / BMT;
-  const int nbn = (ns + NS - 1) / NS;
+  const int nbn = a.nwt > 1 ? a.nbn_all : (a.w.ns + NS - 1) / NS;
   const int ntile = nbm * nbn;
   const int nsplit = a.ksplit > 1 ? a.ksplit : 1;
   const int nwg = ntile * nsplit;
@@ -236,7 +235,12 @@ __global__ __launch_bounds__(512, 1) void woq_gemm7_kernel(GemmArgs a, const _Fl
   const int ntl = nsplit > 1 ? min(a.ktiles, nt - kt0) : nt;
   const int nh = HPT * ntl;            // half steps of the K run
   const int nh2 = (nh + 1) & ~1;       // the loop's (int8: an odd count ends with one all-zero half step)
-  const int bm = bid / nbn, bn = bid % nbn;
+  const int bm = bid / nbn;
+  // fused weights: column tile of the concatenation -> (weight, its own column tile)
+  const int wi = a.nwt > 1 ? int(bid % nbn >= a.nbn_cut[0]) + int(bid % nbn >= a.nbn_cut[1]) : 0;
+  const int bn = bid % nbn - (wi == 0 ? 0 : a.nbn_cut[wi - 1]);
+  const SkinnyWeight& W = wi == 0 ? a.w : a.wf[wi - 1];
+  const int ns = W.ns;
   const int m0 = bm * BMT;
   const int nl = lane & 15, kq = lane >> 4;
 
@@ -540,7 +544,7 @@ __global__ __launch_bounds__(512, 1) void woq_gemm7_kernel(GemmArgs a, const _Fl
       continue;
     }
     float v[4] = {t.x, t.y, t.z, t.w};
-    gemm_epilogue4(a, row, n0, v);
+    gemm_epilogue4(a, W, row, n0, v);
   }
 }
 
@@ -554,7 +558,7 @@ __global__ __launch_bounds__(512, 1) void woq_gemm7_kernel(GemmArgs a, const _Fl
 
 hipError_t G7_CAT(launch_gemm7_b, G7_BITS)(const GemmArgs& a, int bm, const _Float16* A16, int lda16, hipStream_t st) {
   constexpr int BITS = G7_BITS;
-  const int nbm = (a.M + bm - 1) / bm, nbn = (a.w.ns + g7::NS - 1) / g7::NS;
+  const int nbm = (a.M + bm - 1) / bm, nbn = a.nwt > 1 ? a.nbn_all : (a.w.ns + g7::NS - 1) / g7::NS;
   const dim3 grid(nbm * nbn * (a.ksplit > 1 ? a.ksplit : 1));
   auto go = [&](auto k, int lds, bool& done) -> hipError_t {
     if (!done) {  // opt in to the dynamic LDS once per instantiation

@@ -90,6 +90,12 @@ struct GemmArgs {
   int xcd_sg;           // mid-M kernel + its reduce: > 0 = the stripe-group count; the runs of stripe group sg on XCD
                         // sg % 8 (whole rounds of 8 groups), and the reduce workgroups that sum them there too
   int xcd_w;            // ... the stripe group's width in float4 (S stripes x 4)
+  // gemm7 without split K: nwt = 2 / 3 weights of one format and K in one launch (fused QKV prefill); the column tiles
+  // of weight i follow those of weight i - 1 (nbn_cut: running tile-column counts, nbn_all their total); a.w is weight 0
+  int nwt;
+  int nbn_cut[2];
+  int nbn_all;
+  SkinnyWeight wf[2];
   int xcd_tile;         // gemm7 split-K: > 0 = its tile height; XCD x runs every K run of tiles [x T/8, (x+1) T/8) (T tiles,
                         // a multiple of 8), and the reduce workgroups of those tiles run there too
   SkinnyWeight w;

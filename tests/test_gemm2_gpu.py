@@ -135,6 +135,26 @@ def test_gemm_fused_qkv_and_ffn(oracle, m):
     assert _rel_err(y, ref) <= 2 * TOL["fp32"]
 
 
+@pytest.mark.parametrize("m,ns,asym", [(2048, (4096, 4096, 4096), False), (1500, (4096, 3072, 3072), True)])
+def test_gemm7_fused_qkv_is_the_separate_launches(oracle, knob, m, ns, asym):
+    """Fused QKV prefill where each weight runs whole-K gemm7 at one tile height: ONE launch over the weights' column
+    tiles (NAD_GEMM7_FUSE) -- bit-identical to one launch per weight, ragged row tiles and unequal N included; against
+    the oracle on sampled rows at the fold bar."""
+    k = 4096
+    blobs = [_blob(oracle, n, k, 128, S4, BF16 if asym else F16, asym, 4, seed=70 + i) for i, n in enumerate(ns)]
+    ws = [bestla.DeviceWeight(b) for b in blobs]
+    x = (torch.rand((m, k), device="cuda") - 0.5)
+    ys = [y.cpu().numpy() for y in bestla.qkv_forward(x, *ws)]
+    knob("NAD_GEMM7_FUSE", "0")
+    y0 = [y.cpu().numpy() for y in bestla.qkv_forward(x, *ws)]
+    for a, b in zip(ys, y0):
+        assert np.array_equal(a, b)
+    rows = np.random.default_rng(m).choice(m, size=8, replace=False)
+    A = x.cpu().numpy()[rows]
+    for y, b, n in zip(ys, blobs, ns):
+        assert _rel_err(y[rows], oracle.forward(A, b, n, k)) <= FOLD_TOL
+
+
 GEMM4_CASES = [
     # m, n, k, bs, qtype, stype, asym, comp  -- gemm4 (woq_gemm4.hip): int4 g32 / g64, int2 groups >= 64, int8
     (64, 128, 512, 32, S4, F16, False, 4),        # int4 g32 (the reference Python default group)
