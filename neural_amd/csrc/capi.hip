@@ -1378,6 +1378,8 @@ static int run_gemm7_fused(const void* act, int act_t, int lda, int m, int k, co
                            float* const* outs, const int* ldos, hipStream_t st, const A16* pre) {
   const Knobs& kn = knobs();
   if (n < 2 || n > 3 || !kn.gemm7_fuse || m <= kn.mid_max_m) return 0;
+  // the fused instantiation (woq_gemm7_kernel<..., MW>): int4, one group per K tile or more
+  if (ws[0]->bits != 4 || ws[0]->blocksize % 128 != 0) return 0;
   int bm0 = 0;
   for (int i = 0; i < n; i++) {
     const DeviceWeight& w = *ws[i];
@@ -1388,7 +1390,7 @@ static int run_gemm7_fused(const void* act, int act_t, int lda, int m, int k, co
     if (bm != 32 && bm != 64 && bm != 128) bm = 256;
     int kt = w.nt;
     if (splitk_plan(w, m, &kt, bm) != 1) return 0;  // that weight's own launch splits K: other sums
-    if (i > 0 && bm != bm0) return 0;
+    if (bm == 32 || (i > 0 && bm != bm0)) return 0;
     bm0 = bm;
   }
   GemmArgs a{};

@@ -197,7 +197,10 @@ __device__ __forceinline__ h8_t dequant2_fold(uint32_t x, const Dq2c& q, h2_t sc
 // every M-wave) 3-35 % slower than this one (profiles/r05_gemm8_tile_shapes_sweep.txt).  BMT < 256 serves 17 <= M <= 256
 // with split-K runs (the mid-M range): the tile's rows are what the problem has, not 256 rows of which most re-read the
 // last one.
-template <int BITS, int BMT, bool ASYM, int ST, int GPT>
+// MW: several weights in one launch (fused QKV prefill, GemmArgs::nwt; int4 groups of 128 * 2^j, whole K) -- a
+// separate instantiation, so the single-weight kernel keeps its code (the runtime selection in it cost 2-4 %,
+// profiles/r06_gemm7_fused_qkv_ab.txt)
+template <int BITS, int BMT, bool ASYM, int ST, int GPT, bool MW = false>
 __global__ __launch_bounds__(512, 1) void woq_gemm7_kernel(GemmArgs a, const _Float16* __restrict__ A16, int lda16) {
   using BB = Bbuf<BITS, GPT, ST, ASYM>;
   using G = Geo<BMT, BB>;
@@ -216,7 +219,7 @@ __global__ __launch_bounds__(512, 1) void woq_gemm7_kernel(GemmArgs a, const _Fl
 
   // XCD-aware remap (one XCD walks the N tiles of one (M tile, K run)) and split-K runs, as gemm3
   const int nbm = (M + BMT - 1) / BMT;
-  const int nbn = a.nwt > 1 ? a.nbn_all : (a.w.ns + NS - 1) / NS;
+  const int nbn = MW ? a.nbn_all : (a.w.ns + NS - 1) / NS;
   const int ntile = nbm * nbn;
   const int nsplit = a.ksplit > 1 ? a.ksplit : 1;
   const int nwg = ntile * nsplit;
@@ -237,9 +240,9 @@ __global__ __launch_bounds__(512, 1) void woq_gemm7_kernel(GemmArgs a, const _Fl
   const int nh2 = (nh + 1) & ~1;       // the loop's (int8: an odd count ends with one all-zero half step)
   const int bm = bid / nbn;
   // fused weights: column tile of the concatenation -> (weight, its own column tile)
-  const int wi = a.nwt > 1 ? int(bid % nbn >= a.nbn_cut[0]) + int(bid % nbn >= a.nbn_cut[1]) : 0;
-  const int bn = bid % nbn - (wi == 0 ? 0 : a.nbn_cut[wi - 1]);
-  const SkinnyWeight& W = wi == 0 ? a.w : a.wf[wi - 1];
+  const int wi = MW ? int(bid % nbn >= a.nbn_cut[0]) + int(bid % nbn >= a.nbn_cut[1]) : 0;
+  const int bn = bid % nbn - (MW && wi != 0 ? a.nbn_cut[wi - 1] : 0);
+  const SkinnyWeight& W = MW && wi != 0 ? a.wf[wi - 1] : a.w;
   const int ns = W.ns;
   const int m0 = bm * BMT;
   const int nl = lane & 15, kq = lane >> 4;
@@ -578,10 +581,16 @@ hipError_t G7_CAT(launch_gemm7_b, G7_BITS)(const GemmArgs& a, int bm, const _Flo
     const bool asym = a.w.zps != nullptr;
     const int gi = gpt == 4 ? 2 : gpt - 1;
     bool& d = attr[gi][asym][a.scale_t];
+    static bool attr_mw[2][3] = {};
     auto sel = [&](auto asc, auto stc, auto gc) {
       constexpr bool AS = decltype(asc)::value;
       constexpr int STT = decltype(stc)::value, GP = decltype(gc)::value;
-      return go(g7::woq_gemm7_kernel<BITS, BMT, AS, STT, GP>, g7::Geo<BMT, g7::Bbuf<BITS, GP, STT, AS>>::LDS, d);
+      constexpr int LDS = g7::Geo<BMT, g7::Bbuf<BITS, GP, STT, AS>>::LDS;
+      if constexpr (BITS == 4 && GP == 1 && BMT >= 64) {
+        if (a.nwt > 1) return go(g7::woq_gemm7_kernel<BITS, BMT, AS, STT, GP, true>, LDS, attr_mw[AS][a.scale_t]);
+      }
+      if (a.nwt > 1) return hipErrorInvalidValue;  // fused weights: int4 g128 * 2^j, 64-256-row tiles only
+      return go(g7::woq_gemm7_kernel<BITS, BMT, AS, STT, GP>, LDS, d);
     };
     auto by_gpt = [&](auto asc, auto stc) {
       if constexpr (BITS == 4) {
