@@ -84,10 +84,11 @@ static Knobs read_knobs() {
   k.mid_ks = env_int("NAD_MID_KS", 0);         // tests / tuning: its K runs (0 auto)
   k.mid_xcd = env_int("NAD_MID_XCD", 1);       // the runs of a stripe group and their reduce on one XCD (0: off)
   k.mid_wide = env_int("NAD_MID_WIDE", 2);     // mid-M 8-stripe workgroups (M <= 32): 0 never, 1 always, 2 auto
-  k.gemm_xcd = env_int("NAD_GEMM_XCD", 1);
+  k.gemm_xcd = env_int("NAD_GEMM_XCD", 1);        // gemm7 split-K: the runs of a tile and their reduce on one XCD (0: off)
   k.gemm7_fuse = env_int("NAD_GEMM7_FUSE", 1);    // fused QKV prefill as one gemm7 launch (0: one per weight)
-  k.gemm7_model = env_int("NAD_GEMM7_MODEL", 2);  // gemm7 tile-height model: 2 (round 6 refit), 1 (round 5)     // gemm7 split-K: the runs of a tile and their reduce on one XCD (0: off)
-  k.mid_min_m = env_int("NAD_MID_MIN_M", 0);  // ... from this M (0 auto: 12 rows of fp16 activations, 8 of fp32 / bf16)
+  k.gemm7_model = env_int("NAD_GEMM7_MODEL", 2);  // gemm7 tile-height model: 2 (round 6 refit), 1 (round 5)
+  // mid-M from this M (0 auto: fp16 rows from 9 where its grid fits the CUs in one round, else 12; fp32 / bf16 from 8)
+  k.mid_min_m = env_int("NAD_MID_MIN_M", 0);
   k.host_cache_mb = env_int("NAD_HOST_CACHE_MB", 64 * 1024);
   return k;
 }
