@@ -34,7 +34,7 @@ from neural_amd import _lib, bestla  # noqa: E402
 G = int(os.environ.get("SWEEP_GROUP", "128"))  # quantization group of the synthetic weights
 BITS = int(os.environ.get("SWEEP_BITS", "4"))  # weight bits (4, or 2 for the Mistral int2 policy)
 SHAPES = {  # name: (n, k, weights per launch)
-    "qkv": (4096, 4096, 3), "o": (4096, 4096, 1), "gate_up": (11008, 4096, 2), "down": (4096, 11008, 1),
+    "qkv": (4096, 4096, 3), "o": (4096, 4096, 1), "gate_up": (11008, 4096, 2), "down": (4096, 11008, 1), "down14": (4096, 14336, 1),
     "lm_head": (32000, 4096, 1)}
 
 
@@ -55,7 +55,7 @@ def set_env(cfg):
 
 def main():
     dev = torch.device("cuda")
-    x = torch.empty((1, 11008), device=dev).uniform_(-1, 1)
+    x = torch.empty((1, 16384), device=dev).uniform_(-1, 1)
     configs = args.configs or ["base"]
     L = _lib.lib()
     if args.trace:
