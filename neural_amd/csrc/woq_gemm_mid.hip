@@ -349,12 +349,12 @@ static hipError_t mid_go(const GemmArgs& a, int grid, hipStream_t st) {
   return hipGetLastError();
 }
 
-// Geometry per format: 4 stripes per workgroup, 4 waves (one per SIMD: a stage's raw fp32 activation rows, hi / lo
-// fragments and 64 accumulators need more than two waves' register budget); int4 2 stages (K tiles) per wave, 1 for
-// groups finer than a tile at M > 32 (their scale / zero-point registers); int2 (256-deep tiles, 8 steps of activation
-// fragments per stage) 1.  Not taken: int2 at M > 32, int4 with 4 groups per tile (g32) at M > 32.
+// Geometry per format: 4 stripes per workgroup; int4 with one group per K tile or more: 8 waves x 1 stage (K tile)
+// each (round 6), except fp32 rows at M > 48, whose raw rows, hi / lo fragments and 64 accumulators need more than two
+// waves' register budget: 4 waves (one per SIMD) x 2 stages; groups finer than a tile: 4 waves x 2 stages, 1 at M > 32
+// (their scale / zero-point registers); int2 (256-deep tiles, 8 steps of activation fragments per stage) 4 x 1.  Not
+// taken: int2 at M > 32, int4 with 4 groups per tile (g32) at M > 32.
 void mid_geometry(int bits, int gpt, int act_t, int rf, int wide, int* s, int* nw, int* spw) {
-  (void)act_t;
   *nw = 4;
   // 8 stripes x a 512-deep run: half the activation bytes per column.  Not at 3 / 4 row fragments: measured 1.1-1.3 us
   // SLOWER than 4 stripes at M = 33 .. 64, N = 4096 (no spills; the doubled slabs outweigh the halved activation bytes;
@@ -365,6 +365,15 @@ void mid_geometry(int bits, int gpt, int act_t, int rf, int wide, int* s, int* n
     return;
   }
   *s = 4;
+  // int4 with one group per K tile or more: 8 waves x 1 stage -- the same 8-tile chunk as 4 waves x 2 stages, the
+  // loads and the dequant / MFMA of a chunk spread over two waves per SIMD (fp16 rows M = 12 / 32 / 64 7.71 / 9.44 /
+  // 12.62 -> 7.65 / 9.22 / 12.12 us; fp32 M = 48 15.2 -> 13.8; profiles/r06_mid_8waves_ab.txt); not for fp32 rows at
+  // 4 row fragments (their hi / lo stage spills at two waves per SIMD: 19.2 -> 20.0 us)
+  if (bits == 4 && gpt == 1 && !(act_t == kActF32 && rf == 4)) {
+    *nw = 8;
+    *spw = 1;
+    return;
+  }
   *spw = bits == 4 && (rf <= 2 || gpt == 1) ? 2 : 1;
 }
 
@@ -378,6 +387,20 @@ static hipError_t mid_rf(const GemmArgs& a, int rf, int s, int grid, hipStream_t
                        : mid_go<BITS, GPT, ASYM, AT, 2, 8, 4, 1>(a, grid, st);
     }
     if (s != 4) return hipErrorInvalidValue;
+    if constexpr (GPT == 1) {  // 8 waves x 1 stage (mid_geometry)
+      if (!(AT == kActF32 && rf == 4)) {
+        switch (rf) {
+          case 1:
+            return mid_go<BITS, GPT, ASYM, AT, 1, 4, 8, 1>(a, grid, st);
+          case 2:
+            return mid_go<BITS, GPT, ASYM, AT, 2, 4, 8, 1>(a, grid, st);
+          case 3:
+            return mid_go<BITS, GPT, ASYM, AT, 3, 4, 8, 1>(a, grid, st);
+          default:
+            return mid_go<BITS, GPT, ASYM, AT, 4, 4, 8, 1>(a, grid, st);
+        }
+      }
+    }
     switch (rf) {
       case 1:
         return mid_go<BITS, GPT, ASYM, AT, 1, 4, 4, 2>(a, grid, st);

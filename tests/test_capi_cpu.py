@@ -233,7 +233,9 @@ def test_plan_forward_kernel_choice():
     r = p(4, 4096, 4096, 128, m=64)                 # mid-M: fp32 activations read as they are, + the split-K reduce
     assert (r["kernel"], r["fold"], r["ksplit"], r["launches"]) == ("woq_mid_kernel", False, 4, 2), r
     r = p(4, 4096, 4096, 128, m=17, act="fp16")
-    assert (r["kernel"], r["grid"], r["threads"]) == ("woq_mid_kernel", 256, 256), r
+    assert (r["kernel"], r["grid"], r["threads"]) == ("woq_mid_kernel", 256, 512), r   # 8 waves x 1 stage (int4 g128)
+    r = p(4, 4096, 4096, 128, m=64)                 # fp32 rows at 4 row fragments: 4 waves x 2 stages (registers)
+    assert (r["kernel"], r["threads"]) == ("woq_mid_kernel", 256), r
     assert p(4, 11008, 4096, 128, m=32)["ksplit"] == 2      # slabs within the workspace bound: ks x N <= 32768
     # 8-stripe workgroups where 4-stripe ones would take more than one per CU (M <= 32): 86 x 2 instead of 172 x 2
     assert p(4, 11008, 4096, 128, m=32)["grid"] == 172
