@@ -350,10 +350,10 @@ static hipError_t mid_go(const GemmArgs& a, int grid, hipStream_t st) {
 }
 
 // Geometry per format: 4 stripes per workgroup; int4 with one group per K tile or more: 8 waves x 1 stage (K tile)
-// each (round 6), except fp32 rows at M > 48, whose raw rows, hi / lo fragments and 64 accumulators need more than two
-// waves' register budget: 4 waves (one per SIMD) x 2 stages; groups finer than a tile: 4 waves x 2 stages, 1 at M > 32
-// (their scale / zero-point registers); int2 (256-deep tiles, 8 steps of activation fragments per stage) 4 x 1.  Not
-// taken: int2 at M > 32, int4 with 4 groups per tile (g32) at M > 32.
+// each (round 6), except fp32 / bf16 rows at M > 48, whose raw rows, hi / lo fragments and 64 accumulators need more
+// than two waves' register budget: 4 waves (one per SIMD) x 2 stages; groups of half a tile: 8 x 1 to M = 32, then 4
+// waves x 1 (their scale / zero-point registers); groups of a quarter tile: 4 waves x 2 stages; int2 (256-deep tiles, 8 steps of activation fragments per stage)
+// 4 x 1.  Not taken: int2 at M > 32, int4 with 4 groups per tile (g32) at M > 32.
 void mid_geometry(int bits, int gpt, int act_t, int rf, int wide, int* s, int* nw, int* spw) {
   *nw = 4;
   // 8 stripes x a 512-deep run: half the activation bytes per column.  Not at 3 / 4 row fragments: measured 1.1-1.3 us
@@ -367,9 +367,16 @@ void mid_geometry(int bits, int gpt, int act_t, int rf, int wide, int* s, int* n
   *s = 4;
   // int4 with one group per K tile or more: 8 waves x 1 stage -- the same 8-tile chunk as 4 waves x 2 stages, the
   // loads and the dequant / MFMA of a chunk spread over two waves per SIMD (fp16 rows M = 12 / 32 / 64 7.71 / 9.44 /
-  // 12.62 -> 7.65 / 9.22 / 12.12 us; fp32 M = 48 15.2 -> 13.8; profiles/r06_mid_8waves_ab.txt); not for fp32 rows at
-  // 4 row fragments (their hi / lo stage spills at two waves per SIMD: 19.2 -> 20.0 us)
-  if (bits == 4 && gpt == 1 && !(act_t == kActF32 && rf == 4)) {
+  // 12.62 -> 7.65 / 9.22 / 12.12 us; fp32 M = 48 15.2 -> 13.8; profiles/r06_mid_8waves_ab.txt); not for fp32 / bf16 rows
+  // at 4 row fragments (their hi / lo stage spills at two waves per SIMD: fp32 M = 64 19.2 -> 20.0 us)
+  // ... and int4 groups of half a tile (g64) at M <= 32 (M = 24 / 32: fp16 9.68 / 9.94 -> 9.29 / 9.64 us, fp32 12.09 /
+  // 12.63 -> 11.23 / 11.73; profiles/r06_mid_8waves_ab.txt; beyond 2 row fragments their scale registers spill)
+  if (bits == 4 && gpt == 2 && rf <= 2) {
+    *nw = 8;
+    *spw = 1;
+    return;
+  }
+  if (bits == 4 && gpt == 1 && (rf <= 3 || act_t == kActF16)) {
     *nw = 8;
     *spw = 1;
     return;
@@ -387,18 +394,14 @@ static hipError_t mid_rf(const GemmArgs& a, int rf, int s, int grid, hipStream_t
                        : mid_go<BITS, GPT, ASYM, AT, 2, 8, 4, 1>(a, grid, st);
     }
     if (s != 4) return hipErrorInvalidValue;
-    if constexpr (GPT == 1) {  // 8 waves x 1 stage (mid_geometry)
-      if (!(AT == kActF32 && rf == 4)) {
-        switch (rf) {
-          case 1:
-            return mid_go<BITS, GPT, ASYM, AT, 1, 4, 8, 1>(a, grid, st);
-          case 2:
-            return mid_go<BITS, GPT, ASYM, AT, 2, 4, 8, 1>(a, grid, st);
-          case 3:
-            return mid_go<BITS, GPT, ASYM, AT, 3, 4, 8, 1>(a, grid, st);
-          default:
-            return mid_go<BITS, GPT, ASYM, AT, 4, 4, 8, 1>(a, grid, st);
-        }
+    if constexpr (GPT <= 2) {  // 8 waves x 1 stage (mid_geometry)
+      if (rf == 1) return mid_go<BITS, GPT, ASYM, AT, 1, 4, 8, 1>(a, grid, st);
+      if (rf == 2) return mid_go<BITS, GPT, ASYM, AT, 2, 4, 8, 1>(a, grid, st);
+    }
+    if constexpr (GPT == 1) {
+      if (rf == 3) return mid_go<BITS, GPT, ASYM, AT, 3, 4, 8, 1>(a, grid, st);
+      if constexpr (AT == kActF16) {  // fp32 / bf16 rows at 4 row fragments: 4 waves (their hi / lo stage spills)
+        if (rf == 4) return mid_go<BITS, GPT, ASYM, AT, 4, 4, 8, 1>(a, grid, st);
       }
     }
     switch (rf) {

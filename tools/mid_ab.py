@@ -21,12 +21,15 @@ def main():
     ap.add_argument("--n", type=int, default=4096)
     ap.add_argument("--copies", type=int, default=128)
     ap.add_argument("--act", default="fp16", help="activation dtype: fp16, bf16 or fp32")
+    ap.add_argument("--group", type=int, default=128)
+    ap.add_argument("--bits", type=int, default=4)
     args = ap.parse_args()
     import torch
     import bench
     from neural_amd import _lib, bestla
     K, N = 4096, args.n
-    ws = [bestla.DeviceWeight.synthetic(4, N, K, 128, "fp16", False, seed=9000 + i) for i in range(args.copies)]
+    ws = [bestla.DeviceWeight.synthetic(args.bits, N, K, args.group, "fp16", False, seed=9000 + i)
+          for i in range(args.copies)]
     gen = torch.Generator(device="cpu").manual_seed(11)
     dt = {"fp16": torch.float16, "bf16": torch.bfloat16, "fp32": torch.float32}[args.act]
     xs = {m: (torch.rand((m, K), generator=gen) - 0.5).to(dt).cuda() for m in map(int, args.m.split(","))}
