@@ -362,6 +362,9 @@ void mid_geometry(int bits, int gpt, int act_t, int rf, int wide, int* s, int* n
   if (wide && bits == 4 && rf <= 2 && gpt <= 2) {
     *s = 8;
     *spw = 1;
+    // 8 waves (measured N = 11008: fp16 M = 16 / 32 14.9 / 18.7 -> 13.1 / 15.6 us, fp32 15.7 / 21.6 -> 15.2 / 19.6;
+    // profiles/r06_mid_8waves_ab.txt), except g64 at 2 row fragments (its scale registers spill)
+    if (gpt == 1 || rf == 1) *nw = 8;
     return;
   }
   *s = 4;
@@ -389,9 +392,11 @@ static hipError_t mid_rf(const GemmArgs& a, int rf, int s, int grid, hipStream_t
   if constexpr (BITS == 4) {
     constexpr int SPW3 = GPT == 1 ? 2 : 1;  // M > 32
     if constexpr (GPT <= 2) {
-      if (s == 8 && rf <= 2)
-        return rf == 1 ? mid_go<BITS, GPT, ASYM, AT, 1, 8, 4, 1>(a, grid, st)
-                       : mid_go<BITS, GPT, ASYM, AT, 2, 8, 4, 1>(a, grid, st);
+      if (s == 8 && rf == 1) return mid_go<BITS, GPT, ASYM, AT, 1, 8, 8, 1>(a, grid, st);
+      if (s == 8 && rf == 2) {
+        if constexpr (GPT == 1) return mid_go<BITS, GPT, ASYM, AT, 2, 8, 8, 1>(a, grid, st);
+        return mid_go<BITS, GPT, ASYM, AT, 2, 8, 4, 1>(a, grid, st);
+      }
     }
     if (s != 4) return hipErrorInvalidValue;
     if constexpr (GPT <= 2) {  // 8 waves x 1 stage (mid_geometry)
